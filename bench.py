@@ -1,0 +1,311 @@
+"""bench.py — device-resident decode throughput of the Vortex canonicalize hot path on MI355X.
+
+Contract:
+  python bench.py --gpus N --steps K --warmup W
+  * one process per GPU (torchrun for N>1; RCCL barrier + MAX over ranks of the timed region);
+  * a "step" = one vxg_canonicalize (the drop-in C-ABI path) of one array whose buffers are
+    already in HBM;
+  * headline workload = BASELINE config C1 (FastLanes BitPacked u32, W=7, 64 Mi values) —
+    the configuration the north-star target (>=70 % of HBM roofline) is quoted on; chunked
+    arrays shard one chunk per GPU, so every rank decodes its own 64 Mi-value chunk
+    (weak scaling, no data-path collective);
+  * `value` = decoded bytes written by ALL ranks / max-over-ranks time (GB/s);
+  * `roofline` = algorithmic bytes (packed read + decoded write) per launch / mean kernel
+    time from HIP events on the decode stream, against 8.0 TB/s;
+  * `cpu_baseline` = the oracle (C restatement of the reference's single-threaded
+    canonicalize) on a bounded sample, rank 0 only;
+  * the other single-GPU configs (C2 ALP f64, C3 Dict->BitPacked u64 chunk shard, C4 FSST)
+    are measured the same way and reported under "encodings".
+Inputs are rotated across several HBM copies so every step reads from HBM, not from the
+256 MiB Infinity Cache.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+METRIC = "decoded GB/s/GPU (device-resident) per encoding; % HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+# ------------------------------------------------------------------------------ inputs
+def make_c1(rng):
+    """C1: 64 Mi u32 uniform in [0,128) -> BitPacked W=7, no patches."""
+    import vortex_amd.encode as E
+    vals = rng.integers(0, 128, 64 << 20, dtype=np.uint32)
+    return E.encode_bitpacked(vals, bit_width=7, allow_patches=False), dict(
+        name="C1", encoding="fastlanes.bitpacked u32 W=7", values=vals.size,
+        read_bytes=vals.size * 7 // 8, write_bytes=vals.nbytes, dtype="u32")
+
+
+def make_c2(rng):
+    """C2: 64 Mi f64 2-decimal prices + 0.1% random exceptions -> ALP->FoR->BitPacked(u64)."""
+    import vortex_amd.encode as E
+    n = 64 << 20
+    vals = np.round(rng.uniform(1, 100000, n) * 100) / 100
+    k = n // 1000
+    vals[rng.choice(n, k, replace=False)] = rng.standard_normal(k) * 1e9
+    arr = E.encode_alp(vals)
+    return arr, dict(name="C2", encoding="vortex.alp(fastlanes.for(fastlanes.bitpacked u64)) f64",
+                     values=n, read_bytes=arr.nbytes(), write_bytes=vals.nbytes, dtype="f64")
+
+
+def make_c3_shard(rng, world: int):
+    """C3: Chunked x256 [Dict(codes=BitPacked u64 W=10, values=Primitive u64[1024])], 128 Mi
+    values in total; this rank's shard is 256/world... capped at 32 chunks per GPU (the
+    8-GPU share) so per-GPU work is fixed (weak scaling)."""
+    import vortex_amd.arrays as A
+    import vortex_amd.encode as E
+    per_chunk = (128 << 20) // 256
+    n_chunks = 32
+    chunks = []
+    for _ in range(n_chunks):
+        dv = rng.integers(0, 2 ** 63, 1024, dtype=np.uint64)
+        codes = (rng.zipf(1.1, per_chunk) - 1) % 1024
+        chunks.append(A.dict_array(A.primitive(dv),
+                                   A.bitpacked(E.bitpack_buffer(codes.astype(np.uint64), 10), "u64", 10, per_chunk)))
+    arr = A.chunked(chunks)
+    return arr, dict(name="C3", encoding="vortex.chunked[vortex.dict(codes=fastlanes.bitpacked u64 W=10)] u64",
+                     values=n_chunks * per_chunk, read_bytes=arr.nbytes(), write_bytes=n_chunks * per_chunk * 8,
+                     dtype="u64", chunks_per_gpu=n_chunks)
+
+
+WORDS = (b"furiously regular deposits sleep carefully final accounts ironic packages blithely "
+         b"quickly express requests pending theodolites slyly even instructions bold foxes "
+         b"unusual asymptotes special platelets silent pinto beans fluffily careful dependencies "
+         b"daring ideas close courts blithe dolphins quiet excuses ruthless warthogs").split()
+
+
+def make_c4(rng):
+    """C4: 6 001 215 synthetic TPC-H l_comment strings (10..43 chars cut from a word stream;
+    dbgen is unavailable offline) -> FSST (codes VarBin i32 offsets FoR/BitPacked, lengths
+    FoR/BitPacked)."""
+    import vortex_amd.encode as E
+    n = 6_001_215
+    lens = rng.integers(10, 44, n)
+    total = int(lens.sum())
+    wl = np.array([len(w) + 1 for w in WORDS])
+    nw = int(total / wl.mean() * 1.1) + 16
+    ids = rng.integers(0, len(WORDS), nw)
+    mat = np.zeros((len(WORDS), wl.max()), dtype=np.uint8)
+    for i, w in enumerate(WORDS):
+        mat[i, : len(w)] = np.frombuffer(w, np.uint8)
+        mat[i, len(w)] = 32
+    rows = mat[ids]
+    keep = np.arange(mat.shape[1])[None, :] < wl[ids][:, None]
+    stream = rows[keep][:total]
+    offs = np.zeros(n + 1, np.int64)
+    np.cumsum(lens, out=offs[1:])
+    arr = E.encode_fsst_from_heap(stream, offs)
+    return arr, dict(name="C4", encoding="vortex.fsst utf8 -> varbinview", values=n,
+                     read_bytes=arr.nbytes(), write_bytes=total + 16 * n, dtype="u8")
+
+
+# ------------------------------------------------------------------------------ timing
+class Workload:
+    def __init__(self, arr, info, ctx, copies: int):
+        import torch
+        import vortex_amd.arrays as A
+        self.info, self.ctx = info, ctx
+        dev = torch.device("cuda", ctx.device)
+        self.trees = [arr.to(dev) for _ in range(copies)]
+        self.keep = []
+        self.nodes = [A.flatten(t, self.keep) for t in self.trees]
+        vb, db = C.c_uint64(), C.c_uint64()
+        V = ctx.lib
+        chk(V.vxg_canonical_size(ctx.handle, C.byref(self.nodes[0]), C.byref(vb), C.byref(db)))
+        self.out = A._lib.VxgCanonical()
+        if arr.dtype == A.DTYPE["PRIMITIVE"]:
+            self.values = torch.empty(vb.value, dtype=torch.uint8, device=dev)
+            self.out.values = self.values.data_ptr()
+        else:
+            self.views = torch.empty(vb.value, dtype=torch.uint8, device=dev)
+            self.data = torch.empty(db.value + 16, dtype=torch.uint8, device=dev)
+            self.out.views, self.out.data = self.views.data_ptr(), self.data.data_ptr()
+        self.i = 0
+
+    def step(self):
+        node = self.nodes[self.i % len(self.nodes)]
+        self.i += 1
+        chk(self.ctx.lib.vxg_canonicalize(self.ctx.handle, C.byref(node), C.byref(self.out),
+                                          self.ctx.stream_ptr()))
+
+
+def chk(st):
+    from vortex_amd import _lib
+    _lib.check(st)
+
+
+def run_workload(wl: Workload, steps: int, warmup: int, dist, rank: int):
+    import torch
+    for _ in range(warmup):
+        wl.step()
+    wl.ctx.sync()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(steps):
+        ev[s][0].record()
+        wl.step()
+        ev[s][1].record()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    wl.ctx.sync()  # surfaces device-side errors (OOB codes, ...)
+    kms = [a.elapsed_time(b) for a, b in ev]
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, float(np.mean(kms)), float(np.median(kms))
+
+
+def pmc_traffic(name: str):
+    """Per-launch HBM bytes of the dominant kernel from committed rocprofv3 PMC summaries
+    (profiles/pmc_traffic.json, written by tools/pmc_traffic.py: FETCH_SIZE*2 + WRITE_SIZE,
+    KiB -> bytes, gfx950 read correction per MI355X_MICROARCH.md §HBM)."""
+    p = ROOT / "profiles" / "pmc_traffic.json"
+    if not p.exists():
+        return None
+    try:
+        d = json.loads(p.read_text())
+        return d.get(name, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_baseline(budget_s: float):
+    """Oracle ("port") C1 decode on one host core: vxo_unpack over the full 64 Mi array, in
+    the reference's structure (per-1024 block unpack, single thread), repeated for ~budget."""
+    from oracle import oracle as O
+    L = O.lib()
+    rng = np.random.default_rng(42)
+    vals = rng.integers(0, 128, 64 << 20, dtype=np.uint32)
+    packed = np.zeros((vals.size // 1024) * 128 * 7, np.uint8)
+    L.vxo_bitpack(O.PT["u32"], 7, O.p(vals), vals.size, O.p(packed))
+    reps, t = 0, 0.0
+    while t < budget_s:
+        out = np.empty_like(vals)  # the reference allocates its output per call
+        t0 = time.perf_counter()
+        rc = L.vxo_unpack(O.PT["u32"], 7, 0, vals.size, O.p(packed), packed.size, O.p(out))
+        t += time.perf_counter() - t0
+        reps += 1
+        assert rc == 0
+    assert np.array_equal(out, vals)
+    gbs = reps * vals.nbytes / t / 1e9
+    return {"value": round(gbs, 3), "unit": "GB/s", "cores": 1, "kind": "port",
+            "sample": f"C1 full array (64 Mi u32, W=7) decoded {reps}x by oracle/vx_oracle.c vxo_unpack "
+                      f"(-O3 -march=native), fresh output per call; {t:.1f}s of CPU time"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workloads", default="c1,c2,c3,c4",
+                    help="comma list; c1 is the headline, others go under 'encodings'")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world != 1:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # noqa: F811
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    import vortex_amd as V
+    ctx = V.Context(local)
+    rng = np.random.default_rng(42 + rank)
+    makers = {"c1": make_c1, "c2": make_c2, "c3": lambda r: make_c3_shard(r, world), "c4": make_c4}
+    copies = {"c1": 4, "c2": 1, "c3": 2, "c4": 1}
+    results = {}
+    for key in [w.strip() for w in args.workloads.split(",") if w.strip()]:
+        t0 = time.perf_counter()
+        arr, info = makers[key](rng)
+        wl = Workload(arr, info, ctx, copies[key])
+        del arr
+        if rank == 0:
+            log(f"[bench] {info['name']}: built in {time.perf_counter() - t0:.1f}s; timing...")
+        steps = args.steps if key == "c1" else max(3, args.steps // 2)
+        elapsed, kmean, kmed = run_workload(wl, steps, args.warmup if key == "c1" else 2, dist, rank)
+        per_step = elapsed / steps
+        algo = info["read_bytes"] + info["write_bytes"]
+        results[key] = dict(info=info, elapsed=elapsed, ms_per_step=per_step * 1e3, kernel_ms_mean=kmean,
+                            kernel_ms_median=kmed, algo_bytes=algo,
+                            value=world * info["write_bytes"] * steps / elapsed / 1e9)
+        del wl
+        torch.cuda.empty_cache()
+
+    if rank == 0:
+        head_key = "c1" if "c1" in results else next(iter(results))
+        h = results[head_key]
+        info = h["info"]
+        achieved = h["algo_bytes"] / (h["kernel_ms_mean"] / 1e3) / 1e9
+        line = {
+            "metric": METRIC,
+            "value": round(h["value"], 2),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(h["ms_per_step"], 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": info["dtype"],
+            "data": "synthetic (seeded; inputs resident in HBM, rotated across copies)",
+            "config": {"workload": f"{info['name']}: {info['encoding']}, {info['values']} values per GPU, "
+                                   f"one chunk per GPU", "values_per_gpu": info["values"],
+                       "parallelism": f"chunk-per-GPU x{world}"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": pmc_traffic("fl_unpack_u32_w7"),
+                         "kernel_ms_mean": round(h["kernel_ms_mean"], 5),
+                         "algorithmic_bytes_per_launch": h["algo_bytes"]},
+            "encodings": {},
+        }
+        for k, r in results.items():
+            i = r["info"]
+            line["encodings"][i["name"]] = {
+                "encoding": i["encoding"], "values_per_gpu": i["values"],
+                "decoded_GBps_total": round(r["value"], 2),
+                "decoded_GBps_per_gpu_kernel": round(i["write_bytes"] / (r["kernel_ms_mean"] / 1e3) / 1e9, 1),
+                "hbm_frac_algorithmic": round(r["algo_bytes"] / (r["kernel_ms_mean"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
+                "kernel_ms_mean": round(r["kernel_ms_mean"], 5), "ms_per_step": round(r["ms_per_step"], 5),
+                "read_bytes": i["read_bytes"], "write_bytes": i["write_bytes"]}
+        if not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,158 @@
+"""Writes tests/golden/kat.json — known-answer vectors taken from the reference's own unit tests.
+
+Every entry cites the reference test it is transcribed from (paths under the reference checkout,
+workspace 0.12.0).  The reference cannot be built or run in this pipeline (no Rust toolchain,
+SURVEY.md §8c), so these literal inputs/expected outputs are what pins the oracle.  Entries whose
+expected output the reference test derives by roundtrip (decode(encode(x)) == x) carry
+"expect": "roundtrip".  Floats are stored as IEEE-754 bit patterns (hex) so they are exact.
+
+Also writes tests/golden/fastlanes_blocks.npz: one 1024-value block per (T, W) packed by the
+oracle.  The FastLanes packed layout is NOT pinned by any reference fixture (the reference's
+tests are roundtrip-only, bitpacking/compress.rs:416-445), so that file is a regression anchor
+for the restatement ("parity unpinned" at the packed-byte level).
+
+Run:  python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import json
+import math
+import struct
+import sys
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+ROOT = HERE.parent.parent
+
+
+def f64bits(x: float) -> str:
+    return struct.pack("<d", x).hex()
+
+
+def f32bits(x: float) -> str:
+    return struct.pack("<f", x).hex()
+
+
+def kats() -> list[dict]:
+    out = []
+    # ---- ALP -----------------------------------------------------------------------------
+    out.append(dict(
+        name="alp_f32_constant_1025", ref="encodings/alp/src/alp/compress.rs:116-132",
+        kind="alp", ptype="f32", values_bits=[f32bits(1.234)] * 1025,
+        expect_e=9, expect_f=6, expect_encoded=[1234] * 1025, expect_patches=[]))
+    out.append(dict(
+        name="alp_f32_nullable", ref="encodings/alp/src/alp/compress.rs:134-148",
+        kind="alp", ptype="f32", values_bits=[f32bits(0.0), f32bits(1.234), f32bits(0.0)],
+        validity=[False, True, False], expect_e=9, expect_f=6, expect_encoded=[0, 1234, 0],
+        expect_patches=[], expect_decoded_bits=[f32bits(0.0), f32bits(1.234), f32bits(0.0)]))
+    out.append(dict(
+        name="alp_f64_patched", ref="encodings/alp/src/alp/compress.rs:151-166",
+        kind="alp", ptype="f64", values_bits=[f64bits(v) for v in (1.234, 2.718, math.pi, 4.0)],
+        expect_e=16, expect_f=13, expect_encoded=[1234, 2718, 1234, 4000],
+        expect_patches=[[2, f64bits(math.pi)]]))
+    out.append(dict(
+        name="alp_f32_close_fractional", ref="encodings/alp/src/alp/compress.rs:194-205",
+        kind="alp", ptype="f32",
+        values_bits=[f32bits(195.26274), f32bits(195.27837), f32bits(-48.815685)],
+        expect="roundtrip"))
+    # ---- BitPacked -------------------------------------------------------------------------
+    out.append(dict(
+        name="bitpacked_u64_w1_patch_max", ref="encodings/fastlanes/src/bitpacking/mod.rs:266-279",
+        kind="bitpacked", ptype="u64", bit_width=1,
+        values=[1, 0, 1, 0, 1, 0, 2 ** 64 - 1], validity=[True, False, True, False, True, False, True],
+        expect_decoded=[1, 0, 1, 0, 1, 0, 2 ** 64 - 1], expect_patches=[[6, 2 ** 64 - 1]]))
+    for n in (125, 1024, 10_000, 10_240):
+        out.append(dict(
+            name=f"bitpacked_u16_w11_roundtrip_{n}", ref="encodings/fastlanes/src/bitpacking/compress.rs:416-445",
+            kind="bitpacked", ptype="u16", bit_width=11, gen="i % 2047", n=n, expect="roundtrip",
+            check_unpack_single=True))
+    out.append(dict(
+        name="bitpacked_best_bit_width", ref="encodings/fastlanes/src/bitpacking/compress.rs:382-392",
+        kind="bit_width_freq", freq=[0, 10, 20, 15, 1, 0, 0, 0], ptype="u8",
+        expect_best=3, expect_min_patchless=4))
+    # ---- FoR -------------------------------------------------------------------------------
+    out.append(dict(
+        name="for_u32_offset_million", ref="encodings/fastlanes/src/for/compress.rs:126-133",
+        kind="for", ptype="u32", gen="1_000_000 + i", n=10_000, expect_reference=1_000_000,
+        expect="roundtrip"))
+    out.append(dict(
+        name="for_u32_shifted", ref="encodings/fastlanes/src/for/compress.rs:135-152",
+        kind="for", ptype="u32", gen="1_000_000 + 1024 * i", n=98, expect_shift_gt=0,
+        expect="roundtrip"))
+    out.append(dict(
+        name="for_i8_overflow", ref="encodings/fastlanes/src/for/compress.rs:154-180",
+        kind="for", ptype="i8", values=list(range(-128, 128)), expect_reference=-128,
+        expect_encoded=list(range(256)), expect="roundtrip"))
+    # ---- Delta -----------------------------------------------------------------------------
+    out.append(dict(
+        name="delta_u32_range", ref="encodings/fastlanes/src/delta/compress.rs:172-176",
+        kind="delta", ptype="u32", gen="i", n=10_000, expect="roundtrip"))
+    out.append(dict(
+        name="delta_u8_overflow", ref="encodings/fastlanes/src/delta/compress.rs:177-184",
+        kind="delta", ptype="u8", gen="i % 255", n=10_000, expect="roundtrip"))
+    # ---- RunEnd ----------------------------------------------------------------------------
+    out.append(dict(
+        name="runend_encode", ref="encodings/runend/src/compress.rs:159-166",
+        kind="runend_encode", ptype="i32", values=[1, 1, 2, 2, 2, 3, 3, 3, 3, 3],
+        expect_ends=[2, 5, 10], expect_values=[1, 2, 3]))
+    out.append(dict(
+        name="runend_decode", ref="encodings/runend/src/compress.rs:168-178",
+        kind="runend_decode", ptype="i32", ends=[2, 5, 10], run_values=[1, 2, 3], offset=0, len=10,
+        expect_decoded=[1, 1, 2, 2, 2, 3, 3, 3, 3, 3]))
+    # ---- Dict / take ------------------------------------------------------------------------
+    out.append(dict(
+        name="dict_encode_primitive", ref="encodings/dict/src/compress.rs:203-209",
+        kind="dict", ptype="i32", values=[1, 1, 3, 3, 3], expect_codes=[0, 0, 1, 1, 1],
+        expect_values=[1, 3]))
+    out.append(dict(
+        name="dict_encode_varbin", ref="encodings/dict/src/compress.rs:239-254",
+        kind="dict_varbin", strings=["hello", "world", "hello", "again", "world"],
+        expect_codes=[0, 1, 0, 2, 1], expect_values=["hello", "world", "again"]))
+    out.append(dict(
+        name="take_primitive", ref="vortex-array/src/array/primitive/compute/take.rs:39-44",
+        kind="take", ptype="i32", values=[1, 2, 3, 4, 5], codes=[0, 0, 4, 2],
+        expect_decoded=[1, 1, 5, 3]))
+    # ---- ZigZag ----------------------------------------------------------------------------
+    out.append(dict(
+        name="zigzag_i64_range", ref="encodings/zigzag/src/compress.rs:66-74",
+        kind="zigzag", ptype="i64", gen="i - 10_000", n=20_000, expect="roundtrip"))
+    # ---- FSST / VarBin -> VarBinView --------------------------------------------------------
+    out.append(dict(
+        name="fsst_three_sentences", ref="encodings/fsst/tests/fsst_tests.rs:19-35,37-60",
+        kind="fsst", strings=[
+            "The Greeks never said that the limit could not he overstepped",
+            "They said it existed and that whoever dared to exceed it was mercilessly struck down",
+            "Nothing in present history can contradict them"],
+        expect="roundtrip"))
+    out.append(dict(
+        name="varbin_to_views_inline_boundary", ref="vortex-array/src/array/varbin/flatten.rs:28-57",
+        kind="views", strings=[None, None, "123456789012", "1234567890123"],
+        expect_inlined=[None, None, True, False]))
+    return out
+
+
+def fastlanes_blocks() -> dict:
+    sys.path.insert(0, str(ROOT))
+    from oracle import oracle as O  # noqa: E402  (test infrastructure)
+    L = O.lib()
+    rng = np.random.default_rng(42)
+    res = {}
+    for T, dt in ((8, np.uint8), (16, np.uint16), (32, np.uint32), (64, np.uint64)):
+        for W in range(T + 1):
+            if W == T:
+                vals = rng.integers(0, np.iinfo(dt).max, 1024, dtype=dt, endpoint=True)
+            else:
+                vals = rng.integers(0, 1 << W, 1024, dtype=np.uint64).astype(dt) if W else np.zeros(1024, dt)
+            packed = np.zeros(max(128 * W, 1), dtype=np.uint8)
+            L.vxo_fl_pack_block(T, W, O.p(vals), O.p(packed))
+            res[f"T{T}_W{W}_values"] = vals
+            res[f"T{T}_W{W}_packed"] = packed[: 128 * W]
+    return res
+
+
+if __name__ == "__main__":
+    (HERE / "kat.json").write_text(json.dumps(kats(), indent=1) + "\n")
+    np.savez_compressed(HERE / "fastlanes_blocks.npz", **fastlanes_blocks())
+    print("wrote kat.json and fastlanes_blocks.npz")

@@ -1,0 +1,234 @@
+"""CPU canonicalize of a vortex_amd Array tree through the oracle (TEST INFRASTRUCTURE).
+
+Walks the same tree the GPU engine receives and decodes it the way the reference does:
+child-first, one materialised buffer per cascade level, patches applied after the level that
+owns them (canonical.rs:353-357 recursion; per-encoding IntoCanonical impls cited below).
+Every arithmetic step is a call into oracle/liboracle.so (vx_oracle.c).
+"""
+from __future__ import annotations
+
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent.parent
+if str(ROOT) not in sys.path:
+    sys.path.insert(0, str(ROOT))
+
+from oracle import oracle as O  # noqa: E402
+from vortex_amd._lib import DTYPE, ENC, VALIDITY  # noqa: E402
+from vortex_amd.arrays import NP_OF_PTYPE, Array, ptype_width, unsigned_of  # noqa: E402
+
+
+def _buf(b) -> np.ndarray:
+    if hasattr(b, "cpu"):
+        return b.cpu().numpy().view(np.uint8)
+    return np.ascontiguousarray(b).view(np.uint8).reshape(-1)
+
+
+def _validity(a: Array):
+    """Bool mask or None (no nulls) following the reference's validity() accessors."""
+    e = a.encoding
+
+    def from_meta(idx):
+        if a.validity in (VALIDITY["NON_NULLABLE"], VALIDITY["ALL_VALID"]):
+            return None
+        if a.validity == VALIDITY["ALL_INVALID"]:
+            return np.zeros(a.len, dtype=bool)
+        v = a.children[idx]
+        bits = _buf(v.buffers[0])
+        off = v.meta.get("first_byte_bit_offset", 0)
+        return np.unpackbits(bits, bitorder="little")[off: off + a.len].astype(bool)
+
+    if e == ENC["PRIMITIVE"]:
+        return from_meta(0)
+    if e == ENC["FL_BITPACKED"]:
+        return from_meta(1 if a.meta["has_patches"] else 0)
+    if e in (ENC["FL_DELTA"], ENC["RUN_END"], ENC["VARBIN"]):
+        return from_meta(2)
+    if e in (ENC["FL_FOR"], ENC["ZIGZAG"], ENC["ALP"], ENC["ALP_RD"]):
+        return _validity(a.children[0])
+    if e == ENC["FSST"]:
+        return _validity(a.children[2])
+    if e == ENC["CONSTANT"]:
+        return np.zeros(a.len, dtype=bool) if a.meta["is_null"] else None
+    if e == ENC["DICT"]:
+        return None
+    if e == ENC["SPARSE"]:
+        if not a.meta["fill_is_null"]:
+            return None
+        m = np.zeros(a.len, dtype=bool)
+        idx = canon(a.children[0])[0].astype(np.int64) - a.meta["indices_offset"]
+        m[idx] = True
+        return m
+    if e == ENC["CHUNKED"]:
+        parts = [_validity(c) for c in a.children[1:]]
+        if all(p is None for p in parts):
+            return None
+        return np.concatenate([np.ones(c.len, bool) if p is None else p
+                               for p, c in zip(parts, a.children[1:])])
+    return None
+
+
+def _patch(out: np.ndarray, sp: Array) -> None:
+    # SparseArray::resolved_indices + PrimitiveArray::patch
+    idx = canon(sp.children[0])[0]
+    vals = np.ascontiguousarray(canon(sp.children[1])[0]).astype(out.dtype, copy=False)
+    ipt = sp.children[0].ptype
+    rc = O.lib().vxo_patch(O.PT[_pt(out)], O.p(out), out.size, O.PT[ipt], O.p(np.ascontiguousarray(idx)),
+                           sp.meta["indices_offset"], O.p(vals), idx.size)
+    if rc != 0:
+        raise IndexError("patch index out of bounds")
+
+
+def _pt(arr: np.ndarray) -> str:
+    for k, v in NP_OF_PTYPE.items():
+        if np.dtype(v) == arr.dtype:
+            return k
+    raise KeyError(arr.dtype)
+
+
+def canon(a: Array):
+    """-> (values ndarray, validity mask|None) for primitives;
+          ((views u8[n,16], heap u8[]), validity) for utf8/binary."""
+    L = O.lib()
+    e = a.encoding
+    if a.dtype in (DTYPE["UTF8"], DTYPE["BINARY"]):
+        return _canon_string(a), _validity(a)
+    dt = NP_OF_PTYPE[a.ptype]
+    val = _validity(a)
+    if e == ENC["PRIMITIVE"]:
+        return _buf(a.buffers[0])[: a.len * np.dtype(dt).itemsize].view(dt).copy(), val
+    if e == ENC["FL_BITPACKED"]:
+        # bitpacking/compress.rs:167-189
+        out = np.zeros(a.len, dtype=NP_OF_PTYPE[unsigned_of(a.ptype)])
+        packed = _buf(a.buffers[0])
+        rc = L.vxo_unpack(O.PT[unsigned_of(a.ptype)], a.meta["bit_width"], a.meta["offset"], a.len,
+                          O.p(packed), packed.size, O.p(out))
+        if rc:
+            raise ValueError("Invalid packed length")
+        out = out.view(dt)
+        if a.meta["has_patches"]:
+            _patch(out, a.children[0])
+        return out, val
+    if e == ENC["FL_FOR"]:
+        # for/compress.rs:86-98
+        child = np.ascontiguousarray(canon(a.children[0])[0]).view(dt).copy()
+        L.vxo_for_decode(O.PT[a.ptype], O.p(child), child.size, a.meta["reference"], a.meta["shift"], O.p(child))
+        return child, val
+    if e == ENC["ZIGZAG"]:
+        child = np.ascontiguousarray(canon(a.children[0])[0])
+        out = np.zeros(a.len, dtype=dt)
+        L.vxo_zigzag_decode(O.PT[a.ptype], O.p(child), child.size, O.p(out))
+        return out, val
+    if e == ENC["ALP"]:
+        # alp/compress.rs:61-96
+        enc = np.ascontiguousarray(canon(a.children[0])[0])
+        out = np.zeros(a.len, dtype=dt)
+        fn = L.vxo_alp_decode_f32 if a.ptype == "f32" else L.vxo_alp_decode_f64
+        fn(O.p(enc), enc.size, a.meta["e"], a.meta["f"], O.p(out))
+        if a.meta["has_patches"]:
+            _patch(out, a.children[1])
+        return out, val
+    if e == ENC["ALP_RD"]:
+        # alp_rd/array.rs:179-235
+        left = np.ascontiguousarray(canon(a.children[0])[0]).astype(np.uint16)
+        right = np.ascontiguousarray(canon(a.children[1])[0])
+        d = np.array(a.meta["dict"], dtype=np.uint16)
+        pos = np.zeros(0, np.uint64)
+        exc = np.zeros(0, np.uint16)
+        if a.meta["has_exceptions"]:
+            sp = a.children[2]
+            pos = (canon(sp.children[0])[0].astype(np.int64) - sp.meta["indices_offset"]).astype(np.uint64)
+            exc = np.ascontiguousarray(canon(sp.children[1])[0]).astype(np.uint16)
+        out = np.zeros(a.len, dtype=dt)
+        fn = L.vxo_alprd_decode_f32 if a.ptype == "f32" else L.vxo_alprd_decode_f64
+        fn(O.p(left), O.p(d), a.meta["right_bit_width"], O.p(right), a.len, O.p(pos), O.p(exc), pos.size, O.p(out))
+        return out, val
+    if e == ENC["DICT"]:
+        values = np.ascontiguousarray(canon(a.children[0])[0])
+        codes = np.ascontiguousarray(canon(a.children[1])[0])
+        out = np.zeros(a.len, dtype=dt)
+        rc = L.vxo_take(values.dtype.itemsize, O.p(values), values.size, O.PT[a.children[1].ptype],
+                        O.p(codes), codes.size, O.p(out))
+        if rc:
+            raise IndexError("take: index out of bounds")
+        return out, val
+    if e == ENC["FL_DELTA"]:
+        bases = np.ascontiguousarray(canon(a.children[0])[0])
+        deltas = np.ascontiguousarray(canon(a.children[1])[0])
+        out = np.zeros(a.len, dtype=dt)
+        rc = L.vxo_delta_decode(O.PT[a.ptype], O.p(bases), bases.size, O.p(deltas), deltas.size,
+                                a.meta["offset"], a.len, O.p(out))
+        if rc:
+            raise ValueError("delta decode failed")
+        return out, val
+    if e == ENC["RUN_END"]:
+        ends = np.ascontiguousarray(canon(a.children[0])[0])
+        values = np.ascontiguousarray(canon(a.children[1])[0])
+        out = np.zeros(a.len, dtype=dt)
+        rc = L.vxo_runend_decode(values.dtype.itemsize, O.p(values), O.PT[a.children[0].ptype], O.p(ends),
+                                 ends.size, a.meta["offset"], a.len, O.p(out))
+        if rc:
+            raise ValueError("runend decode failed")
+        return out, val
+    if e == ENC["SPARSE"]:
+        fill = np.frombuffer(bytes(a.meta["fill"])[: np.dtype(dt).itemsize], dtype=dt)
+        out = np.full(a.len, 0 if a.meta["fill_is_null"] else fill[0], dtype=dt)
+        _patch(out, a)
+        return out, val
+    if e == ENC["CONSTANT"]:
+        sc = np.frombuffer(bytes(a.meta["scalar"])[: np.dtype(dt).itemsize], dtype=dt)
+        return np.full(a.len, 0 if a.meta["is_null"] else sc[0], dtype=dt), val
+    if e == ENC["CHUNKED"]:
+        # chunked/canonical.rs:170-187 pack_primitives
+        parts = [canon(c)[0] for c in a.children[1:]]
+        return (np.concatenate(parts).astype(dt) if parts else np.zeros(0, dt)), val
+    raise NotImplementedError(f"oracle canonicalize for encoding {e}")
+
+
+def _canon_string(a: Array):
+    L = O.lib()
+    e = a.encoding
+    val = _validity(a)
+    vbits = None if val is None else np.packbits(val, bitorder="little")
+    if e == ENC["VARBIN"]:
+        offs = canon(a.children[0])[0].astype(np.int64)
+        heap = np.ascontiguousarray(canon(a.children[1])[0]).astype(np.uint8)
+        views = np.zeros((a.len, 16), dtype=np.uint8)
+        L.vxo_make_views(O.p(heap), O.p(offs), a.len, O.p(vbits) if vbits is not None else None, 0, O.p(views))
+        return views, heap
+    if e == ENC["FSST"]:
+        syms = np.ascontiguousarray(canon(a.children[0])[0]).astype(np.uint64)
+        slen = np.ascontiguousarray(canon(a.children[1])[0]).astype(np.uint8)
+        codes = a.children[2]
+        coffs = np.ascontiguousarray(canon(codes.children[0])[0])
+        cbytes = np.ascontiguousarray(canon(codes.children[1])[0]).astype(np.uint8)
+        lens = np.ascontiguousarray(canon(a.children[3])[0])
+        total = int(lens.astype(np.int64).sum())
+        heap = np.zeros(total + 16, dtype=np.uint8)
+        views = np.zeros((a.len, 16), dtype=np.uint8)
+        import ctypes as C
+        hl = C.c_size_t()
+        rc = L.vxo_fsst_canonicalize(O.p(syms), O.p(slen), O.p(cbytes), O.PT[codes.children[0].ptype], O.p(coffs),
+                                     O.PT[a.children[3].ptype], O.p(lens), a.len,
+                                     O.p(vbits) if vbits is not None else None, O.p(heap), C.byref(hl), O.p(views))
+        if rc:
+            raise ValueError("fsst canonicalize: decoded length mismatch")
+        return views, heap[: hl.value]
+    if e == ENC["DICT"]:
+        (vviews, vheap), _ = canon(a.children[0])
+        codes = canon(a.children[1])[0].astype(np.int64)
+        return vviews[codes], vheap
+    raise NotImplementedError(f"oracle string canonicalize for encoding {e}")
+
+
+def view_bytes(views: np.ndarray, heap: np.ndarray, i: int):
+    """Logical string of view i (None-safe caller) — Appendix C decoding."""
+    v = views[i]
+    n = int(np.frombuffer(v[:4].tobytes(), dtype=np.uint32)[0])
+    if n <= 12:
+        return v[4: 4 + n].tobytes()
+    off = int(np.frombuffer(v[12:16].tobytes(), dtype=np.uint32)[0])
+    return heap[off: off + n].tobytes()

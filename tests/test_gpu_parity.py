@@ -1,0 +1,336 @@
+"""GPU parity: the HIP engine (through the C ABI) against the oracle, bit-exact.
+
+Every case builds a Vortex array tree with the reference encoders, canonicalizes it on the
+MI355X with vxg_canonicalize (or a per-encoding entry point), and compares every output byte
+with the oracle's CPU canonicalize of the same tree (tests/oracle_tree.py) — and with the
+original data (decode(encode(x)) == x).  Floating point is compared as raw bits.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import vortex_amd as V
+import vortex_amd.arrays as A
+import vortex_amd.encode as E
+from oracle_tree import canon, view_bytes
+
+pytestmark = pytest.mark.gpu
+
+UT = {8: np.uint8, 16: np.uint16, 32: np.uint32, 64: np.uint64}
+
+
+def gpu(arr, ctx):
+    import torch
+    dev = arr.to(torch.device("cuda", 0))
+    return V.canonicalize(dev, ctx)
+
+
+def assert_primitive_parity(arr, ctx, expect=None):
+    res = gpu(arr, ctx)
+    got = res.numpy()
+    ref, rvalid = canon(arr)
+    assert got.dtype == ref.dtype and got.size == ref.size
+    assert got.tobytes() == ref.tobytes()
+    if expect is not None:
+        assert got.tobytes() == np.ascontiguousarray(expect).astype(got.dtype).tobytes()
+    gvalid = res.validity_mask()
+    if rvalid is None:
+        assert gvalid is None or gvalid.all()
+    else:
+        assert np.array_equal(gvalid, rvalid)
+    return got
+
+
+def assert_string_parity(arr, ctx, strings=None):
+    res = gpu(arr, ctx)
+    views, heap = res.numpy()
+    (rviews, rheap), rvalid = canon(arr)
+    assert heap.tobytes() == rheap.tobytes()
+    assert views.tobytes() == rviews.tobytes()
+    gvalid = res.validity_mask()
+    if rvalid is None:
+        assert gvalid is None
+    else:
+        assert np.array_equal(gvalid, rvalid)
+    if strings is not None:
+        for i, s in enumerate(strings):
+            if s is not None:
+                assert view_bytes(views, heap, i) == s
+
+
+# ------------------------------------------------------------------ K1 BitPacked
+@pytest.mark.parametrize("T", [8, 16, 32, 64])
+def test_bitunpack_every_width(ctx, T):
+    rng = np.random.default_rng(T)
+    dt = UT[T]
+    n = 3 * 1024 + 17
+    for W in range(T):
+        vals = (rng.integers(0, 1 << W, n, dtype=np.uint64) if W else np.zeros(n, np.uint64)).astype(dt)
+        arr = E.encode_bitpacked(vals, bit_width=W, allow_patches=False)
+        assert_primitive_parity(arr, ctx, vals)
+
+
+@pytest.mark.parametrize("T,W", [(8, 3), (16, 11), (32, 7), (32, 17), (64, 24), (64, 63)])
+@pytest.mark.parametrize("n", [1, 1000, 1024, 1025, 65_535, 1 << 20])
+def test_bitunpack_sizes(ctx, T, W, n):
+    rng = np.random.default_rng(n + W)
+    vals = rng.integers(0, 1 << W, n, dtype=np.uint64).astype(UT[T])
+    assert_primitive_parity(E.encode_bitpacked(vals, bit_width=W, allow_patches=False), ctx, vals)
+
+
+@pytest.mark.parametrize("offset", [1, 3, 511, 1023])
+@pytest.mark.parametrize("T", [8, 32, 64])
+def test_bitunpack_sliced_offset(ctx, offset, T):
+    rng = np.random.default_rng(offset)
+    W = T // 2 - 1
+    vals = rng.integers(0, 1 << W, 5000, dtype=np.uint64).astype(UT[T])
+    assert_primitive_parity(E.encode_bitpacked(vals, bit_width=W, offset=offset), ctx, vals)
+
+
+@pytest.mark.parametrize("T", [8, 16, 32, 64])
+def test_bitunpack_with_patches(ctx, T):
+    rng = np.random.default_rng(11)
+    dt = UT[T]
+    vals = rng.integers(0, 16, 70_000, dtype=np.uint64).astype(dt)
+    vals[rng.choice(vals.size, 700, replace=False)] = np.iinfo(dt).max
+    arr = E.encode_bitpacked(vals)  # best width -> patches, indices BitPacked u64
+    assert arr.meta["has_patches"]
+    assert_primitive_parity(arr, ctx, vals)
+
+
+def test_bitpacked_reference_kat_patch_max(ctx):
+    vals = np.array([1, 0, 1, 0, 1, 0, 2 ** 64 - 1], np.uint64)
+    arr = E.encode_bitpacked(vals, bit_width=1, validity=[True, False, True, False, True, False, True])
+    got = assert_primitive_parity(arr, ctx)
+    assert got.tolist() == [1, 0, 1, 0, 1, 0, 2 ** 64 - 1]
+
+
+def test_signed_bitpacked_reinterpret(ctx):
+    # unpack of a signed ptype reinterpret-casts (bitpacking/compress.rs:179-182)
+    vals = np.arange(0, 3000, dtype=np.int32) % 100
+    arr = E.encode_bitpacked(vals.view(np.uint32), bit_width=7)
+    arr.ptype = "i32"
+    assert_primitive_parity(arr, ctx, vals)
+
+
+# ------------------------------------------------------------------ FoR / ZigZag / ALP
+@pytest.mark.parametrize("dt", [np.int8, np.uint16, np.int32, np.uint32, np.int64, np.uint64])
+def test_for_bitpacked_fused(ctx, dt):
+    rng = np.random.default_rng(5)
+    info = np.iinfo(dt)
+    base = int(info.min) // 2 + 7 if info.min < 0 else 1000
+    vals = (base + 4 * rng.integers(0, 50, 9000)).astype(dt)
+    arr = E.encode_for_bitpacked(vals)
+    assert arr.encoding == A.ENC["FL_FOR"] and arr.meta["shift"] == 2
+    assert_primitive_parity(arr, ctx, vals)
+
+
+def test_for_i8_overflow_kat(ctx):
+    vals = np.arange(-128, 128, dtype=np.int8)
+    assert_primitive_parity(E.encode_for_bitpacked(vals), ctx, vals)
+
+
+def test_for_over_primitive_child(ctx):
+    enc = np.arange(5000, dtype=np.uint32) * 3
+    arr = A.frame_of_reference(A.primitive(enc), 1_000_000, 1, "u32")
+    assert_primitive_parity(arr, ctx)
+
+
+@pytest.mark.parametrize("dt", [np.int8, np.int16, np.int32, np.int64])
+def test_zigzag(ctx, dt):
+    vals = (np.arange(-5000, 5000) % 120 - 60).astype(dt)
+    assert_primitive_parity(E.encode_zigzag(vals), ctx, vals)
+
+
+@pytest.mark.parametrize("n", [3, 1025, 100_000])
+def test_alp_f64_cascade(ctx, n):
+    rng = np.random.default_rng(n)
+    vals = np.round(rng.uniform(1, 100000, n) * 100) / 100
+    if n > 10:
+        vals[rng.choice(n, n // 1000 + 1, replace=False)] = rng.standard_normal(n // 1000 + 1) * 1e9
+    arr = E.encode_alp(vals)
+    got = assert_primitive_parity(arr, ctx)
+    assert got.tobytes() == vals.tobytes()
+
+
+def test_alp_reference_kats_on_gpu(ctx):
+    import math
+    vals = np.array([1.234, 2.718, math.pi, 4.0])
+    arr = E.encode_alp(vals, cascade=False)
+    assert (arr.meta["e"], arr.meta["f"]) == (16, 13)
+    assert assert_primitive_parity(arr, ctx).tobytes() == vals.tobytes()
+    vals32 = np.full(1025, 1.234, np.float32)
+    arr = E.encode_alp(vals32)
+    assert (arr.meta["e"], arr.meta["f"]) == (9, 6)
+    assert assert_primitive_parity(arr, ctx).tobytes() == vals32.tobytes()
+
+
+def test_alp_f32_cascade(ctx):
+    rng = np.random.default_rng(4)
+    vals = (np.round(rng.uniform(-500, 500, 50_000) * 10) / 10).astype(np.float32)
+    assert assert_primitive_parity(E.encode_alp(vals), ctx).tobytes() == vals.tobytes()
+
+
+@pytest.mark.parametrize("ptype", ["f32", "f64"])
+def test_alprd(ctx, ptype):
+    rng = np.random.default_rng(8)
+    vals = (rng.standard_normal(40_000) * 1000).astype(A.NP_OF_PTYPE[ptype])
+    vals[::997] = rng.standard_normal(vals[::997].size).astype(vals.dtype) * 1e30
+    assert assert_primitive_parity(E.encode_alprd(vals), ctx).tobytes() == vals.tobytes()
+
+
+# ------------------------------------------------------------------ Dict / take
+@pytest.mark.parametrize("vdt", [np.uint8, np.int16, np.float32, np.uint64])
+@pytest.mark.parametrize("card", [1, 2, 200, 4000])
+def test_dict_fused(ctx, vdt, card):
+    rng = np.random.default_rng(card)
+    pool = rng.integers(0, 120, card * 2).astype(vdt)
+    pool = np.unique(pool)[:card]
+    vals = pool[rng.integers(0, pool.size, 30_000)]
+    arr = E.encode_dict(vals)
+    assert_primitive_parity(arr, ctx, vals)
+
+
+def test_dict_unpacked_codes_take(ctx):
+    arr = A.dict_array(A.primitive(np.array([1, 2, 3, 4, 5], np.int32)), A.primitive(np.array([0, 0, 4, 2], np.uint64)))
+    assert assert_primitive_parity(arr, ctx).tolist() == [1, 1, 5, 3]
+
+
+def test_take_out_of_bounds_is_an_error(ctx):
+    arr = A.dict_array(A.primitive(np.array([1, 2], np.int32)), A.primitive(np.array([0, 5], np.uint64)))
+    with pytest.raises(V.VortexGpuError) as ei:
+        gpu(arr, ctx)
+    assert ei.value.kind == "OutOfBounds"
+
+
+def test_dict_strings(ctx):
+    strings = [b"hello", b"world", b"hello", b"again", b"world", b"a much longer string value"] * 500
+    codes, _ = E.dict_encode(np.array([hash(s) for s in strings], np.int64))
+    uniq = []
+    for s in strings:
+        if s not in uniq:
+            uniq.append(s)
+    heap, offs, _ = E.strings_to_heap(uniq)
+    values = A.varbin(A.primitive(offs.astype(np.int32)), A.primitive(heap))
+    arr = A.dict_array(values, E.encode_bitpacked(codes, allow_patches=False))
+    assert_string_parity(arr, ctx, strings)
+
+
+# ------------------------------------------------------------------ Delta / RunEnd
+@pytest.mark.parametrize("dt", [np.uint8, np.uint16, np.uint32, np.uint64])
+@pytest.mark.parametrize("n", [1, 1024, 4097, 200_000])
+def test_delta(ctx, dt, n):
+    rng = np.random.default_rng(n)
+    vals = np.cumsum(rng.integers(0, 5, n)).astype(dt)
+    assert_primitive_parity(E.encode_delta(vals), ctx, vals)
+
+
+def test_delta_sliced(ctx):
+    vals = np.cumsum(np.random.default_rng(5).integers(0, 9, 9000)).astype(np.uint32)
+    arr = E.encode_delta(vals)
+    sl = A.delta(arr.children[0], arr.children[1], offset=300, length=7000)
+    assert_primitive_parity(sl, ctx, vals[300:7300])
+
+
+@pytest.mark.parametrize("vdt", [np.int8, np.int32, np.float64])
+def test_runend(ctx, vdt):
+    rng = np.random.default_rng(2)
+    vals = np.repeat(rng.integers(-100, 100, 3000).astype(vdt), rng.integers(1, 40, 3000))
+    arr = E.encode_runend(vals)
+    assert_primitive_parity(arr, ctx, vals)
+    arr.meta["offset"] = 33
+    arr.len = vals.size - 100
+    assert_primitive_parity(arr, ctx, vals[33:33 + arr.len])
+
+
+# ------------------------------------------------------------------ Sparse / Constant / Chunked
+def test_sparse_null_fill_validity(ctx):
+    idx = E.encode_bitpacked(np.array([3, 5, 9, 4000], np.uint64), bit_width=12, allow_patches=False)
+    arr = A.sparse(idx, A.primitive(np.array([7, 8, 9, 10], np.int64)), 5000, fill=None)
+    assert_primitive_parity(arr, ctx)
+
+
+def test_constant(ctx):
+    assert_primitive_parity(A.constant(-3, 10_000, "i16"), ctx, np.full(10_000, -3, np.int16))
+    assert_primitive_parity(A.constant(None, 100, "u32"), ctx)
+
+
+def test_chunked_grouped_dict(ctx):
+    rng = np.random.default_rng(3)
+    chunks, expect = [], []
+    for c in range(12):
+        dv = rng.integers(0, 2 ** 63, 1024, dtype=np.uint64)
+        vals = dv[rng.zipf(1.1, 50_000 + 1024 * (c % 3)) % 1024]
+        codes = E.dict_encode(vals)[0]
+        chunks.append(A.dict_array(A.primitive(E.dict_encode(vals)[1]), E.encode_bitpacked(codes, bit_width=10, allow_patches=False)))
+        expect.append(vals)
+    arr = A.chunked(chunks)
+    assert_primitive_parity(arr, ctx, np.concatenate(expect))
+
+
+def test_chunked_mixed_with_validity(ctx):
+    a = E.encode_bitpacked(np.arange(3000, dtype=np.uint32) % 77, validity=(np.arange(3000) % 5 != 0))
+    b = A.primitive(np.arange(1001, dtype=np.uint32), validity=None)
+    c = E.encode_delta(np.arange(2048, dtype=np.uint32))
+    assert_primitive_parity(A.chunked([a, b, c]), ctx)
+
+
+# ------------------------------------------------------------------ strings: VarBin, FSST
+def test_varbin_views_boundary(ctx):
+    strings = [None, None, b"123456789012", b"1234567890123", b"", b"x" * 100]
+    heap, offs, valid = E.strings_to_heap(strings)
+    arr = A.varbin(A.primitive(offs.astype(np.int32)), A.primitive(heap), validity=valid)
+    assert_string_parity(arr, ctx, strings)
+
+
+@pytest.mark.parametrize("n", [3, 1000, 40_000])
+def test_fsst(ctx, n):
+    rng = np.random.default_rng(n)
+    words = [b"carefully", b"final", b"deposits", b"sleep", b"quickly", b"ironic", b"packages",
+             b"blithely", b"regular", b"accounts", b"\x00\xff", b"furiously"]
+    strings = []
+    for i in range(n):
+        if i % 23 == 7:
+            strings.append(None)
+        else:
+            k = int(rng.integers(1, 7))
+            strings.append(b" ".join(words[j] for j in rng.integers(0, len(words), k)))
+    assert_string_parity(E.encode_fsst(strings), ctx, strings)
+
+
+def test_fsst_long_strings_direct_path(ctx):
+    # strings large enough that a 256-string tile overflows the LDS images
+    rng = np.random.default_rng(1)
+    strings = [bytes(rng.integers(97, 123, int(rng.integers(100, 600))).astype(np.uint8)) for _ in range(700)]
+    assert_string_parity(E.encode_fsst(strings), ctx, strings)
+
+
+# ------------------------------------------------------------------ direct C-ABI entry points
+def test_direct_bitunpack_entry(ctx):
+    import torch
+    lib = V.gpu_lib()
+    vals = (np.arange(1 << 16, dtype=np.uint32) * 2654435761 % 128).astype(np.uint32)
+    packed = E.bitpack_buffer(vals, 7)
+    dp = torch.from_numpy(packed).cuda()
+    out = torch.empty(vals.size * 4, dtype=torch.uint8, device="cuda")
+    st = lib.vxg_bitunpack(ctx.handle, V.PTYPE["u32"], 7, 0, vals.size, C.c_void_p(dp.data_ptr()),
+                           packed.size, C.c_void_p(out.data_ptr()), ctx.stream_ptr())
+    assert st == 0
+    ctx.sync()
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), vals)
+    # wrong packed length is rejected like BitPackedArray::try_new (bitpacking/mod.rs:80-88)
+    st = lib.vxg_bitunpack(ctx.handle, V.PTYPE["u32"], 7, 0, vals.size + 5000, C.c_void_p(dp.data_ptr()),
+                           packed.size, C.c_void_p(out.data_ptr()), ctx.stream_ptr())
+    assert st == 3 and b"packed bytes" in lib.vxg_last_error()
+
+
+def test_full_size_c1_roundtrip(ctx):
+    """BASELINE config 1 at full size (64 Mi u32, W=7): size-independent property checks
+    (exact roundtrip + checksum) on top of a bit-exact oracle comparison."""
+    rng = np.random.default_rng(42)
+    vals = rng.integers(0, 128, 64 << 20, dtype=np.uint32)
+    arr = E.encode_bitpacked(vals, bit_width=7, allow_patches=False)
+    got = gpu(arr, ctx).numpy()
+    assert got.tobytes() == vals.tobytes()
+    assert int(got.astype(np.uint64).sum()) == int(vals.astype(np.uint64).sum())

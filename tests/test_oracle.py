@@ -1,0 +1,354 @@
+"""CPU tests: the oracle against the reference's known-answer vectors and the FastLanes
+invariants, and the product encoders against the oracle."""
+import json
+import math
+import struct
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from oracle_tree import canon, view_bytes
+import vortex_amd.arrays as A
+import vortex_amd.encode as E
+
+GOLD = Path(__file__).resolve().parent / "golden"
+KATS = {k["name"]: k for k in json.loads((GOLD / "kat.json").read_text())}
+L = O.lib()
+UT = {8: np.uint8, 16: np.uint16, 32: np.uint32, 64: np.uint64}
+
+
+def _f(bits_hex, ptype):
+    fmt = "<f" if ptype == "f32" else "<d"
+    return np.array([struct.unpack(fmt, bytes.fromhex(h))[0] for h in bits_hex],
+                    dtype=np.float32 if ptype == "f32" else np.float64)
+
+
+def _gen(k):
+    i = np.arange(k["n"], dtype=np.int64)
+    return eval(k["gen"], {"i": i}).astype(A.NP_OF_PTYPE[k["ptype"]])  # literal from kat.json
+
+
+# ---------------------------------------------------------------- FastLanes invariants
+@pytest.mark.parametrize("T", [8, 16, 32, 64])
+def test_fl_index_is_bijection(T):
+    lanes = 1024 // T
+    idx = {L.vxo_fl_index(T, r, l) for r in range(T) for l in range(lanes)}
+    assert idx == set(range(1024))
+
+
+def test_fl_transpose_is_bijection():
+    assert sorted(L.vxo_fl_transpose(i) for i in range(1024)) == list(range(1024))
+
+
+@pytest.mark.parametrize("T", [8, 16, 32, 64])
+def test_fl_lane_rows_contiguous_after_transpose(T):
+    # invariant 3: transpose(index(row, lane)) over rows is a contiguous ascending run
+    for lane in range(1024 // T):
+        pos = [L.vxo_fl_transpose(L.vxo_fl_index(T, r, lane)) for r in range(T)]
+        assert pos == list(range(pos[0], pos[0] + T))
+
+
+@pytest.mark.parametrize("T", [8, 16, 32, 64])
+def test_fl_pack_unpack_roundtrip_all_widths(T):
+    rng = np.random.default_rng(T)
+    dt = UT[T]
+    for W in range(T + 1):
+        if W == T:
+            vals = rng.integers(0, np.iinfo(dt).max, 1024, dtype=dt, endpoint=True)
+        else:
+            vals = (rng.integers(0, 1 << W, 1024, dtype=np.uint64) if W else np.zeros(1024, np.uint64)).astype(dt)
+        packed = np.zeros(max(128 * W, 16), np.uint8)
+        L.vxo_fl_pack_block(T, W, O.p(vals), O.p(packed))
+        out = np.zeros(1024, dt)
+        L.vxo_fl_unpack_block(T, W, O.p(packed), O.p(out))
+        assert np.array_equal(out, vals), (T, W)
+        # invariant 2: unpack_single == unpack at every position
+        for i in range(0, 1024, 37):
+            assert L.vxo_fl_unpack_single(T, W, O.p(packed), i) == int(vals[i])
+
+
+def test_fastlanes_blocks_fixture_regression():
+    """The committed per-(T,W) blocks must still unpack identically (restatement regression)."""
+    z = np.load(GOLD / "fastlanes_blocks.npz")
+    for T in (8, 16, 32, 64):
+        for W in range(T + 1):
+            vals, packed = z[f"T{T}_W{W}_values"], z[f"T{T}_W{W}_packed"]
+            assert packed.size == 128 * W  # invariant 4
+            out = np.zeros(1024, UT[T])
+            L.vxo_fl_unpack_block(T, W, O.p(packed if packed.size else np.zeros(16, np.uint8)), O.p(out))
+            assert np.array_equal(out, vals)
+
+
+@pytest.mark.parametrize("T", [8, 16, 32, 64])
+def test_product_bitpack_matches_oracle_pack(T):
+    rng = np.random.default_rng(7)
+    dt = UT[T]
+    for W in (1, 3, T // 2, T - 1):
+        vals = (rng.integers(0, 1 << W, 5000, dtype=np.uint64)).astype(dt)
+        ours = E.bitpack_buffer(vals, W)
+        ref = np.zeros(((5000 + 1023) // 1024) * 128 * W, np.uint8)
+        n = L.vxo_bitpack(O.PT[f"u{T}"], W, O.p(vals), vals.size, O.p(ref))
+        assert n == ref.size and np.array_equal(ours, ref)
+
+
+# ---------------------------------------------------------------- reference KATs
+def test_kat_alp_f32_constant():
+    k = KATS["alp_f32_constant_1025"]
+    vals = _f(k["values_bits"], "f32")
+    e, f, enc, idx, pv = E.alp_encode(vals)
+    assert (e, f) == (k["expect_e"], k["expect_f"])
+    assert enc.tolist() == k["expect_encoded"] and idx.size == 0
+    out = np.zeros(vals.size, np.float32)
+    L.vxo_alp_decode_f32(O.p(enc), enc.size, e, f, O.p(out))
+    assert out.tobytes() == vals.tobytes()
+
+
+def test_kat_alp_f32_nullable():
+    k = KATS["alp_f32_nullable"]
+    vals = _f(k["values_bits"], "f32")
+    e, f, enc, idx, pv = E.alp_encode(vals)
+    assert (e, f) == (k["expect_e"], k["expect_f"]) and enc.tolist() == k["expect_encoded"]
+    out = np.zeros(3, np.float32)
+    L.vxo_alp_decode_f32(O.p(enc), 3, e, f, O.p(out))
+    assert out.tobytes() == _f(k["expect_decoded_bits"], "f32").tobytes()
+
+
+def test_kat_alp_f64_patched():
+    k = KATS["alp_f64_patched"]
+    vals = _f(k["values_bits"], "f64")
+    e, f, enc, idx, pv = E.alp_encode(vals)
+    assert (e, f) == (k["expect_e"], k["expect_f"])
+    assert enc.tolist() == k["expect_encoded"]  # fill-forward of the patched slot
+    assert [[int(i), struct.pack("<d", v).hex()] for i, v in zip(idx, pv)] == k["expect_patches"]
+    arr = E.encode_alp(vals, cascade=True)
+    got, _ = canon(arr)
+    assert got.tobytes() == vals.tobytes()
+    # decode_single pinned: 1234 * F10[13] * IF10[16] == 1.234 exactly
+    one = np.zeros(1, np.float64)
+    L.vxo_alp_decode_f64(O.p(np.array([1234], np.int64)), 1, 16, 13, O.p(one))
+    assert one[0] == 1.234
+
+
+def test_kat_alp_f32_close_fractional():
+    vals = _f(KATS["alp_f32_close_fractional"]["values_bits"], "f32")
+    got, _ = canon(E.encode_alp(vals))
+    assert got.tobytes() == vals.tobytes()
+
+
+def test_kat_bitpacked_patch_max():
+    k = KATS["bitpacked_u64_w1_patch_max"]
+    vals = np.array(k["values"], dtype=np.uint64)
+    arr = E.encode_bitpacked(vals, bit_width=k["bit_width"], validity=k["validity"])
+    assert arr.meta["has_patches"]
+    sp = arr.children[0]
+    assert canon(sp.children[0])[0].tolist() == [p[0] for p in k["expect_patches"]]
+    got, valid = canon(arr)
+    assert got.tolist() == k["expect_decoded"]
+    assert valid.tolist() == k["validity"]
+
+
+@pytest.mark.parametrize("n", [125, 1024, 10_000, 10_240])
+def test_kat_bitpacked_u16_w11_roundtrip(n):
+    k = KATS[f"bitpacked_u16_w11_roundtrip_{n}"]
+    vals = _gen(k)
+    arr = E.encode_bitpacked(vals, bit_width=11)
+    assert not arr.meta["has_patches"]
+    got, _ = canon(arr)
+    assert np.array_equal(got, vals)
+    packed = np.asarray(arr.buffers[0])
+    for i in range(0, n, 97):  # unpack_single (compress.rs:441-444)
+        blk = packed[(i // 1024) * 128 * 11:][: 128 * 11]
+        assert L.vxo_fl_unpack_single(16, 11, O.p(blk), i % 1024) == vals[i]
+
+
+def test_kat_best_bit_width():
+    k = KATS["bitpacked_best_bit_width"]
+    freq = k["freq"]
+    vals = np.concatenate([np.full(c, (1 << bw) - 1 if bw else 0, dtype=np.uint8) for bw, c in enumerate(freq)])
+    lib = E._lib_enc()
+    assert lib.vxe_best_bit_width(0, E._p(vals), vals.size) == k["expect_best"]
+    assert lib.vxe_min_patchless_bit_width(0, E._p(vals), vals.size) == k["expect_min_patchless"]
+
+
+def test_kat_for():
+    k = KATS["for_u32_offset_million"]
+    vals = _gen(k)
+    enc, ref, shift = E.for_compress(vals)
+    assert ref == k["expect_reference"]
+    assert np.array_equal(canon(E.encode_for_bitpacked(vals))[0], vals)
+    k = KATS["for_u32_shifted"]
+    vals = _gen(k)
+    enc, ref, shift = E.for_compress(vals)
+    assert shift > 0
+    assert np.array_equal(canon(E.encode_for_bitpacked(vals))[0], vals)
+    k = KATS["for_i8_overflow"]
+    vals = np.array(k["values"], dtype=np.int8)
+    enc, ref, shift = E.for_compress(vals)
+    assert ref == k["expect_reference"] and enc.tolist() == k["expect_encoded"]
+    assert np.array_equal(canon(E.encode_for_bitpacked(vals))[0], vals)
+
+
+@pytest.mark.parametrize("name", ["delta_u32_range", "delta_u8_overflow"])
+def test_kat_delta_roundtrip(name):
+    vals = _gen(KATS[name])
+    assert np.array_equal(canon(E.encode_delta(vals))[0], vals)
+
+
+def test_kat_runend():
+    k = KATS["runend_encode"]
+    ends, rv = E.runend_encode(np.array(k["values"], dtype=np.int32))
+    assert ends.tolist() == k["expect_ends"] and rv.tolist() == k["expect_values"]
+    k = KATS["runend_decode"]
+    arr = A.run_end(A.primitive(np.array(k["ends"], np.int32)), A.primitive(np.array(k["run_values"], np.int32)),
+                    length=k["len"], offset=k["offset"])
+    assert canon(arr)[0].tolist() == k["expect_decoded"]
+
+
+def test_kat_dict_and_take():
+    k = KATS["dict_encode_primitive"]
+    codes, dv = E.dict_encode(np.array(k["values"], np.int32))
+    assert codes.tolist() == k["expect_codes"] and dv.tolist() == k["expect_values"]
+    k = KATS["take_primitive"]
+    arr = A.dict_array(A.primitive(np.array(k["values"], np.int32)), A.primitive(np.array(k["codes"], np.uint64)))
+    assert canon(arr)[0].tolist() == k["expect_decoded"]
+
+
+def test_kat_zigzag():
+    vals = _gen(KATS["zigzag_i64_range"])
+    assert np.array_equal(canon(E.encode_zigzag(vals))[0], vals)
+
+
+def test_kat_fsst_roundtrip():
+    strings = [s.encode() for s in KATS["fsst_three_sentences"]["strings"]]
+    arr = E.encode_fsst(strings)
+    (views, heap), valid = canon(arr)
+    assert valid is None
+    assert [view_bytes(views, heap, i) for i in range(3)] == strings
+    assert heap.tobytes() == b"".join(strings)
+
+
+def test_kat_views_inline_boundary():
+    k = KATS["varbin_to_views_inline_boundary"]
+    strings = [None if s is None else s.encode() for s in k["strings"]]
+    heap, offs, valid = E.strings_to_heap(strings)
+    arr = A.varbin(A.primitive(offs.astype(np.int32)), A.primitive(heap), validity=valid)
+    (views, h), v = canon(arr)
+    assert v.tolist() == [False, False, True, True]
+    assert not views[0].any() and not views[1].any()  # null view == 0
+    for i, inl in enumerate(k["expect_inlined"]):
+        if inl is None:
+            continue
+        n = int(views[i, :4].view(np.uint32)[0])
+        assert (n <= 12) == inl
+        assert view_bytes(views, h, i) == strings[i]
+    # ref view: buffer_index 0, offset = start offset in the heap
+    assert views[3, 8:12].view(np.uint32)[0] == 0 and views[3, 12:16].view(np.uint32)[0] == 12
+
+
+# ---------------------------------------------------------------- encoder roundtrips
+@pytest.mark.parametrize("dt", [np.uint8, np.uint16, np.uint32, np.uint64])
+@pytest.mark.parametrize("n", [0, 1, 1023, 1024, 1025, 5000])
+def test_bitpacked_roundtrip_with_patches(dt, n):
+    rng = np.random.default_rng(n)
+    T = np.dtype(dt).itemsize * 8
+    vals = rng.integers(0, 1 << min(T - 1, 5), n, dtype=np.uint64).astype(dt)
+    if n > 10:
+        vals[rng.choice(n, n // 50 + 1, replace=False)] = np.iinfo(dt).max
+    arr = E.encode_bitpacked(vals)
+    assert np.array_equal(canon(arr)[0], vals)
+
+
+@pytest.mark.parametrize("offset", [1, 100, 1023])
+def test_bitpacked_sliced_offset(offset):
+    rng = np.random.default_rng(offset)
+    vals = rng.integers(0, 1 << 9, 3000, dtype=np.uint32)
+    arr = E.encode_bitpacked(vals, bit_width=9, offset=offset)
+    assert np.array_equal(canon(arr)[0], vals)
+
+
+def test_alp_f64_prices_roundtrip():
+    rng = np.random.default_rng(42)
+    vals = np.round(rng.uniform(1, 100000, 20000) * 100) / 100
+    vals[rng.choice(vals.size, 20, replace=False)] = rng.standard_normal(20) * 1e6
+    arr = E.encode_alp(vals)
+    got, _ = canon(arr)
+    assert got.tobytes() == vals.tobytes()
+
+
+@pytest.mark.parametrize("ptype", ["f32", "f64"])
+def test_alprd_roundtrip(ptype):
+    rng = np.random.default_rng(3)
+    vals = (rng.standard_normal(5000) * 1000).astype(A.NP_OF_PTYPE[ptype])
+    arr = E.encode_alprd(vals)
+    got, _ = canon(arr)
+    assert got.tobytes() == vals.tobytes()
+
+
+def test_dict_bitpacked_roundtrip():
+    rng = np.random.default_rng(1)
+    dv = rng.integers(0, 2 ** 63, 300, dtype=np.uint64)
+    vals = dv[rng.integers(0, 300, 7000)]
+    assert np.array_equal(canon(E.encode_dict(vals))[0], vals)
+
+
+def test_runend_roundtrip_and_slice():
+    rng = np.random.default_rng(2)
+    vals = np.repeat(rng.integers(-100, 100, 500).astype(np.int32), rng.integers(1, 40, 500))
+    arr = E.encode_runend(vals)
+    assert np.array_equal(canon(arr)[0], vals)
+    # sliced RunEnd: offset into the runs (runend/array.rs offset/len semantics)
+    arr.meta["offset"] = 17
+    arr.len = vals.size - 40
+    assert np.array_equal(canon(arr)[0], vals[17:17 + arr.len])
+
+
+def test_delta_sliced():
+    vals = np.cumsum(np.random.default_rng(5).integers(0, 9, 5000)).astype(np.uint32)
+    arr = E.encode_delta(vals)
+    sl = A.delta(arr.children[0], arr.children[1], offset=300, length=4000)
+    assert np.array_equal(canon(sl)[0], vals[300:4300])
+
+
+def test_fsst_with_nulls_and_long_strings():
+    rng = np.random.default_rng(9)
+    words = [b"quick", b"brown", b"fox", b"jumps", b"over", b"lazy", b"dogs", b"\xff\x00"]
+    strings = []
+    for i in range(2000):
+        if i % 17 == 0:
+            strings.append(None)
+        else:
+            strings.append(b" ".join(words[j] for j in rng.integers(0, len(words), rng.integers(0, 12))))
+    arr = E.encode_fsst(strings)
+    (views, heap), valid = canon(arr)
+    assert valid.tolist() == [s is not None for s in strings]
+    for i, s in enumerate(strings):
+        if s is None:
+            assert not views[i].any()
+        else:
+            assert view_bytes(views, heap, i) == s
+
+
+def test_sparse_and_constant():
+    idx = A.primitive(np.array([3, 5, 9], np.uint64))
+    vals = A.primitive(np.array([7, 8, 9], np.int64))
+    got, valid = canon(A.sparse(idx, vals, 12, fill=None))
+    assert got.tolist() == [0, 0, 0, 7, 0, 8, 0, 0, 0, 9, 0, 0]
+    assert valid.tolist() == [i in (3, 5, 9) for i in range(12)]
+    got, valid = canon(A.sparse(idx, vals, 12, fill=-1))
+    assert got.tolist() == [-1, -1, -1, 7, -1, 8, -1, -1, -1, 9, -1, -1] and valid is None
+    assert canon(A.constant(2.5, 4, "f64"))[0].tolist() == [2.5] * 4
+
+
+def test_reference_validation_errors():
+    with pytest.raises(A.VortexError, match="uint"):
+        A.bitpacked(np.zeros(128, np.uint8), "i32", 1, 10)
+    with pytest.raises(A.VortexError, match="packed bytes"):
+        A.bitpacked(np.zeros(100, np.uint8), "u32", 1, 10)
+    with pytest.raises(A.VortexError, match="1024"):
+        A.bitpacked(np.zeros(128, np.uint8), "u32", 1, 10, offset=1024)
+    with pytest.raises(A.VortexError):
+        A.dict_array(A.primitive(np.array([1], np.int32)), A.primitive(np.array([0], np.int32)))
+    with pytest.raises(A.VortexError, match="bit width"):
+        E.encode_bitpacked(np.array([1, 2], np.uint8), bit_width=8)

@@ -1,0 +1,462 @@
+"""Host-side mirror of the Vortex array model for the canonicalize hot path.
+
+`Array` mirrors vortex-array's `Array`/`ArrayData` (vortex-array/src/data.rs:14-22): an encoding
+id (encoding/mod.rs:106-147), a dtype, a length, the encoding's metadata struct, its buffers
+and its children in the reference's child order.  The factory functions restate the
+reference constructors *including their validation* (e.g. `BitPackedArray::try_new`,
+bitpacking/mod.rs:54-130) so malformed trees fail the same way, with the same VortexError
+kind, before anything reaches the GPU.
+
+`canonicalize(array, ctx)` is `Array::into_canonical` (canonical.rs:353-357): the tree is
+flattened into `vxg_array` descriptors and handed to the C ABI (`vxg_canonicalize`); the result
+is a `Canonical` whose buffers are torch tensors in HBM.  There is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import Any, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import DTYPE, ENC, PTYPE, PTYPES, VALIDITY, VortexGpuError
+
+NP_OF_PTYPE = {"u8": np.uint8, "u16": np.uint16, "u32": np.uint32, "u64": np.uint64,
+               "i8": np.int8, "i16": np.int16, "i32": np.int32, "i64": np.int64,
+               "f16": np.float16, "f32": np.float32, "f64": np.float64}
+PTYPE_OF_NP = {np.dtype(v): k for k, v in NP_OF_PTYPE.items()}
+
+
+def ptype_width(p: str) -> int:
+    return np.dtype(NP_OF_PTYPE[p]).itemsize
+
+
+def unsigned_of(p: str) -> str:
+    return "u" + p[1:] if p[0] == "i" else p
+
+
+class VortexError(VortexGpuError):
+    pass
+
+
+def _bail(kind: str, msg: str):
+    code = {v: k for k, v in _lib.STATUS.items()}[kind]
+    raise VortexError(code, msg)
+
+
+@dataclass
+class Array:
+    encoding: int
+    len: int
+    dtype: int = DTYPE["PRIMITIVE"]
+    ptype: str = "u8"
+    nullable: bool = False
+    validity: int = VALIDITY["NON_NULLABLE"]
+    meta: dict = field(default_factory=dict)
+    buffers: list = field(default_factory=list)  # numpy arrays (host) or torch tensors (device)
+    children: list = field(default_factory=list)
+
+    # ---- movement -----------------------------------------------------------------
+    def to(self, device) -> "Array":
+        """Copy every buffer into device memory (torch tensors; 16-byte aligned)."""
+        import torch
+
+        def mv(b):
+            if isinstance(b, torch.Tensor):
+                return b.to(device)
+            a = np.ascontiguousarray(b).view(np.uint8).reshape(-1)
+            t = torch.empty(max(a.size, 16), dtype=torch.uint8, device=device)
+            if a.size:
+                t[: a.size].copy_(torch.from_numpy(a))
+            return t[: a.size] if a.size else t[:0]
+
+        return Array(self.encoding, self.len, self.dtype, self.ptype, self.nullable, self.validity,
+                     dict(self.meta), [mv(b) for b in self.buffers],
+                     [c.to(device) for c in self.children])
+
+    def nbytes(self) -> int:
+        """Bytes of all buffers in the tree (the compressed size the decoder reads)."""
+        tot = 0
+        for b in self.buffers:
+            tot += b.numel() * b.element_size() if hasattr(b, "element_size") else np.asarray(b).nbytes
+        return tot + sum(c.nbytes() for c in self.children)
+
+
+# ---- constructors (reference validation restated) -------------------------------------
+def _np(x, p=None):
+    a = np.ascontiguousarray(x)
+    if p is not None:
+        a = a.astype(NP_OF_PTYPE[p], copy=False)
+    return a
+
+
+def bool_validity(mask) -> "Array":
+    """Canonical BoolArray validity (LSB bitmap), array/bool/mod.rs:25-28."""
+    m = np.asarray(mask, dtype=bool)
+    bits = np.packbits(m, bitorder="little")
+    return Array(ENC["BOOL"], len(m), DTYPE["BOOL"], "u8", False, VALIDITY["NON_NULLABLE"],
+                 {"first_byte_bit_offset": 0}, [bits])
+
+
+def _validity_kind(nullable: bool, validity) -> tuple[int, Optional[Array]]:
+    if validity is None:
+        return (VALIDITY["ALL_VALID"] if nullable else VALIDITY["NON_NULLABLE"]), None
+    if isinstance(validity, str):
+        return VALIDITY[validity], None
+    return VALIDITY["ARRAY"], bool_validity(validity)
+
+
+def primitive(values, ptype: Optional[str] = None, validity=None) -> Array:
+    """PrimitiveArray (array/primitive/mod.rs:33-72)."""
+    a = _np(values)
+    p = ptype or PTYPE_OF_NP[a.dtype]
+    a = a.astype(NP_OF_PTYPE[p], copy=False)
+    nullable = validity is not None
+    vk, vchild = _validity_kind(nullable, validity)
+    return Array(ENC["PRIMITIVE"], len(a), DTYPE["PRIMITIVE"], p, nullable, vk, {}, [a],
+                 [vchild] if vchild is not None else [])
+
+
+def bitpacked(packed, ptype: str, bit_width: int, length: int, offset: int = 0,
+              patches: Optional[Array] = None, validity=None) -> Array:
+    """BitPackedArray::try_new_from_offset (bitpacking/mod.rs:54-130)."""
+    if ptype[0] != "u":
+        _bail("MismatchedTypes", f"expected type: uint but instead got {ptype}")
+    if bit_width > 64:
+        _bail("InvalidArgument", f"Unsupported bit width {bit_width}")
+    if offset > 1023:
+        _bail("InvalidArgument", f"Offset must be less than full block, i.e. 1024, got {offset}")
+    packed = np.ascontiguousarray(packed).view(np.uint8).reshape(-1)
+    expected = ((length + offset + 1023) // 1024) * (128 * bit_width)
+    if packed.size != expected:
+        _bail("InvalidArgument", f"Expected {expected} packed bytes, got {packed.size}")
+    if patches is not None:
+        if patches.len != length:
+            _bail("InvalidArgument", "Mismatched length in BitPackedArray between encoded and patches")
+        if patches.encoding == ENC["SPARSE"] and patches.children[0].len == 0:
+            _bail("InvalidArgument", "cannot construct BitPackedArray using patches without indices")
+    nullable = validity is not None
+    vk, vchild = _validity_kind(nullable, validity)
+    children = ([patches] if patches is not None else []) + ([vchild] if vchild is not None else [])
+    return Array(ENC["FL_BITPACKED"], length, DTYPE["PRIMITIVE"], ptype, nullable, vk,
+                 {"bit_width": bit_width, "offset": offset, "has_patches": patches is not None},
+                 [packed], children)
+
+
+def sparse(indices: Array, values: Array, length: int, indices_offset: int = 0,
+           fill=None, ptype: Optional[str] = None) -> Array:
+    """SparseArray (array/sparse/mod.rs:24-29); fill None = ScalarValue::Null."""
+    p = ptype or values.ptype
+    fill_bytes = bytes(16)
+    if fill is not None:
+        fill_bytes = np.array([fill], dtype=NP_OF_PTYPE[p]).tobytes().ljust(16, b"\0")
+    return Array(ENC["SPARSE"], length, DTYPE["PRIMITIVE"], p, fill is None,
+                 VALIDITY["NON_NULLABLE"],
+                 {"indices_offset": indices_offset, "indices_len": indices.len,
+                  "fill_is_null": fill is None, "fill": fill_bytes}, [], [indices, values])
+
+
+def frame_of_reference(encoded: Array, reference: int, shift: int, ptype: str) -> Array:
+    """FoRArray::try_new (for/mod.rs:26-52); encoded child dtype = unsigned(ptype) (:57-66)."""
+    if encoded.ptype != unsigned_of(ptype):
+        _bail("MismatchedTypes", f"FoR child must be {unsigned_of(ptype)}, got {encoded.ptype}")
+    ref_bits = int(np.array([reference], dtype=NP_OF_PTYPE[ptype]).view(
+        NP_OF_PTYPE[unsigned_of(ptype)])[0])
+    return Array(ENC["FL_FOR"], encoded.len, DTYPE["PRIMITIVE"], ptype, encoded.nullable,
+                 VALIDITY["NON_NULLABLE"], {"reference": ref_bits, "shift": shift}, [], [encoded])
+
+
+def zigzag(encoded: Array) -> Array:
+    """ZigZagArray (zigzag/array.rs:22-103): encoded unsigned -> signed of same width."""
+    if encoded.ptype[0] != "u":
+        _bail("MismatchedTypes", "ZigZag encoded child must be unsigned")
+    return Array(ENC["ZIGZAG"], encoded.len, DTYPE["PRIMITIVE"], "i" + encoded.ptype[1:],
+                 encoded.nullable, VALIDITY["NON_NULLABLE"], {}, [], [encoded])
+
+
+def alp(encoded: Array, e: int, f: int, patches: Optional[Array] = None) -> Array:
+    """ALPArray::try_new (alp/array.rs:33-77): encoded i32 -> f32, i64 -> f64."""
+    fp = {"i32": "f32", "i64": "f64"}.get(encoded.ptype)
+    if fp is None:
+        _bail("MismatchedTypes", f"ALP encoded child must be i32/i64, got {encoded.ptype}")
+    return Array(ENC["ALP"], encoded.len, DTYPE["PRIMITIVE"], fp, encoded.nullable,
+                 VALIDITY["NON_NULLABLE"], {"e": e, "f": f, "has_patches": patches is not None},
+                 [], [encoded] + ([patches] if patches is not None else []))
+
+
+def alp_rd(ptype: str, left_parts: Array, left_dict: Sequence[int], right_parts: Array,
+           right_bit_width: int, exceptions: Optional[Array] = None) -> Array:
+    """ALPRDArray::try_new (alp_rd/array.rs:27-115)."""
+    if left_parts.len != right_parts.len:
+        _bail("InvalidArgument", "left_parts and right_parts must be of same length")
+    if left_parts.ptype[0] != "u":
+        _bail("InvalidArgument", "left_parts dtype must be uint")
+    if right_parts.nullable or right_parts.ptype[0] != "u":
+        _bail("MismatchedTypes", "right_parts must be non-nullable uint")
+    d = list(left_dict) + [0] * (8 - len(left_dict))
+    return Array(ENC["ALP_RD"], left_parts.len, DTYPE["PRIMITIVE"], ptype, left_parts.nullable,
+                 VALIDITY["NON_NULLABLE"],
+                 {"right_bit_width": right_bit_width, "dict_len": len(left_dict), "dict": d,
+                  "left_parts_ptype": PTYPE[left_parts.ptype], "has_exceptions": exceptions is not None},
+                 [], [left_parts, right_parts] + ([exceptions] if exceptions is not None else []))
+
+
+def dict_array(values: Array, codes: Array) -> Array:
+    """DictArray::try_new (dict/array.rs:34-49): codes non-nullable unsigned."""
+    if codes.ptype[0] != "u" or codes.nullable:
+        _bail("MismatchedTypes", f"non-nullable unsigned int, got {codes.ptype}")
+    return Array(ENC["DICT"], codes.len, values.dtype, values.ptype, values.nullable,
+                 VALIDITY["NON_NULLABLE"], {"codes_ptype": PTYPE[codes.ptype], "values_len": values.len},
+                 [], [values, codes])
+
+
+def delta(bases: Array, deltas: Array, offset: int = 0, length: Optional[int] = None,
+          validity=None) -> Array:
+    """DeltaArray::try_new (delta/mod.rs:89-157)."""
+    length = deltas.len - offset if length is None else length
+    if offset >= 1024:
+        _bail("InvalidArgument", f"offset must be less than 1024: {offset}")
+    if offset + length > deltas.len:
+        _bail("InvalidArgument", "offset + logical_len must be <= the size of deltas")
+    if bases.ptype != deltas.ptype:
+        _bail("InvalidArgument", "DeltaArray: bases and deltas must have the same dtype")
+    lanes = 1024 // (8 * ptype_width(deltas.ptype))
+    expect = (deltas.len // 1024) * lanes + (1 if deltas.len % 1024 else 0)
+    if bases.len != expect:
+        _bail("InvalidArgument", f"DeltaArray: bases.len() ({bases.len}) != expected_bases_len ({expect})")
+    nullable = validity is not None
+    vk, vchild = _validity_kind(nullable, validity)
+    return Array(ENC["FL_DELTA"], length, DTYPE["PRIMITIVE"], deltas.ptype, nullable, vk,
+                 {"deltas_len": deltas.len, "offset": offset}, [],
+                 [bases, deltas] + ([vchild] if vchild is not None else []))
+
+
+def run_end(ends: Array, values: Array, length: Optional[int] = None, offset: int = 0,
+            validity=None) -> Array:
+    """RunEndArray (runend/array.rs:47-106)."""
+    if ends.ptype[0] not in "ui":
+        _bail("InvalidArgument", "Run ends must be integers")
+    length = length if length is not None else None
+    nullable = validity is not None
+    vk, vchild = _validity_kind(nullable, validity)
+    return Array(ENC["RUN_END"], length, DTYPE["PRIMITIVE"], values.ptype, nullable, vk,
+                 {"ends_ptype": PTYPE[ends.ptype], "num_runs": ends.len, "offset": offset}, [],
+                 [ends, values] + ([vchild] if vchild is not None else []))
+
+
+def constant(value, length: int, ptype: str) -> Array:
+    """ConstantArray (array/constant/mod.rs:22-60); value None = null scalar."""
+    sc = bytes(16) if value is None else np.array([value], dtype=NP_OF_PTYPE[ptype]).tobytes().ljust(16, b"\0")
+    return Array(ENC["CONSTANT"], length, DTYPE["PRIMITIVE"], ptype, value is None,
+                 VALIDITY["NON_NULLABLE"], {"is_null": value is None, "scalar": sc})
+
+
+def chunked(chunks: Sequence[Array]) -> Array:
+    """ChunkedArray::try_new (array/chunked/mod.rs:47-80): child 0 = u64 chunk offsets."""
+    if not chunks:
+        _bail("InvalidArgument", "chunked needs at least one chunk for a dtype")
+    d0 = (chunks[0].dtype, chunks[0].ptype)
+    for c in chunks:
+        if (c.dtype, c.ptype) != d0:
+            _bail("MismatchedTypes", "Chunks must have the same dtype")
+    offs = np.zeros(len(chunks) + 1, dtype=np.uint64)
+    offs[1:] = np.cumsum([c.len for c in chunks])
+    return Array(ENC["CHUNKED"], int(offs[-1]), chunks[0].dtype, chunks[0].ptype,
+                 any(c.nullable for c in chunks), VALIDITY["NON_NULLABLE"],
+                 {"nchunks": len(chunks)}, [], [primitive(offs)] + list(chunks))
+
+
+def varbin(offsets: Array, data: Array, utf8: bool = True, validity=None) -> Array:
+    """VarBinArray (array/varbin/mod.rs:35-100): children offsets, bytes, validity."""
+    nullable = validity is not None
+    vk, vchild = _validity_kind(nullable, validity)
+    return Array(ENC["VARBIN"], offsets.len - 1, DTYPE["UTF8" if utf8 else "BINARY"], "u8", nullable,
+                 vk, {"offsets_ptype": PTYPE[offsets.ptype], "bytes_len": data.len}, [],
+                 [offsets, data] + ([vchild] if vchild is not None else []))
+
+
+def fsst(symbols: Array, symbol_lengths: Array, codes: Array, uncompressed_lengths: Array,
+         utf8: bool = True) -> Array:
+    """FSSTArray::try_new (fsst/array.rs:43-105)."""
+    if symbols.len > 255:
+        _bail("InvalidArgument", "symbols array must have length <= 255")
+    if symbols.len != symbol_lengths.len:
+        _bail("InvalidArgument", "symbols and symbol_lengths arrays must have same length")
+    if uncompressed_lengths.len != codes.len:
+        _bail("InvalidArgument", "uncompressed_lengths must be same len as codes")
+    if codes.encoding != ENC["VARBIN"]:
+        _bail("InvalidArgument", "codes array must be VarBin")
+    return Array(ENC["FSST"], codes.len, DTYPE["UTF8" if utf8 else "BINARY"], "u8", codes.nullable,
+                 VALIDITY["NON_NULLABLE"],
+                 {"symbols_len": symbols.len, "codes_nullable": codes.nullable,
+                  "uncompressed_lengths_ptype": PTYPE[uncompressed_lengths.ptype]}, [],
+                 [symbols, symbol_lengths, codes, uncompressed_lengths])
+
+
+# ---- flattening to the C ABI -------------------------------------------------------------
+def _fill_meta(m: _lib.VxgMeta, a: Array) -> None:
+    md = a.meta
+    e = a.encoding
+    if e == ENC["FL_BITPACKED"]:
+        m.bitpacked.bit_width, m.bitpacked.has_patches, m.bitpacked.offset = (
+            md["bit_width"], int(md["has_patches"]), md["offset"])
+    elif e == ENC["FL_FOR"]:
+        m.for_.reference, m.for_.shift = md["reference"], md["shift"]
+    elif e == ENC["FL_DELTA"]:
+        m.delta.deltas_len, m.delta.offset = md["deltas_len"], md["offset"]
+    elif e == ENC["ALP"]:
+        m.alp.e, m.alp.f, m.alp.has_patches = md["e"], md["f"], int(md["has_patches"])
+    elif e == ENC["ALP_RD"]:
+        m.alprd.right_bit_width = md["right_bit_width"]
+        m.alprd.dict_len = md["dict_len"]
+        m.alprd.left_parts_ptype = md["left_parts_ptype"]
+        m.alprd.has_exceptions = int(md["has_exceptions"])
+        for i, v in enumerate(md["dict"]):
+            m.alprd.dict[i] = v
+    elif e == ENC["DICT"]:
+        m.dict.codes_ptype, m.dict.values_len = md["codes_ptype"], md["values_len"]
+    elif e == ENC["FSST"]:
+        m.fsst.symbols_len = md["symbols_len"]
+        m.fsst.codes_nullable = int(md["codes_nullable"])
+        m.fsst.uncompressed_lengths_ptype = md["uncompressed_lengths_ptype"]
+    elif e == ENC["RUN_END"]:
+        m.runend.ends_ptype, m.runend.num_runs, m.runend.offset = (
+            md["ends_ptype"], md["num_runs"], md["offset"])
+    elif e == ENC["SPARSE"]:
+        m.sparse.indices_offset = md["indices_offset"]
+        m.sparse.indices_len = md["indices_len"]
+        m.sparse.fill_is_null = int(md["fill_is_null"])
+        for i, b in enumerate(md["fill"][:16]):
+            m.sparse.fill[i] = b
+    elif e == ENC["CONSTANT"]:
+        m.constant.is_null = int(md["is_null"])
+        for i, b in enumerate(md["scalar"][:16]):
+            m.constant.scalar[i] = b
+    elif e == ENC["CHUNKED"]:
+        m.chunked.nchunks = md["nchunks"]
+    elif e == ENC["VARBIN"]:
+        m.varbin.offsets_ptype, m.varbin.bytes_len = md["offsets_ptype"], md["bytes_len"]
+    elif e == ENC["BOOL"]:
+        m.boolean.first_byte_bit_offset = md.get("first_byte_bit_offset", 0)
+
+
+def _buf_ptr(b) -> tuple[int, int]:
+    import torch
+    if not isinstance(b, torch.Tensor) or not b.is_cuda:
+        raise VortexError(3, "array buffers must be device tensors: call Array.to(device) first")
+    return b.data_ptr(), b.numel() * b.element_size()
+
+
+def flatten(a: Array, keep: list) -> _lib.VxgArray:
+    node = _lib.VxgArray()
+    node.encoding = a.encoding
+    node.dtype = a.dtype
+    node.ptype = PTYPE[a.ptype]
+    node.nullable = int(a.nullable)
+    node.validity = a.validity
+    node.len = a.len
+    _fill_meta(node.meta, a)
+    if a.buffers:
+        bufs = (_lib.VxgBuffer * len(a.buffers))()
+        for i, b in enumerate(a.buffers):
+            bufs[i].ptr, bufs[i].len = _buf_ptr(b)
+        keep.append(bufs)
+        node.buffers = C.cast(bufs, C.POINTER(_lib.VxgBuffer))
+        node.n_buffers = len(a.buffers)
+    if a.children:
+        kids = (_lib.VxgArray * len(a.children))()
+        for i, c in enumerate(a.children):
+            kids[i] = flatten(c, keep)
+        keep.append(kids)
+        node.children = C.cast(kids, C.POINTER(_lib.VxgArray))
+        node.n_children = len(a.children)
+    return node
+
+
+# ---- context + canonical output ----------------------------------------------------------
+class Context:
+    """One vxg_ctx per device (one context per device, thread-safe calls)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = _lib.gpu_lib()
+        self.device = device
+        h = C.c_void_p()
+        _lib.check(self.lib.vxg_open(device, C.byref(h)))
+        self.handle = h
+
+    def close(self):
+        if self.handle:
+            self.lib.vxg_close(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def stream_ptr(self):
+        import torch
+        return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def sync(self):
+        _lib.check(self.lib.vxg_stream_sync(self.handle, self.stream_ptr()))
+
+
+@dataclass
+class Canonical:
+    """Canonical::Primitive or Canonical::VarBinView (canonical.rs:56-63), device tensors."""
+    kind: str
+    len: int
+    ptype: str
+    values: Any = None       # torch.uint8 tensor (len * width bytes) for Primitive
+    views: Any = None        # torch.uint8 tensor (16 * len) for VarBinView
+    data: Any = None         # torch.uint8 tensor: buffer 0 of the view array
+    validity: Any = None     # torch.uint8 LSB bitmap or None (no nulls)
+
+    def numpy(self):
+        """Host copy: values as the ptype's numpy dtype, or (views u8[n,16], data u8[])."""
+        if self.kind == "primitive":
+            return self.values.cpu().numpy().view(NP_OF_PTYPE[self.ptype])
+        return self.views.cpu().numpy().reshape(-1, 16), self.data.cpu().numpy()
+
+    def validity_mask(self):
+        if self.validity is None:
+            return None
+        bits = self.validity.cpu().numpy()
+        return np.unpackbits(bits, bitorder="little")[: self.len].astype(bool)
+
+
+def canonicalize(a: Array, ctx: Context, out_values=None, sync: bool = True) -> Canonical:
+    """Array::into_canonical on the GPU (vxg_canonicalize).  `out_values` (a device uint8
+    tensor of len*width bytes) decodes in place, e.g. into a slice of a chunked output."""
+    import torch
+    keep: list = []
+    node = flatten(a, keep)
+    dev = torch.device("cuda", ctx.device)
+    vb, db = C.c_uint64(), C.c_uint64()
+    _lib.check(ctx.lib.vxg_canonical_size(ctx.handle, C.byref(node), C.byref(vb), C.byref(db)))
+    out = _lib.VxgCanonical()
+    res = Canonical("primitive" if a.dtype == DTYPE["PRIMITIVE"] else "varbinview", a.len, a.ptype)
+    nbits = ((a.len + 31) // 32) * 4
+    valid_t = torch.empty(max(nbits, 4), dtype=torch.uint8, device=dev) if a.nullable else None
+    if a.dtype == DTYPE["PRIMITIVE"]:
+        vals = out_values if out_values is not None else torch.empty(max(vb.value, 16), dtype=torch.uint8, device=dev)
+        out.values = vals.data_ptr()
+        res.values = vals[: vb.value]
+    else:
+        views = torch.empty(max(vb.value, 16), dtype=torch.uint8, device=dev)
+        data = torch.empty(db.value + 16, dtype=torch.uint8, device=dev)
+        out.views, out.data = views.data_ptr(), data.data_ptr()
+        res.views, res.data = views[: vb.value], data[: db.value]
+    if valid_t is not None:
+        out.validity = valid_t.data_ptr()
+    _lib.check(ctx.lib.vxg_canonicalize(ctx.handle, C.byref(node), C.byref(out), ctx.stream_ptr()))
+    if out.validity:
+        if valid_t is None or out.validity != valid_t.data_ptr():
+            raise VortexError(7, "engine allocated validity for a non-nullable dtype")
+        res.validity = valid_t[: (a.len + 7) // 8]
+    if sync:
+        ctx.sync()
+    return res

@@ -1,0 +1,990 @@
+// capi.hip — the C ABI (include/vortex_gpu.h) and the canonicalize planner.
+//
+// The planner is the host-side mirror of the reference's dispatch: Array::into_canonical
+// (vortex-array/src/canonical.rs:353-357) -> ArrayEncoding::canonicalize (encoding/mod.rs:53)
+// -> per-encoding IntoCanonical.  Where the reference materialises one buffer per cascade
+// level (e.g. ALP -> FoR -> BitPacked is 3-4 passes, SURVEY.md §3 stack B) the planner
+// recognises the cascade and issues ONE fused K1 launch (+ tiny patch scatters); anything it
+// does not recognise is decoded child-first into temporaries exactly like the reference.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "vxg_internal.hpp"
+
+struct vxg_ctx {
+    vxg::Ctx c;
+};
+
+namespace vxg {
+
+const float kF10f[11] = {1.0f, 10.0f, 100.0f, 1000.0f, 10000.0f, 100000.0f, 1000000.0f,
+                         10000000.0f, 100000000.0f, 1000000000.0f, 10000000000.0f};
+const float kIF10f[11] = {1.0f, 0.1f, 0.01f, 0.001f, 0.0001f, 0.00001f, 0.000001f,
+                          0.0000001f, 0.00000001f, 0.000000001f, 0.0000000001f};
+const double kF10d[24] = {
+    1.0, 10.0, 100.0, 1000.0, 10000.0, 100000.0, 1000000.0, 10000000.0, 100000000.0,
+    1000000000.0, 10000000000.0, 100000000000.0, 1000000000000.0, 10000000000000.0,
+    100000000000000.0, 1000000000000000.0, 10000000000000000.0, 100000000000000000.0,
+    1000000000000000000.0, 10000000000000000000.0, 100000000000000000000.0,
+    1000000000000000000000.0, 10000000000000000000000.0, 100000000000000000000000.0};
+const double kIF10d[24] = {
+    1.0, 0.1, 0.01, 0.001, 0.0001, 0.00001, 0.000001, 0.0000001, 0.00000001, 0.000000001,
+    0.0000000001, 0.00000000001, 0.000000000001, 0.0000000000001, 0.00000000000001,
+    0.000000000000001, 0.0000000000000001, 0.00000000000000001, 0.000000000000000001,
+    0.0000000000000000001, 0.00000000000000000001, 0.000000000000000000001,
+    0.0000000000000000000001, 0.00000000000000000000001};
+
+static thread_local std::string g_last_error;
+
+vxg_status set_error(vxg_status s, const std::string& msg) {
+    if (s != VXG_OK) g_last_error = msg;
+    return s;
+}
+
+vxg_status hip_check(hipError_t e, const char* what) {
+    if (e == hipSuccess) return VXG_OK;
+    return set_error(e == hipErrorOutOfMemory ? VXG_ERR_OUT_OF_MEMORY : VXG_ERR_HIP,
+                     std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// K1 dispatch over the instantiation units.
+vxg_status launch_fl_unpack(int T, int W, Epi epi, int vw, const UnpackArgs& a, hipStream_t s) {
+    if (W < 0 || W > T) return set_error(VXG_ERR_INVALID_ARGUMENT, "bit width out of range");
+    switch (epi) {
+    case Epi::Plain:
+    case Epi::For:
+    case Epi::ForZigZag:
+        switch (T) {
+        case 8: return fl_plain_8(W, epi, a, s);
+        case 16: return fl_plain_16(W, epi, a, s);
+        case 32: return fl_plain_32(W, epi, a, s);
+        case 64: return fl_plain_64(W, epi, a, s);
+        }
+        return set_error(VXG_ERR_INVALID_ARGUMENT, "bad FastLanes width");
+    case Epi::AlpF32:
+    case Epi::AlpF64:
+        return fl_alp(T, W, epi, a, s);
+    case Epi::Dict:
+        if (W > kDictFusedMaxW) return VXG_ERR_NOT_IMPLEMENTED;
+        switch (vw) {
+        case 1: return fl_dict_1(T, W, a, s);
+        case 2: return fl_dict_2(T, W, a, s);
+        case 4: return fl_dict_4(T, W, a, s);
+        case 8: return fl_dict_8(T, W, a, s);
+        case 16: return fl_dict_16(T, W, a, s);
+        }
+        return set_error(VXG_ERR_INVALID_ARGUMENT, "bad dictionary value width");
+    }
+    return VXG_ERR_INVALID_ARGUMENT;
+}
+
+vxg_status launch_fl_unpack_dict_chunks(int T, int W, int vw, const DictChunkDev* d, uint32_t n,
+                                        uint64_t g, uint32_t* err, hipStream_t s) {
+    if (W > kDictFusedMaxW) return VXG_ERR_NOT_IMPLEMENTED;
+    switch (vw) {
+    case 1: return fl_dict_chunks_1(T, W, d, n, g, err, s);
+    case 2: return fl_dict_chunks_2(T, W, d, n, g, err, s);
+    case 4: return fl_dict_chunks_4(T, W, d, n, g, err, s);
+    case 8: return fl_dict_chunks_8(T, W, d, n, g, err, s);
+    case 16: return fl_dict_chunks_16(T, W, d, n, g, err, s);
+    }
+    return set_error(VXG_ERR_INVALID_ARGUMENT, "bad dictionary value width");
+}
+
+}  // namespace vxg
+
+using namespace vxg;
+
+namespace {
+
+#define VXG_TRY(expr)                         \
+    do {                                      \
+        vxg_status _s = (expr);               \
+        if (_s != VXG_OK) return _s;          \
+    } while (0)
+
+inline hipStream_t S(void* s) { return static_cast<hipStream_t>(s); }
+
+vxg_status use_device(vxg_ctx* ctx) {
+    if (!ctx) return set_error(VXG_ERR_INVALID_ARGUMENT, "null vxg_ctx");
+    return hip_check(hipSetDevice(ctx->c.device), "hipSetDevice");
+}
+
+vxg_status bitunpack_common(vxg_ctx* ctx, int T, unsigned W, unsigned offset, uint64_t len,
+                            const void* packed, uint64_t packed_bytes, Epi epi, int vw,
+                            UnpackArgs a, void* out, void* stream) {
+    if (offset > 1023) return set_error(VXG_ERR_INVALID_ARGUMENT, "Offset must be less than full block, i.e. 1024");
+    if (W > unsigned(T)) return set_error(VXG_ERR_INVALID_ARGUMENT, "Unsupported bit width");
+    const uint64_t nblk = (len + offset + 1023) / 1024;
+    if (W > 0 && packed_bytes != nblk * 128ull * W)  // bitpacking/mod.rs:80-88
+        return set_error(VXG_ERR_INVALID_ARGUMENT, "Expected " + std::to_string(nblk * 128ull * W) +
+                                                       " packed bytes, got " + std::to_string(packed_bytes));
+    a.packed = static_cast<const uint8_t*>(packed);
+    a.out = out;
+    a.n_blocks = nblk;
+    a.offset = offset;
+    a.len = len;
+    a.err = ctx->c.err_word;
+    if (reinterpret_cast<uintptr_t>(out) & 15)
+        return set_error(VXG_ERR_INVALID_ARGUMENT, "output buffer must be 16-byte aligned");
+    if (W > 0 && (reinterpret_cast<uintptr_t>(packed) & 15))
+        return set_error(VXG_ERR_INVALID_ARGUMENT, "packed buffer must be 16-byte aligned");
+    return launch_fl_unpack(T, int(W), epi, vw, a, S(stream));
+}
+
+// ===================================================================================
+// Planner
+// ===================================================================================
+class Planner {
+  public:
+    Planner(vxg_ctx* ctx, hipStream_t s) : ctx_(ctx), s_(s) {}
+    ~Planner() {
+        for (void* p : temps_) (void)hipFreeAsync(p, s_);
+    }
+
+    vxg_status canonical(const vxg_array& a, vxg_canonical& out);
+    vxg_status canonical_size(const vxg_array& a, uint64_t& vb, uint64_t& db);
+
+  private:
+    vxg_ctx* ctx_;
+    hipStream_t s_;
+    std::vector<void*> temps_;
+
+    vxg_status temp(uint64_t bytes, void** p) {
+        if (bytes == 0) bytes = 16;
+        VXG_TRY(hip_check(hipMallocAsync(p, (bytes + 15) & ~15ull, s_), "hipMallocAsync"));
+        temps_.push_back(*p);
+        return VXG_OK;
+    }
+
+    static bool is_primitive_dtype(const vxg_array& a) { return a.dtype == VXG_DTYPE_PRIMITIVE; }
+    static int width(const vxg_array& a) { return ptype_width(a.ptype); }
+
+    const vxg_buffer* buf(const vxg_array& a, uint32_t i) const {
+        return i < a.n_buffers ? &a.buffers[i] : nullptr;
+    }
+    const vxg_array* child(const vxg_array& a, uint32_t i) const {
+        return i < a.n_children ? &a.children[i] : nullptr;
+    }
+
+    // Decode a primitive-typed array into dst (len * width bytes, 16-B aligned).
+    vxg_status decode_into(const vxg_array& a, void* dst);
+    // Canonical primitive values of `a` as a device pointer (aliases PRIMITIVE buffers).
+    vxg_status view_primitive(const vxg_array& a, const void** p);
+
+    vxg_status decode_bitpacked(const vxg_array& bp, Epi epi, int vw, UnpackArgs a, void* dst);
+    vxg_status apply_sparse_patches(const vxg_array& sparse, int T, Epi epi, int vw, const UnpackArgs& a,
+                                    void* dst, uint64_t out_len);
+    vxg_status decode_alp(const vxg_array& a, void* dst);
+    vxg_status decode_dict_primitive(const vxg_array& a, void* dst);
+    vxg_status decode_chunked_primitive(const vxg_array& a, void* dst);
+    vxg_status decode_alprd(const vxg_array& a, void* dst);
+    vxg_status decode_sparse_values(const vxg_array& a, void* dst);
+
+    vxg_status validity_into(const vxg_array& a, void** bitmap);
+    vxg_status validity_source(const vxg_array& a, const vxg_array** node, int* kind);
+    vxg_status string_canonical(const vxg_array& a, vxg_canonical& out);
+};
+
+vxg_status Planner::view_primitive(const vxg_array& a, const void** p) {
+    if (a.encoding == VXG_ENC_PRIMITIVE) {
+        const vxg_buffer* b = buf(a, 0);
+        if (!b && a.len) return set_error(VXG_ERR_INVALID_ARGUMENT, "Primitive array without buffer");
+        if (b && b->len < a.len * width(a))
+            return set_error(VXG_ERR_INVALID_ARGUMENT, "Primitive buffer shorter than len * width");
+        *p = b ? b->ptr : nullptr;
+        return VXG_OK;
+    }
+    void* t;
+    VXG_TRY(temp(a.len * width(a), &t));
+    VXG_TRY(decode_into(a, t));
+    *p = t;
+    return VXG_OK;
+}
+
+vxg_status Planner::apply_sparse_patches(const vxg_array& sp, int T, Epi epi, int vw, const UnpackArgs& a,
+                                         void* dst, uint64_t out_len) {
+    // bitpacking/compress.rs:191-207 / alp/compress.rs:80-96: only SparseArray patches.
+    if (sp.encoding != VXG_ENC_SPARSE)
+        return set_error(VXG_ERR_INVALID_ARGUMENT, "Can't patch with a non-Sparse array");
+    const vxg_array* idx = child(sp, 0);
+    const vxg_array* val = child(sp, 1);
+    if (!idx || !val) return set_error(VXG_ERR_INVALID_ARGUMENT, "Sparse patches need indices and values");
+    if (idx->len != val->len) return set_error(VXG_ERR_INVALID_ARGUMENT, "Sparse indices/values length mismatch");
+    const void *pi, *pv;
+    VXG_TRY(view_primitive(*idx, &pi));
+    VXG_TRY(view_primitive(*val, &pv));
+    return launch_patch(vw, width(*idx), ptype_is_signed(idx->ptype), epi, T, dst, out_len, pi,
+                        sp.meta.sparse.indices_offset, pv, idx->len, a, s_);
+}
+
+vxg_status Planner::decode_bitpacked(const vxg_array& bp, Epi epi, int vw, UnpackArgs a, void* dst) {
+    // bitpacking/mod.rs:215-219 -> compress.rs:167-189 (patches: child 0 when has_patches)
+    const int T = 8 * width(bp);
+    if (!ptype_is_int(bp.ptype)) return set_error(VXG_ERR_MISMATCHED_TYPES, "BitPacked needs an integer ptype");
+    const vxg_buffer* packed = buf(bp, 0);
+    const unsigned W = bp.meta.bitpacked.bit_width;
+    a.err = ctx_->c.err_word;
+    VXG_TRY(bitunpack_common(ctx_, T, W, bp.meta.bitpacked.offset, bp.len, packed ? packed->ptr : nullptr,
+                             packed ? packed->len : 0, epi, vw, a, dst, s_));
+    if (bp.meta.bitpacked.has_patches) {
+        const vxg_array* p = child(bp, 0);
+        if (!p) return set_error(VXG_ERR_INVALID_ARGUMENT, "BitPackedArray: patches child missing");
+        VXG_TRY(apply_sparse_patches(*p, T, epi, vw, a, dst, bp.len));
+    }
+    return VXG_OK;
+}
+
+vxg_status Planner::decode_alp(const vxg_array& a, void* dst) {
+    // alp/array.rs:269 -> alp/compress.rs:61-78 (+ patch_decoded :80-96)
+    const vxg_array* enc = child(a, 0);
+    if (!enc) return set_error(VXG_ERR_INVALID_ARGUMENT, "ALPArray: encoded child missing");
+    const bool f32 = a.ptype == VXG_F32;
+    if (!f32 && a.ptype != VXG_F64) return set_error(VXG_ERR_MISMATCHED_TYPES, "ALP can only encode f32 and f64");
+    const unsigned e = a.meta.alp.e, f = a.meta.alp.f;
+    if ((f32 && (e > 10 || f > 10)) || (!f32 && (e > 23 || f > 23)))
+        return set_error(VXG_ERR_INVALID_ARGUMENT, "ALP exponents out of range");
+    UnpackArgs ua{};
+    ua.alp_a = f32 ? double(kF10f[f]) : kF10d[f];
+    ua.alp_b = f32 ? double(kIF10f[e]) : kIF10d[e];
+    const Epi epi = f32 ? Epi::AlpF32 : Epi::AlpF64;
+    const vxg_array* bp = nullptr;
+    if (enc->encoding == VXG_ENC_FL_FOR && child(*enc, 0) &&
+        child(*enc, 0)->encoding == VXG_ENC_FL_BITPACKED) {
+        ua.reference = enc->meta.for_.reference;
+        ua.shift = enc->meta.for_.shift;
+        bp = child(*enc, 0);
+    } else if (enc->encoding == VXG_ENC_FL_BITPACKED) {
+        bp = enc;
+    }
+    if (bp && width(*bp) == (f32 ? 4 : 8)) {
+        VXG_TRY(decode_bitpacked(*bp, epi, 0, ua, dst));  // fused unpack+FoR+ALP (+inner patches)
+    } else {
+        const void* penc;
+        VXG_TRY(view_primitive(*enc, &penc));
+        VXG_TRY(launch_alp(a.ptype, penc, a.len, ua.alp_a, ua.alp_b, dst, s_));
+    }
+    if (a.meta.alp.has_patches) {
+        const vxg_array* p = child(a, 1);
+        if (!p) return set_error(VXG_ERR_INVALID_ARGUMENT, "ALPArray: patches child missing");
+        UnpackArgs plain{};
+        plain.err = ctx_->c.err_word;
+        VXG_TRY(apply_sparse_patches(*p, f32 ? 32 : 64, Epi::Plain, 0, plain, dst, a.len));
+    }
+    return VXG_OK;
+}
+
+vxg_status Planner::decode_dict_primitive(const vxg_array& a, void* dst) {
+    // dict/array.rs:68-73: take(canonical(values), codes)
+    const vxg_array* values = child(a, 0);
+    const vxg_array* codes = child(a, 1);
+    if (!values || !codes) return set_error(VXG_ERR_INVALID_ARGUMENT, "DictArray needs values and codes");
+    if (!ptype_is_unsigned(codes->ptype) || codes->nullable)
+        return set_error(VXG_ERR_MISMATCHED_TYPES, "Dict codes must be non-nullable unsigned int");
+    const void* pv;
+    VXG_TRY(view_primitive(*values, &pv));
+    const int vw = width(*values);
+    if (codes->encoding == VXG_ENC_FL_BITPACKED && codes->meta.bitpacked.bit_width <= kDictFusedMaxW) {
+        UnpackArgs ua{};
+        ua.dict = pv;
+        ua.dict_len = values->len;
+        return decode_bitpacked(*codes, Epi::Dict, vw, ua, dst);
+    }
+    const void* pc;
+    VXG_TRY(view_primitive(*codes, &pc));
+    return launch_take(vw, pv, values->len, width(*codes), pc, a.len, dst, ctx_->c.err_word, s_);
+}
+
+vxg_status Planner::decode_chunked_primitive(const vxg_array& a, void* dst) {
+    // chunked/canonical.rs:27-122 / pack_primitives :170-187 -- each chunk decodes straight
+    // into its slice of the output (no per-chunk materialisation + memcpy).
+    const uint64_t n = a.meta.chunked.nchunks;
+    if (a.n_children != n + 1) return set_error(VXG_ERR_INVALID_ARGUMENT, "Chunked child count != nchunks + 1");
+    const int w = width(a);
+    // Fast path: every chunk is Dict(codes = BitPacked, no patches, offset 0, same T/W/VW) ->
+    // one grouped launch over all chunks.
+    bool grouped = n > 1;
+    int T = 0, W = -1, vw = 0;
+    for (uint64_t i = 0; i < n && grouped; i++) {
+        const vxg_array& c = a.children[i + 1];
+        const vxg_array* codes = child(c, 1);
+        const vxg_array* values = child(c, 0);
+        if (c.encoding != VXG_ENC_DICT || !codes || !values || codes->encoding != VXG_ENC_FL_BITPACKED ||
+            codes->meta.bitpacked.has_patches || codes->meta.bitpacked.offset != 0 ||
+            codes->meta.bitpacked.bit_width > kDictFusedMaxW || values->encoding != VXG_ENC_PRIMITIVE) {
+            grouped = false;
+            break;
+        }
+        const int t = 8 * width(*codes), ww = codes->meta.bitpacked.bit_width, v = width(*values);
+        if (i == 0) { T = t; W = ww; vw = v; }
+        else if (t != T || ww != W || v != vw) grouped = false;
+    }
+    uint64_t off = 0;
+    if (grouped) {
+        std::vector<DictChunkDev> h(n);
+        uint64_t groups = 0;
+        for (uint64_t i = 0; i < n; i++) {
+            const vxg_array& c = a.children[i + 1];
+            const vxg_array& codes = *child(c, 1);
+            const vxg_array& values = *child(c, 0);
+            const uint64_t nblk = (c.len + 1023) / 1024;
+            if (W > 0 && codes.buffers[0].len != nblk * 128ull * W)
+                return set_error(VXG_ERR_INVALID_ARGUMENT, "Chunk packed length mismatch");
+            h[i] = DictChunkDev{static_cast<const uint8_t*>(codes.buffers[0].ptr), values.buffers[0].ptr,
+                                static_cast<uint8_t*>(dst) + off * w, nblk, c.len, values.len, groups};
+            if (((off * w) & 15) != 0) { grouped = false; break; }
+            groups += (nblk + 31) / 32;
+            off += c.len;
+        }
+        if (grouped) {
+            void* d;
+            VXG_TRY(temp(n * sizeof(DictChunkDev), &d));
+            VXG_TRY(hip_check(hipMemcpyAsync(d, h.data(), n * sizeof(DictChunkDev), hipMemcpyHostToDevice, s_),
+                              "chunk table upload"));
+            // the host table must stay alive until the async copy has consumed it
+            VXG_TRY(hip_check(hipStreamSynchronize(s_), "chunk table sync"));
+            return launch_fl_unpack_dict_chunks(T, W, vw, static_cast<DictChunkDev*>(d), uint32_t(n), groups,
+                                                ctx_->c.err_word, s_);
+        }
+        off = 0;
+    }
+    for (uint64_t i = 0; i < n; i++) {
+        const vxg_array& c = a.children[i + 1];
+        uint8_t* slice = static_cast<uint8_t*>(dst) + off * w;
+        if ((reinterpret_cast<uintptr_t>(slice) & 15) == 0) {
+            VXG_TRY(decode_into(c, slice));
+        } else {
+            const void* p;
+            VXG_TRY(view_primitive(c, &p));
+            VXG_TRY(hip_check(hipMemcpyAsync(slice, p, c.len * w, hipMemcpyDeviceToDevice, s_), "chunk copy"));
+        }
+        off += c.len;
+    }
+    if (off != a.len) return set_error(VXG_ERR_INVALID_ARGUMENT, "Chunked len != sum of chunk lens");
+    return VXG_OK;
+}
+
+vxg_status Planner::decode_alprd(const vxg_array& a, void* dst) {
+    // alp_rd/array.rs:179-235 -> alp_rd/mod.rs:260-301
+    const vxg_array* left = child(a, 0);
+    const vxg_array* right = child(a, 1);
+    if (!left || !right) return set_error(VXG_ERR_INVALID_ARGUMENT, "ALPRDArray needs left/right parts");
+    if (left->ptype != VXG_U16) return set_error(VXG_ERR_MISMATCHED_TYPES, "ALP-RD left parts must be u16");
+    const void *pl, *pr;
+    VXG_TRY(view_primitive(*left, &pl));
+    VXG_TRY(view_primitive(*right, &pr));
+    const void* pos = nullptr;
+    const void* exc = nullptr;
+    uint64_t n_exc = 0, pos_off = 0;
+    int pw = 8;
+    bool psg = false;
+    if (a.meta.alprd.has_exceptions) {
+        const vxg_array* sp = child(a, 2);
+        if (!sp || sp->encoding != VXG_ENC_SPARSE)
+            return set_error(VXG_ERR_INVALID_ARGUMENT, "left_parts_exceptions must be SparseArray encoded");
+        const vxg_array* si = child(*sp, 0);
+        const vxg_array* sv = child(*sp, 1);
+        VXG_TRY(view_primitive(*si, &pos));
+        VXG_TRY(view_primitive(*sv, &exc));
+        n_exc = si->len;
+        pos_off = sp->meta.sparse.indices_offset;
+        pw = width(*si);
+        psg = ptype_is_signed(si->ptype);
+    }
+    return launch_alprd(a.ptype, static_cast<const uint16_t*>(pl), a.meta.alprd.dict, a.meta.alprd.dict_len,
+                        a.meta.alprd.right_bit_width, pr, a.len, pos, pw, psg, pos_off,
+                        static_cast<const uint16_t*>(exc), n_exc, dst, ctx_->c.err_word, s_);
+}
+
+vxg_status Planner::decode_sparse_values(const vxg_array& a, void* dst) {
+    // array/sparse/flatten.rs:68-98: fill (null fill -> default 0), then scatter values.
+    uint8_t fill[16] = {0};
+    if (!a.meta.sparse.fill_is_null) std::memcpy(fill, a.meta.sparse.fill, 16);
+    VXG_TRY(launch_fill(width(a), fill, a.len, dst, s_));
+    UnpackArgs plain{};
+    plain.err = ctx_->c.err_word;
+    return apply_sparse_patches(a, 8 * width(a), Epi::Plain, 0, plain, dst, a.len);
+}
+
+vxg_status Planner::decode_into(const vxg_array& a, void* dst) {
+    if (!is_primitive_dtype(a)) return set_error(VXG_ERR_MISMATCHED_TYPES, "expected a primitive dtype");
+    const int w = width(a);
+    if (w == 0) return set_error(VXG_ERR_NOT_IMPLEMENTED, "unsupported ptype");
+    switch (a.encoding) {
+    case VXG_ENC_PRIMITIVE: {
+        const void* p;
+        VXG_TRY(view_primitive(a, &p));
+        if (p != dst && a.len)
+            VXG_TRY(hip_check(hipMemcpyAsync(dst, p, a.len * w, hipMemcpyDeviceToDevice, s_), "primitive copy"));
+        return VXG_OK;
+    }
+    case VXG_ENC_FL_BITPACKED:
+        return decode_bitpacked(a, Epi::Plain, 0, UnpackArgs{}, dst);
+    case VXG_ENC_FL_FOR: {
+        // for/mod.rs:105-109 -> for/compress.rs:86-98
+        const vxg_array* enc = child(a, 0);
+        if (!enc) return set_error(VXG_ERR_INVALID_ARGUMENT, "FoRArray is missing encoded child array");
+        if (!ptype_is_int(a.ptype)) return set_error(VXG_ERR_MISMATCHED_TYPES, "FoR needs an integer ptype");
+        if (enc->encoding == VXG_ENC_FL_BITPACKED && width(*enc) == w) {
+            UnpackArgs ua{};
+            ua.reference = a.meta.for_.reference;
+            ua.shift = a.meta.for_.shift;
+            return decode_bitpacked(*enc, Epi::For, 0, ua, dst);
+        }
+        VXG_TRY(decode_into(*enc, dst));
+        return launch_for(w, dst, a.len, a.meta.for_.reference, a.meta.for_.shift, false, dst, s_);
+    }
+    case VXG_ENC_ZIGZAG: {
+        const vxg_array* enc = child(a, 0);
+        if (!enc) return set_error(VXG_ERR_INVALID_ARGUMENT, "ZigZagArray is missing encoded child");
+        if (!ptype_is_signed(a.ptype)) return set_error(VXG_ERR_MISMATCHED_TYPES, "ZigZag decodes to signed ints");
+        if (enc->encoding == VXG_ENC_FL_BITPACKED && width(*enc) == w)
+            return decode_bitpacked(*enc, Epi::ForZigZag, 0, UnpackArgs{}, dst);
+        VXG_TRY(decode_into(*enc, dst));
+        return launch_zigzag(w, dst, a.len, dst, s_);
+    }
+    case VXG_ENC_ALP:
+        return decode_alp(a, dst);
+    case VXG_ENC_ALP_RD:
+        return decode_alprd(a, dst);
+    case VXG_ENC_DICT:
+        return decode_dict_primitive(a, dst);
+    case VXG_ENC_FL_DELTA: {
+        // delta/mod.rs:237 -> delta/compress.rs:100-166
+        const vxg_array* bases = child(a, 0);
+        const vxg_array* deltas = child(a, 1);
+        if (!bases || !deltas) return set_error(VXG_ERR_INVALID_ARGUMENT, "DeltaArray needs bases and deltas");
+        const int T = 8 * w, lanes = 1024 / T;
+        const uint64_t nd = deltas->len;
+        if (bases->len != (nd / 1024) * lanes + (nd % 1024 ? 1 : 0))
+            return set_error(VXG_ERR_INVALID_ARGUMENT, "DeltaArray: bases.len() != expected_bases_len");
+        if (a.meta.delta.offset >= 1024 || a.meta.delta.offset + a.len > nd)
+            return set_error(VXG_ERR_INVALID_ARGUMENT, "DeltaArray: offset/len out of range");
+        const void *pb, *pd;
+        VXG_TRY(view_primitive(*bases, &pb));
+        VXG_TRY(view_primitive(*deltas, &pd));
+        return launch_delta(w, pb, pd, nd, a.meta.delta.offset, a.len, dst, s_);
+    }
+    case VXG_ENC_RUN_END: {
+        // runend/array.rs:191-197 -> runend/compress.rs:95-148
+        const vxg_array* ends = child(a, 0);
+        const vxg_array* values = child(a, 1);
+        if (!ends || !values) return set_error(VXG_ERR_INVALID_ARGUMENT, "RunEndArray needs ends and values");
+        if (ends->len != values->len) return set_error(VXG_ERR_INVALID_ARGUMENT, "RunEnd ends/values length mismatch");
+        const void *pe, *pv;
+        VXG_TRY(view_primitive(*ends, &pe));
+        VXG_TRY(view_primitive(*values, &pv));
+        return launch_runend(w, pv, width(*ends), pe, ends->len, a.meta.runend.offset, a.len, dst,
+                             ctx_->c.err_word, s_);
+    }
+    case VXG_ENC_SPARSE:
+        return decode_sparse_values(a, dst);
+    case VXG_ENC_CONSTANT: {
+        uint8_t sc[16] = {0};
+        if (!a.meta.constant.is_null) std::memcpy(sc, a.meta.constant.scalar, 16);
+        return launch_fill(w, sc, a.len, dst, s_);
+    }
+    case VXG_ENC_CHUNKED:
+        return decode_chunked_primitive(a, dst);
+    default:
+        return set_error(VXG_ERR_NOT_IMPLEMENTED,
+                         "no GPU canonicalize for encoding id " + std::to_string(a.encoding));
+    }
+}
+
+// Where does the validity of `a` come from?  kind: 0 = no nulls, 1 = all invalid,
+// 2 = Bool child array `node` (canonical bitmap buffer 0).
+vxg_status Planner::validity_source(const vxg_array& a, const vxg_array** node, int* kind) {
+    *node = nullptr;
+    *kind = 0;
+    auto from_meta = [&](uint32_t child_idx) -> vxg_status {
+        switch (a.validity) {
+        case VXG_VALIDITY_NON_NULLABLE:
+        case VXG_VALIDITY_ALL_VALID: return VXG_OK;
+        case VXG_VALIDITY_ALL_INVALID: *kind = 1; return VXG_OK;
+        default: {
+            const vxg_array* v = child(a, child_idx);
+            if (!v || v->encoding != VXG_ENC_BOOL)
+                return set_error(VXG_ERR_NOT_IMPLEMENTED, "validity child must be a canonical BoolArray");
+            *node = v;
+            *kind = 2;
+            return VXG_OK;
+        }
+        }
+    };
+    switch (a.encoding) {
+    case VXG_ENC_PRIMITIVE: return from_meta(0);
+    case VXG_ENC_FL_BITPACKED: return from_meta(a.meta.bitpacked.has_patches ? 1 : 0);
+    case VXG_ENC_FL_DELTA: return from_meta(2);
+    case VXG_ENC_RUN_END: return from_meta(2);
+    case VXG_ENC_VARBIN: return from_meta(2);
+    case VXG_ENC_FL_FOR:
+    case VXG_ENC_ZIGZAG:
+    case VXG_ENC_ALP: return child(a, 0) ? validity_source(*child(a, 0), node, kind) : VXG_OK;
+    case VXG_ENC_ALP_RD: return child(a, 0) ? validity_source(*child(a, 0), node, kind) : VXG_OK;
+    case VXG_ENC_FSST: return child(a, 2) ? validity_source(*child(a, 2), node, kind) : VXG_OK;
+    case VXG_ENC_CONSTANT: *kind = a.meta.constant.is_null ? 1 : 0; return VXG_OK;
+    case VXG_ENC_DICT: {
+        const vxg_array* v = child(a, 0);
+        if (!v) return VXG_OK;
+        VXG_TRY(validity_source(*v, node, kind));
+        if (*kind != 0) return set_error(VXG_ERR_NOT_IMPLEMENTED, "nullable dictionary values");
+        return VXG_OK;
+    }
+    case VXG_ENC_SPARSE:
+        if (a.meta.sparse.fill_is_null) { *kind = 3; *node = &a; }
+        return VXG_OK;
+    case VXG_ENC_CHUNKED: {
+        for (uint32_t i = 1; i < a.n_children; i++) {
+            const vxg_array* n2;
+            int k2;
+            VXG_TRY(validity_source(a.children[i], &n2, &k2));
+            if (k2 != 0) { *kind = 4; *node = &a; return VXG_OK; }
+        }
+        return VXG_OK;
+    }
+    default: return VXG_OK;
+    }
+}
+
+vxg_status Planner::validity_into(const vxg_array& a, void** bitmap) {
+    const vxg_array* node;
+    int kind;
+    VXG_TRY(validity_source(a, &node, &kind));
+    if (kind == 0) {  // no nulls: validity NULL (a caller-provided bitmap is left untouched)
+        *bitmap = nullptr;
+        return VXG_OK;
+    }
+    const uint64_t bytes = ((a.len + 31) / 32) * 4;
+    if (!*bitmap) VXG_TRY(hip_check(hipMalloc(bitmap, bytes ? bytes : 4), "validity alloc"));
+    VXG_TRY(hip_check(hipMemsetAsync(*bitmap, 0, bytes ? bytes : 4, s_), "validity memset"));
+    if (kind == 1) return VXG_OK;
+    if (kind == 2) {
+        const vxg_buffer* b = buf(*node, 0);
+        if (!b) return set_error(VXG_ERR_INVALID_ARGUMENT, "BoolArray without buffer");
+        return launch_copy_bits(*bitmap, 0, static_cast<const uint8_t*>(b->ptr),
+                                node->meta.boolean.first_byte_bit_offset, a.len, false, s_);
+    }
+    if (kind == 3) {  // Sparse with null fill: valid exactly at the indices (flatten.rs:82-93)
+        const vxg_array* idx = child(a, 0);
+        const void* pi;
+        VXG_TRY(view_primitive(*idx, &pi));
+        return launch_set_bits_at(*bitmap, pi, width(*idx), ptype_is_signed(idx->ptype),
+                                  a.meta.sparse.indices_offset, idx->len, a.len, s_);
+    }
+    // kind 4: chunked concatenation of chunk validities
+    uint64_t off = 0;
+    for (uint32_t i = 1; i < a.n_children; i++) {
+        const vxg_array& c = a.children[i];
+        const vxg_array* n2;
+        int k2;
+        VXG_TRY(validity_source(c, &n2, &k2));
+        if (k2 == 0) {
+            VXG_TRY(launch_copy_bits(*bitmap, off, nullptr, 0, c.len, true, s_));
+        } else if (k2 == 2) {
+            VXG_TRY(launch_copy_bits(*bitmap, off, static_cast<const uint8_t*>(n2->buffers[0].ptr),
+                                     n2->meta.boolean.first_byte_bit_offset, c.len, false, s_));
+        } else if (k2 != 1) {
+            void* sub = nullptr;
+            VXG_TRY(temp(((c.len + 31) / 32) * 4, &sub));
+            VXG_TRY(validity_into(c, &sub));
+            VXG_TRY(launch_copy_bits(*bitmap, off, static_cast<const uint8_t*>(sub), 0, c.len, false, s_));
+        }
+        off += c.len;
+    }
+    return VXG_OK;
+}
+
+vxg_status Planner::string_canonical(const vxg_array& a, vxg_canonical& out) {
+    out.kind = VXG_ENC_VARBINVIEW;
+    out.len = a.len;
+    out.dtype = a.dtype;
+    uint64_t vb, db;
+    VXG_TRY(canonical_size(a, vb, db));
+    if (!out.views) VXG_TRY(hip_check(hipMalloc(&out.views, vb ? vb : 16), "views alloc"));
+    if (!out.data) VXG_TRY(hip_check(hipMalloc(&out.data, db + 16), "data alloc"));
+    out.data_bytes = db;
+    VXG_TRY(validity_into(a, &out.validity));
+    if (a.encoding == VXG_ENC_VARBIN) {
+        // varbin/flatten.rs:10-17: views over the whole bytes buffer (block 0)
+        const vxg_array* offs = child(a, 0);
+        const vxg_array* bytes = child(a, 1);
+        const void *po, *pb;
+        VXG_TRY(view_primitive(*offs, &po));
+        VXG_TRY(view_primitive(*bytes, &pb));
+        if (db) VXG_TRY(hip_check(hipMemcpyAsync(out.data, pb, db, hipMemcpyDeviceToDevice, s_), "heap copy"));
+        return launch_varbin_views(static_cast<const uint8_t*>(out.data), width(*offs), po, a.len,
+                                   static_cast<const uint8_t*>(out.validity), static_cast<uint8_t*>(out.views), s_);
+    }
+    if (a.encoding == VXG_ENC_FSST) {
+        // fsst/canonical.rs:7-57
+        const vxg_array* sym = child(a, 0);
+        const vxg_array* slen = child(a, 1);
+        const vxg_array* codes = child(a, 2);
+        const vxg_array* ulen = child(a, 3);
+        if (!sym || !slen || !codes || !ulen || codes->encoding != VXG_ENC_VARBIN)
+            return set_error(VXG_ERR_INVALID_ARGUMENT, "FSSTArray needs symbols, lengths, VarBin codes, lengths");
+        const void *psym, *pslen, *pco, *pcb, *pul;
+        VXG_TRY(view_primitive(*sym, &psym));
+        VXG_TRY(view_primitive(*slen, &pslen));
+        VXG_TRY(view_primitive(*child(*codes, 0), &pco));
+        VXG_TRY(view_primitive(*child(*codes, 1), &pcb));
+        VXG_TRY(view_primitive(*ulen, &pul));
+        void* scratch;
+        VXG_TRY(temp(fsst_scratch_bytes(a.len), &scratch));
+        return launch_fsst(static_cast<const uint64_t*>(psym), static_cast<const uint8_t*>(pslen),
+                           unsigned(sym->len), static_cast<const uint8_t*>(pcb), width(*child(*codes, 0)), pco,
+                           width(*ulen), ptype_is_signed(ulen->ptype), pul, a.len,
+                           static_cast<const uint8_t*>(out.validity), scratch, static_cast<uint8_t*>(out.data),
+                           static_cast<uint8_t*>(out.views), s_);
+    }
+    if (a.encoding == VXG_ENC_DICT) {
+        // Dict over string values: take on the 16-B views, buffers kept (varbinview/compute.rs:68-76)
+        const vxg_array* values = child(a, 0);
+        const vxg_array* codes = child(a, 1);
+        vxg_canonical vc{};
+        VXG_TRY(canonical(*values, vc));
+        temps_.push_back(vc.views);
+        temps_.push_back(vc.data);
+        if (vc.validity) temps_.push_back(vc.validity);
+        if (vc.data_bytes)
+            VXG_TRY(hip_check(hipMemcpyAsync(out.data, vc.data, vc.data_bytes, hipMemcpyDeviceToDevice, s_), "dict heap"));
+        if (codes->encoding == VXG_ENC_FL_BITPACKED && codes->meta.bitpacked.bit_width <= kDictFusedMaxW) {
+            UnpackArgs ua{};
+            ua.dict = vc.views;
+            ua.dict_len = values->len;
+            return decode_bitpacked(*codes, Epi::Dict, 16, ua, out.views);
+        }
+        const void* pc;
+        VXG_TRY(view_primitive(*codes, &pc));
+        return launch_take(16, vc.views, values->len, width(*codes), pc, a.len, out.views, ctx_->c.err_word, s_);
+    }
+    return set_error(VXG_ERR_NOT_IMPLEMENTED, "string canonicalize for encoding id " + std::to_string(a.encoding));
+}
+
+vxg_status Planner::canonical_size(const vxg_array& a, uint64_t& vb, uint64_t& db) {
+    vb = db = 0;
+    if (a.dtype == VXG_DTYPE_PRIMITIVE) {
+        vb = a.len * width(a);
+        return VXG_OK;
+    }
+    if (a.dtype != VXG_DTYPE_UTF8 && a.dtype != VXG_DTYPE_BINARY)
+        return set_error(VXG_ERR_NOT_IMPLEMENTED, "canonical size for this dtype");
+    vb = a.len * 16;
+    if (a.encoding == VXG_ENC_VARBIN) {
+        const vxg_array* bytes = child(a, 1);
+        db = bytes ? bytes->len : 0;
+        return VXG_OK;
+    }
+    if (a.encoding == VXG_ENC_FSST) {
+        const vxg_array* ulen = child(a, 3);
+        if (!ulen) return set_error(VXG_ERR_INVALID_ARGUMENT, "FSST lengths child missing");
+        const void* pul;
+        VXG_TRY(view_primitive(*ulen, &pul));
+        void* d;
+        VXG_TRY(temp(8, &d));
+        VXG_TRY(launch_sum(pul, width(*ulen), ptype_is_signed(ulen->ptype), ulen->len, d, s_));
+        uint64_t h = 0;
+        VXG_TRY(hip_check(hipMemcpyAsync(&h, d, 8, hipMemcpyDeviceToHost, s_), "sum readback"));
+        VXG_TRY(hip_check(hipStreamSynchronize(s_), "sum sync"));
+        db = h;
+        return VXG_OK;
+    }
+    if (a.encoding == VXG_ENC_DICT) {
+        uint64_t v2, d2;
+        VXG_TRY(canonical_size(*child(a, 0), v2, d2));
+        db = d2;
+        return VXG_OK;
+    }
+    return set_error(VXG_ERR_NOT_IMPLEMENTED, "canonical size for encoding id " + std::to_string(a.encoding));
+}
+
+vxg_status Planner::canonical(const vxg_array& a, vxg_canonical& out) {
+    out.len = a.len;
+    out.dtype = a.dtype;
+    out.ptype = a.ptype;
+    if (a.dtype == VXG_DTYPE_UTF8 || a.dtype == VXG_DTYPE_BINARY) return string_canonical(a, out);
+    if (a.dtype != VXG_DTYPE_PRIMITIVE)
+        return set_error(VXG_ERR_NOT_IMPLEMENTED, "canonicalize supports primitive and utf8/binary dtypes");
+    out.kind = VXG_ENC_PRIMITIVE;
+    out.values_bytes = a.len * width(a);
+    if (!out.values)
+        VXG_TRY(hip_check(hipMalloc(&out.values, out.values_bytes ? out.values_bytes : 16), "values alloc"));
+    VXG_TRY(decode_into(a, out.values));
+    return validity_into(a, &out.validity);
+}
+
+}  // namespace
+
+// ===================================================================================
+// C ABI
+// ===================================================================================
+extern "C" {
+
+int vxg_abi_version(void) { return VXG_ABI_VERSION; }
+
+const char* vxg_last_error(void) { return g_last_error.c_str(); }
+
+vxg_status vxg_open(int device, vxg_ctx** out) {
+    if (!out) return set_error(VXG_ERR_INVALID_ARGUMENT, "null out");
+    int n = 0;
+    VXG_TRY(hip_check(hipGetDeviceCount(&n), "hipGetDeviceCount"));
+    if (device < 0 || device >= n) return set_error(VXG_ERR_INVALID_ARGUMENT, "no such device");
+    VXG_TRY(hip_check(hipSetDevice(device), "hipSetDevice"));
+    auto* c = new vxg_ctx();
+    c->c.device = device;
+    hipError_t e = hipMalloc(&c->c.err_word, 16);
+    if (e == hipSuccess) e = hipMemset(c->c.err_word, 0, 16);
+    if (e != hipSuccess) {
+        delete c;
+        return hip_check(e, "error word");
+    }
+    *out = c;
+    return VXG_OK;
+}
+
+vxg_status vxg_close(vxg_ctx* ctx) {
+    if (!ctx) return VXG_OK;
+    (void)hipSetDevice(ctx->c.device);
+    (void)hipFree(ctx->c.err_word);
+    delete ctx;
+    return VXG_OK;
+}
+
+vxg_status vxg_alloc(vxg_ctx* ctx, uint64_t bytes, void** dptr) {
+    VXG_TRY(use_device(ctx));
+    return hip_check(hipMalloc(dptr, bytes ? bytes : 16), "hipMalloc");
+}
+
+vxg_status vxg_free(vxg_ctx* ctx, void* dptr) {
+    VXG_TRY(use_device(ctx));
+    return hip_check(hipFree(dptr), "hipFree");
+}
+
+vxg_status vxg_memcpy_h2d(vxg_ctx* ctx, void* dst, const void* src, uint64_t bytes, void* stream) {
+    VXG_TRY(use_device(ctx));
+    return hip_check(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, S(stream)), "h2d");
+}
+
+vxg_status vxg_memcpy_d2h(vxg_ctx* ctx, void* dst, const void* src, uint64_t bytes, void* stream) {
+    VXG_TRY(use_device(ctx));
+    return hip_check(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, S(stream)), "d2h");
+}
+
+vxg_status vxg_stream_sync(vxg_ctx* ctx, void* stream) {
+    VXG_TRY(use_device(ctx));
+    VXG_TRY(hip_check(hipStreamSynchronize(S(stream)), "hipStreamSynchronize"));
+    uint32_t err = 0;
+    VXG_TRY(hip_check(hipMemcpy(&err, ctx->c.err_word, 4, hipMemcpyDeviceToHost), "error word readback"));
+    if (err) {
+        VXG_TRY(hip_check(hipMemset(ctx->c.err_word, 0, 4), "error word reset"));
+        if (err & kErrTakeOOB) return set_error(VXG_ERR_OUT_OF_BOUNDS, "take: index out of bounds");
+        if (err & kErrPatchOOB) return set_error(VXG_ERR_OUT_OF_BOUNDS, "patch index out of bounds");
+        if (err & kErrRunEnd) return set_error(VXG_ERR_INVALID_ARGUMENT, "RunEnd ends do not cover the array");
+    }
+    return VXG_OK;
+}
+
+vxg_status vxg_canonical_size(vxg_ctx* ctx, const vxg_array* a, uint64_t* values_bytes, uint64_t* data_bytes) {
+    VXG_TRY(use_device(ctx));
+    if (!a) return set_error(VXG_ERR_INVALID_ARGUMENT, "null array");
+    Planner p(ctx, nullptr);
+    uint64_t vb = 0, db = 0;
+    VXG_TRY(p.canonical_size(*a, vb, db));
+    if (values_bytes) *values_bytes = vb;
+    if (data_bytes) *data_bytes = db;
+    return VXG_OK;
+}
+
+vxg_status vxg_canonicalize(vxg_ctx* ctx, const vxg_array* a, vxg_canonical* out, void* stream) {
+    VXG_TRY(use_device(ctx));
+    if (!a || !out) return set_error(VXG_ERR_INVALID_ARGUMENT, "null array/out");
+    Planner p(ctx, S(stream));
+    return p.canonical(*a, *out);
+}
+
+static int unsigned_T(int ptype) { return 8 * ptype_width(ptype); }
+
+vxg_status vxg_bitunpack(vxg_ctx* ctx, int ptype, unsigned bit_width, unsigned offset, uint64_t len,
+                         const void* packed, uint64_t packed_bytes, void* out, void* stream) {
+    VXG_TRY(use_device(ctx));
+    if (!ptype_is_int(ptype)) return set_error(VXG_ERR_MISMATCHED_TYPES, "BitPacked needs an integer ptype");
+    return bitunpack_common(ctx, unsigned_T(ptype), bit_width, offset, len, packed, packed_bytes, Epi::Plain, 0,
+                            UnpackArgs{}, out, stream);
+}
+
+vxg_status vxg_bitunpack_for(vxg_ctx* ctx, int ptype, unsigned bit_width, unsigned offset, uint64_t len,
+                             const void* packed, uint64_t packed_bytes, uint64_t reference, unsigned shift,
+                             int zigzag, void* out, void* stream) {
+    VXG_TRY(use_device(ctx));
+    if (!ptype_is_int(ptype)) return set_error(VXG_ERR_MISMATCHED_TYPES, "FoR needs an integer ptype");
+    UnpackArgs a{};
+    a.reference = reference;
+    a.shift = shift;
+    return bitunpack_common(ctx, unsigned_T(ptype), bit_width, offset, len, packed, packed_bytes,
+                            zigzag ? Epi::ForZigZag : Epi::For, 0, a, out, stream);
+}
+
+vxg_status vxg_bitunpack_alp(vxg_ctx* ctx, int float_ptype, unsigned bit_width, unsigned offset, uint64_t len,
+                             const void* packed, uint64_t packed_bytes, uint64_t for_reference,
+                             unsigned for_shift, unsigned e, unsigned f, void* out, void* stream) {
+    VXG_TRY(use_device(ctx));
+    const bool f32 = float_ptype == VXG_F32;
+    if (!f32 && float_ptype != VXG_F64) return set_error(VXG_ERR_MISMATCHED_TYPES, "ALP decodes to f32/f64");
+    if ((f32 && (e > 10 || f > 10)) || (!f32 && (e > 23 || f > 23)))
+        return set_error(VXG_ERR_INVALID_ARGUMENT, "ALP exponents out of range");
+    UnpackArgs a{};
+    a.reference = for_reference;
+    a.shift = for_shift;
+    a.alp_a = f32 ? double(kF10f[f]) : kF10d[f];
+    a.alp_b = f32 ? double(kIF10f[e]) : kIF10d[e];
+    return bitunpack_common(ctx, f32 ? 32 : 64, bit_width, offset, len, packed, packed_bytes,
+                            f32 ? Epi::AlpF32 : Epi::AlpF64, 0, a, out, stream);
+}
+
+vxg_status vxg_bitunpack_dict(vxg_ctx* ctx, int codes_ptype, unsigned bit_width, unsigned offset, uint64_t len,
+                              const void* packed, uint64_t packed_bytes, const void* dict_values,
+                              uint64_t dict_len, unsigned value_width, void* out, void* stream) {
+    VXG_TRY(use_device(ctx));
+    if (!ptype_is_unsigned(codes_ptype)) return set_error(VXG_ERR_MISMATCHED_TYPES, "Dict codes must be unsigned");
+    if (bit_width > unsigned(kDictFusedMaxW))
+        return set_error(VXG_ERR_NOT_IMPLEMENTED, "fused dict decode supports code widths <= 16");
+    UnpackArgs a{};
+    a.dict = dict_values;
+    a.dict_len = dict_len;
+    return bitunpack_common(ctx, unsigned_T(codes_ptype), bit_width, offset, len, packed, packed_bytes, Epi::Dict,
+                            int(value_width), a, out, stream);
+}
+
+vxg_status vxg_bitunpack_dict_chunks(vxg_ctx* ctx, int codes_ptype, unsigned bit_width, unsigned value_width,
+                                     const vxg_dict_chunk* chunks_host, uint32_t n_chunks, void* stream) {
+    VXG_TRY(use_device(ctx));
+    if (!ptype_is_unsigned(codes_ptype)) return set_error(VXG_ERR_MISMATCHED_TYPES, "Dict codes must be unsigned");
+    if (bit_width > unsigned(kDictFusedMaxW))
+        return set_error(VXG_ERR_NOT_IMPLEMENTED, "fused dict decode supports code widths <= 16");
+    std::vector<DictChunkDev> h(n_chunks);
+    uint64_t groups = 0;
+    for (uint32_t i = 0; i < n_chunks; i++) {
+        const vxg_dict_chunk& c = chunks_host[i];
+        if (c.n_blocks != (c.len + 1023) / 1024)
+            return set_error(VXG_ERR_INVALID_ARGUMENT, "chunk n_blocks != ceil(len/1024)");
+        if ((reinterpret_cast<uintptr_t>(c.out) | reinterpret_cast<uintptr_t>(c.packed)) & 15)
+            return set_error(VXG_ERR_INVALID_ARGUMENT, "chunk buffers must be 16-byte aligned");
+        h[i] = DictChunkDev{static_cast<const uint8_t*>(c.packed), c.dict_values, c.out, c.n_blocks, c.len,
+                            c.dict_len, groups};
+        groups += (c.n_blocks + 31) / 32;
+    }
+    void* d;
+    VXG_TRY(hip_check(hipMallocAsync(&d, n_chunks * sizeof(DictChunkDev) + 16, S(stream)), "chunk table"));
+    VXG_TRY(hip_check(hipMemcpyAsync(d, h.data(), n_chunks * sizeof(DictChunkDev), hipMemcpyHostToDevice,
+                                     S(stream)), "chunk table upload"));
+    VXG_TRY(hip_check(hipStreamSynchronize(S(stream)), "chunk table sync"));
+    vxg_status st = launch_fl_unpack_dict_chunks(unsigned_T(codes_ptype), int(bit_width), int(value_width),
+                                                 static_cast<DictChunkDev*>(d), n_chunks, groups,
+                                                 ctx->c.err_word, S(stream));
+    (void)hipFreeAsync(d, S(stream));
+    return st;
+}
+
+vxg_status vxg_patch(vxg_ctx* ctx, int ptype, void* out, uint64_t out_len, int indices_ptype, const void* indices,
+                     uint64_t indices_offset, const void* values, uint64_t n_patches, void* stream) {
+    VXG_TRY(use_device(ctx));
+    const int w = ptype_width(ptype);
+    if (!w || !ptype_is_int(indices_ptype)) return set_error(VXG_ERR_INVALID_ARGUMENT, "bad ptype");
+    UnpackArgs a{};
+    a.err = ctx->c.err_word;
+    return launch_patch(0, ptype_width(indices_ptype), ptype_is_signed(indices_ptype), Epi::Plain, 8 * w, out,
+                        out_len, indices, indices_offset, values, n_patches, a, S(stream));
+}
+
+vxg_status vxg_for_decode(vxg_ctx* ctx, int ptype, const void* in, uint64_t n, uint64_t reference,
+                          unsigned shift, void* out, void* stream) {
+    VXG_TRY(use_device(ctx));
+    if (!ptype_is_int(ptype)) return set_error(VXG_ERR_MISMATCHED_TYPES, "FoR needs an integer ptype");
+    return launch_for(ptype_width(ptype), in, n, reference, shift, false, out, S(stream));
+}
+
+vxg_status vxg_zigzag_decode(vxg_ctx* ctx, int out_ptype, const void* in, uint64_t n, void* out, void* stream) {
+    VXG_TRY(use_device(ctx));
+    if (!ptype_is_signed(out_ptype)) return set_error(VXG_ERR_MISMATCHED_TYPES, "ZigZag decodes to signed ints");
+    return launch_zigzag(ptype_width(out_ptype), in, n, out, S(stream));
+}
+
+vxg_status vxg_alp_decode(vxg_ctx* ctx, int float_ptype, const void* encoded, uint64_t n, unsigned e, unsigned f,
+                          void* out, void* stream) {
+    VXG_TRY(use_device(ctx));
+    const bool f32 = float_ptype == VXG_F32;
+    if ((f32 && (e > 10 || f > 10)) || (!f32 && (e > 23 || f > 23)))
+        return set_error(VXG_ERR_INVALID_ARGUMENT, "ALP exponents out of range");
+    return launch_alp(float_ptype, encoded, n, f32 ? double(kF10f[f]) : kF10d[f],
+                      f32 ? double(kIF10f[e]) : kIF10d[e], out, S(stream));
+}
+
+vxg_status vxg_alprd_decode(vxg_ctx* ctx, int float_ptype, const uint16_t* left_codes, const uint16_t* dict_host,
+                            unsigned dict_len, unsigned right_bw, const void* right, uint64_t n,
+                            const uint64_t* exc_pos, const uint16_t* exc_vals, uint64_t n_exc, void* out,
+                            void* stream) {
+    VXG_TRY(use_device(ctx));
+    if (dict_len > 8) return set_error(VXG_ERR_INVALID_ARGUMENT, "ALP-RD dictionary holds at most 8 entries");
+    return launch_alprd(float_ptype, left_codes, dict_host, dict_len, right_bw, right, n, exc_pos, 8, false, 0,
+                        exc_vals, n_exc, out, ctx->c.err_word, S(stream));
+}
+
+vxg_status vxg_take(vxg_ctx* ctx, unsigned value_width, const void* values, uint64_t n_values, int codes_ptype,
+                    const void* codes, uint64_t n, void* out, void* stream) {
+    VXG_TRY(use_device(ctx));
+    if (!ptype_is_unsigned(codes_ptype)) return set_error(VXG_ERR_MISMATCHED_TYPES, "take indices must be unsigned");
+    return launch_take(int(value_width), values, n_values, ptype_width(codes_ptype), codes, n, out,
+                       ctx->c.err_word, S(stream));
+}
+
+vxg_status vxg_delta_decode(vxg_ctx* ctx, int ptype, const void* bases, uint64_t n_bases, const void* deltas,
+                            uint64_t n_deltas, uint64_t offset, uint64_t len, void* out, void* stream) {
+    VXG_TRY(use_device(ctx));
+    const int w = ptype_width(ptype);
+    if (!ptype_is_unsigned(ptype)) return set_error(VXG_ERR_MISMATCHED_TYPES, "Delta decodes unsigned ints");
+    const uint64_t lanes = 1024 / (8 * w);
+    if (n_bases != (n_deltas / 1024) * lanes + (n_deltas % 1024 ? 1 : 0))
+        return set_error(VXG_ERR_INVALID_ARGUMENT, "DeltaArray: bases.len() != expected_bases_len");
+    if (offset + len > n_deltas) return set_error(VXG_ERR_INVALID_ARGUMENT, "offset + len > deltas len");
+    return launch_delta(w, bases, deltas, n_deltas, offset, len, out, S(stream));
+}
+
+vxg_status vxg_runend_decode(vxg_ctx* ctx, unsigned value_width, const void* values, int ends_ptype,
+                             const void* ends, uint64_t n_runs, uint64_t offset, uint64_t len, void* out,
+                             void* stream) {
+    VXG_TRY(use_device(ctx));
+    if (!ptype_is_int(ends_ptype)) return set_error(VXG_ERR_MISMATCHED_TYPES, "RunEnd ends must be integers");
+    return launch_runend(int(value_width), values, ptype_width(ends_ptype), ends, n_runs, offset, len, out,
+                         ctx->c.err_word, S(stream));
+}
+
+uint64_t vxg_fsst_scratch_bytes(uint64_t n) { return fsst_scratch_bytes(n); }
+
+vxg_status vxg_fsst_decode(vxg_ctx* ctx, const uint64_t* symbols, const uint8_t* sym_lens, unsigned n_symbols,
+                           const uint8_t* code_bytes, int offs_ptype, const void* code_offsets, int lens_ptype,
+                           const void* lens, uint64_t n, const uint8_t* validity, void* scratch, uint8_t* heap,
+                           uint8_t* views, void* stream) {
+    VXG_TRY(use_device(ctx));
+    if (!ptype_is_int(offs_ptype) || !ptype_is_int(lens_ptype))
+        return set_error(VXG_ERR_MISMATCHED_TYPES, "FSST offsets/lengths must be integers");
+    return launch_fsst(symbols, sym_lens, n_symbols, code_bytes, ptype_width(offs_ptype), code_offsets,
+                       ptype_width(lens_ptype), ptype_is_signed(lens_ptype), lens, n, validity, scratch, heap, views,
+                       S(stream));
+}
+
+vxg_status vxg_fill(vxg_ctx* ctx, unsigned value_width, const void* scalar_host, uint64_t n, void* out,
+                    void* stream) {
+    VXG_TRY(use_device(ctx));
+    uint8_t sc[16] = {0};
+    if (value_width > 16) return set_error(VXG_ERR_INVALID_ARGUMENT, "value width > 16");
+    std::memcpy(sc, scalar_host, value_width);
+    return launch_fill(int(value_width), sc, n, out, S(stream));
+}
+
+}  // extern "C"

@@ -1,0 +1,348 @@
+// fl_unpack_impl.hpp — K1: FastLanes bit-unpack for CDNA4 (gfx950) with fused epilogues.
+//
+// Restates fastlanes 0.1.8 `BitPacking::unchecked_unpack` as used by
+// encodings/fastlanes/src/bitpacking/compress.rs:209-273 (unpack_primitive), fused with the
+// cascades the reference runs as separate materialised passes:
+//   FoR       for/compress.rs:100-117           out = (v << shift) wrapping_add reference
+//   ZigZag    zigzag/compress.rs:35-57          out = (u >> 1) ^ -(u & 1)
+//   ALP       alp/mod.rs:161-163, compress.rs:98-106   out = ((float)enc * F10[f]) * IF10[e]
+//   Dict      dict/array.rs:68-73 -> primitive/compute/take.rs:58-67   out = values[code]
+//
+// Work decomposition (MI355X-first):
+//   * A FastLanes block (1024 values of T bits) stores W "word rows" of 128 bytes each
+//     (word w of lane l at packed[l + LANES*w]).  Every word row is 1024 bits for every T.
+//   * 8 threads own one block; thread t owns byte slice [16t, 16t+16) of every word row,
+//     i.e. 16/sizeof(T) adjacent lanes.  It issues W independent 16-byte loads (one
+//     global_load_dwordx4 per word row; 8 threads = one full 128-byte line) and keeps them in
+//     VGPRs for the whole block: every packed byte is read from HBM exactly once.
+//   * Rows are extracted lane-parallel inside 32-bit (T<=32) or 64-bit (T=64) registers
+//     (SWAR: T-bit lanes never leak because every shift is followed by a per-lane mask).
+//   * Row r of the thread's lanes lands at out[index(r, lane0) .. +16/sizeof(T)) — 16
+//     contiguous bytes — so every output row is one global_store_dwordx4 and 8 threads write
+//     one full 128-byte line.  A 64-lane wave covers 8 blocks = 8 KiB of u32 output.
+//   * W and T are template parameters: all shifts/masks fold to immediates, the packed words
+//     stay in registers (no scratch), and the row loop is fully unrolled.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <type_traits>
+#include <utility>
+
+#include "vxg_internal.hpp"
+
+namespace vxg {
+
+template <int T> struct Fl;
+template <> struct Fl<8> {
+    using E = uint8_t;  using U = uint32_t;
+    static constexpr uint32_t rep(uint32_t m) { return m * 0x01010101u; }
+};
+template <> struct Fl<16> {
+    using E = uint16_t; using U = uint32_t;
+    static constexpr uint32_t rep(uint32_t m) { return m * 0x00010001u; }
+};
+template <> struct Fl<32> {
+    using E = uint32_t; using U = uint32_t;
+    static constexpr uint32_t rep(uint32_t m) { return m; }
+};
+template <> struct Fl<64> {
+    using E = uint64_t; using U = uint64_t;
+    static constexpr uint64_t rep(uint64_t m) { return m; }
+};
+
+template <typename U> __host__ __device__ constexpr U low_mask(int bits) {
+    return bits >= int(8 * sizeof(U)) ? ~U(0) : ((U(1) << bits) - U(1));
+}
+
+template <int VW> struct VType;
+template <> struct VType<0> { using t = uint8_t; };  // placeholder for non-Dict epilogues
+template <> struct VType<1> { using t = uint8_t; };
+template <> struct VType<2> { using t = uint16_t; };
+template <> struct VType<4> { using t = uint32_t; };
+template <> struct VType<8> { using t = uint64_t; };
+template <> struct VType<16> { using t = uint4; };
+
+// 16 bytes of lane data held as NV words of U.
+template <int T> struct Vec16 {
+    using U = typename Fl<T>::U;
+    static constexpr int NV = 16 / sizeof(U);
+    U w[NV];
+    __device__ __forceinline__ typename Fl<T>::E elem(int j) const {
+        using E = typename Fl<T>::E;
+        if constexpr (T == 64) {
+            return w[j];
+        } else {
+            constexpr int PER = 32 / T;
+            return E((w[j / PER] >> ((j % PER) * T)) & low_mask<uint32_t>(T));
+        }
+    }
+};
+
+template <int T>
+__device__ __forceinline__ Vec16<T> load16(const uint8_t* p) {
+    Vec16<T> v;
+    uint4 q = *reinterpret_cast<const uint4*>(p);
+    static_assert(sizeof(v.w) == 16, "");
+    __builtin_memcpy(v.w, &q, 16);
+    return v;
+}
+
+// Extract row R of W-bit values from the register-resident word rows (SWAR over lanes).
+template <int T, int W, int R>
+__device__ __forceinline__ Vec16<T> extract_row(const Vec16<T>* p) {
+    using U = typename Fl<T>::U;
+    constexpr int NV = Vec16<T>::NV;
+    Vec16<T> v;
+    if constexpr (W == 0) {
+#pragma unroll
+        for (int k = 0; k < NV; k++) v.w[k] = 0;
+    } else if constexpr (W == T) {
+        v = p[R];
+    } else {
+        constexpr int start = R * W, word = start / T, shift = start % T;
+        if constexpr (shift + W <= T) {
+            constexpr U m = Fl<T>::rep(low_mask<U>(W));
+#pragma unroll
+            for (int k = 0; k < NV; k++) v.w[k] = (p[word].w[k] >> shift) & m;
+        } else {
+            constexpr int cur = T - shift;
+            constexpr U mlo = Fl<T>::rep(low_mask<U>(cur));
+            constexpr U mhi = Fl<T>::rep(low_mask<U>(W - cur));
+#pragma unroll
+            for (int k = 0; k < NV; k++)
+                v.w[k] = ((p[word].w[k] >> shift) & mlo) | ((p[word + 1].w[k] & mhi) << cur);
+        }
+    }
+    return v;
+}
+
+struct EpiParams {
+    uint64_t reference;
+    uint32_t shift;
+    double alp_a, alp_b;
+    const void* dict;
+    uint64_t dict_len;
+    uint32_t* err;
+};
+
+template <int T, Epi EPI, int VW> struct EpiOut {
+    using type = typename Fl<T>::E;
+};
+template <int T, int VW> struct EpiOut<T, Epi::AlpF32, VW> { using type = float; };
+template <int T, int VW> struct EpiOut<T, Epi::AlpF64, VW> { using type = double; };
+template <int T, int VW> struct EpiOut<T, Epi::Dict, VW> { using type = typename VType<VW>::t; };
+
+// Apply the epilogue to one element.
+template <int T, Epi EPI, int VW>
+__device__ __forceinline__ typename EpiOut<T, EPI, VW>::type apply_epi(typename Fl<T>::E e,
+                                                                      const EpiParams& ep) {
+    using E = typename Fl<T>::E;
+    if constexpr (EPI == Epi::Plain) {
+        return e;
+    } else if constexpr (EPI == Epi::For || EPI == Epi::ForZigZag) {
+        E v = E(E(e << ep.shift) + E(ep.reference));  // wrapping in T
+        if constexpr (EPI == Epi::ForZigZag) v = E((v >> 1) ^ E(E(0) - E(v & 1)));
+        return v;
+    } else if constexpr (EPI == Epi::AlpF32) {
+        static_assert(T == 32, "ALP f32 decodes i32");
+        E v = E(E(e << ep.shift) + E(ep.reference));
+        float x = float(int32_t(v));                 // v_cvt_f32_i32: RN
+        x = __fmul_rn(x, float(ep.alp_a));           // F10[f]
+        return __fmul_rn(x, float(ep.alp_b));        // IF10[e]
+    } else if constexpr (EPI == Epi::AlpF64) {
+        static_assert(T == 64, "ALP f64 decodes i64");
+        E v = E(E(e << ep.shift) + E(ep.reference));
+        double x = double(int64_t(v));               // exact hi*2^32 + lo, one RN rounding
+        x = __dmul_rn(x, ep.alp_a);
+        return __dmul_rn(x, ep.alp_b);
+    } else {  // Dict gather
+        using VT = typename VType<VW>::t;
+        uint64_t c = uint64_t(e);
+        if (c >= ep.dict_len) {
+            __hip_atomic_fetch_or(ep.err, kErrTakeOOB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            c = 0;
+        }
+        return static_cast<const VT*>(ep.dict)[c];
+    }
+}
+
+// Store N bytes (compile-time) from a register array using the widest aligned stores.
+template <int NBYTES>
+__device__ __forceinline__ void store_bytes(uint8_t* dst, const void* src) {
+    if constexpr (NBYTES >= 16) {
+#pragma unroll
+        for (int i = 0; i < NBYTES / 16; i++) {
+            uint4 q;
+            __builtin_memcpy(&q, static_cast<const uint8_t*>(src) + 16 * i, 16);
+            reinterpret_cast<uint4*>(dst)[i] = q;
+        }
+    } else if constexpr (NBYTES == 8) {
+        uint2 q; __builtin_memcpy(&q, src, 8); *reinterpret_cast<uint2*>(dst) = q;
+    } else if constexpr (NBYTES == 4) {
+        uint32_t q; __builtin_memcpy(&q, src, 4); *reinterpret_cast<uint32_t*>(dst) = q;
+    } else if constexpr (NBYTES == 2) {
+        uint16_t q; __builtin_memcpy(&q, src, 2); *reinterpret_cast<uint16_t*>(dst) = q;
+    } else {
+        *dst = *static_cast<const uint8_t*>(src);
+    }
+}
+
+// One output row R of this thread's 16-byte lane slice.
+template <int T, int W, Epi EPI, int VW, int R>
+__device__ __forceinline__ void process_row(const Vec16<T>* p, int lane0,
+                                            typename EpiOut<T, EPI, VW>::type* __restrict__ out,
+                                            int64_t out_base, bool full, uint64_t len,
+                                            const EpiParams& ep) {
+    using E = typename Fl<T>::E;
+    using O = typename EpiOut<T, EPI, VW>::type;
+    constexpr int EPV = 16 / int(sizeof(E));  // elements per 16-byte lane slice
+    const Vec16<T> v = extract_row<T, W, R>(p);
+    const int idx = fl_index(R, lane0);
+    if (full) {
+        O* dst = out + (out_base + idx);
+        if constexpr (EPI == Epi::Plain) {
+            store_bytes<16>(reinterpret_cast<uint8_t*>(dst), v.w);
+        } else {
+            O o[EPV];
+#pragma unroll
+            for (int j = 0; j < EPV; j++) o[j] = apply_epi<T, EPI, VW>(v.elem(j), ep);
+            store_bytes<EPV * int(sizeof(O))>(reinterpret_cast<uint8_t*>(dst), o);
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < EPV; j++) {
+            const int64_t o = out_base + idx + j;
+            if (o >= 0 && uint64_t(o) < len) out[o] = apply_epi<T, EPI, VW>(v.elem(j), ep);
+        }
+    }
+}
+
+template <int T, int W, Epi EPI, int VW, int... Rs>
+__device__ __forceinline__ void process_rows(const Vec16<T>* p, int lane0,
+                                             typename EpiOut<T, EPI, VW>::type* __restrict__ out,
+                                             int64_t out_base, bool full, uint64_t len,
+                                             const EpiParams& ep, std::integer_sequence<int, Rs...>) {
+    (process_row<T, W, EPI, VW, Rs>(p, lane0, out, out_base, full, len, ep), ...);
+}
+
+// Decode one FastLanes block: this thread's 16-byte lane slice `t` of every word row.
+// out_base = output index of the block's packed position 0 (negative for the first block of
+// a slice with offset > 0); `full` = the whole block lands inside [0, len) with 16-B alignment.
+template <int T, int W, Epi EPI, int VW>
+__device__ __forceinline__ void unpack_block(const uint8_t* __restrict__ blk_packed, int t,
+                                             typename EpiOut<T, EPI, VW>::type* __restrict__ out,
+                                             int64_t out_base, bool full, uint64_t len,
+                                             const EpiParams& ep) {
+    using E = typename Fl<T>::E;
+    constexpr int EPV = 16 / int(sizeof(E));
+    constexpr int NW = W > 0 ? W : 1;
+    Vec16<T> p[NW];
+    if constexpr (W > 0) {
+#pragma unroll
+        for (int w = 0; w < W; w++) p[w] = load16<T>(blk_packed + 128 * w + 16 * t);
+    }
+    process_rows<T, W, EPI, VW>(p, t * EPV, out, out_base, full, len, ep,
+                                std::make_integer_sequence<int, T>{});
+}
+
+template <int T, int W, Epi EPI, int VW>
+__global__ __launch_bounds__(256) void fl_unpack_kernel(const uint8_t* __restrict__ packed,
+                                                        void* __restrict__ out_v, uint64_t n_blocks,
+                                                        uint32_t offset, uint64_t len,
+                                                        EpiParams ep) {
+    using O = typename EpiOut<T, EPI, VW>::type;
+    const uint64_t gid = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    const uint64_t blk = gid >> 3;
+    const int t = int(gid & 7);
+    if (blk >= n_blocks) return;
+    const int64_t out_base = int64_t(blk * 1024) - int64_t(offset);
+    const bool full = offset == 0 && (blk + 1) * 1024 <= len;
+    unpack_block<T, W, EPI, VW>(packed + blk * (128 * W), t, static_cast<O*>(out_v), out_base,
+                                full, len, ep);
+}
+
+// Many independent chunks (e.g. Chunked[Dict(BitPacked)]) in one launch; each workgroup of
+// 256 threads covers 32 blocks of exactly one chunk.
+template <int T, int W, Epi EPI, int VW>
+__global__ __launch_bounds__(256) void fl_unpack_chunks_kernel(const DictChunkDev* __restrict__ chunks,
+                                                               uint32_t n_chunks, EpiParams ep0) {
+    using O = typename EpiOut<T, EPI, VW>::type;
+    // binary search the chunk owning this workgroup
+    uint32_t lo = 0, hi = n_chunks;
+    const uint64_t g = blockIdx.x;
+    while (hi - lo > 1) {
+        uint32_t mid = (lo + hi) >> 1;
+        if (chunks[mid].first_group <= g) lo = mid; else hi = mid;
+    }
+    const DictChunkDev c = chunks[lo];
+    const uint64_t blk = (g - c.first_group) * 32 + (threadIdx.x >> 3);
+    const int t = int(threadIdx.x & 7);
+    if (blk >= c.n_blocks) return;
+    EpiParams ep = ep0;
+    ep.dict = c.dict;
+    ep.dict_len = c.dict_len;
+    const bool full = (blk + 1) * 1024 <= c.len;
+    unpack_block<T, W, EPI, VW>(c.packed + blk * (128 * W), t, static_cast<O*>(c.out),
+                                int64_t(blk * 1024), full, c.len, ep);
+}
+
+inline EpiParams to_epi(const UnpackArgs& a) {
+    EpiParams ep;
+    ep.reference = a.reference;
+    ep.shift = a.shift;
+    ep.alp_a = a.alp_a;
+    ep.alp_b = a.alp_b;
+    ep.dict = a.dict;
+    ep.dict_len = a.dict_len;
+    ep.err = a.err;
+    return ep;
+}
+
+template <int T, int W, Epi EPI, int VW>
+vxg_status launch_one(const UnpackArgs& a, hipStream_t s) {
+    if (a.n_blocks == 0) return VXG_OK;
+    const uint64_t threads = a.n_blocks * 8;
+    const uint64_t grid = (threads + 255) / 256;
+    hipLaunchKernelGGL((fl_unpack_kernel<T, W, EPI, VW>), dim3(unsigned(grid)), dim3(256), 0, s,
+                       a.packed, a.out, a.n_blocks, a.offset, a.len, to_epi(a));
+    return hip_check(hipGetLastError(), "fl_unpack_kernel launch");
+}
+
+template <int T, int W, Epi EPI, int VW>
+vxg_status launch_chunks_one(const DictChunkDev* d_chunks, uint32_t n_chunks, uint64_t total_groups,
+                             uint32_t* err, hipStream_t s) {
+    if (total_groups == 0) return VXG_OK;
+    EpiParams ep{};
+    ep.err = err;
+    hipLaunchKernelGGL((fl_unpack_chunks_kernel<T, W, EPI, VW>), dim3(unsigned(total_groups)),
+                       dim3(256), 0, s, d_chunks, n_chunks, ep);
+    return hip_check(hipGetLastError(), "fl_unpack_chunks_kernel launch");
+}
+
+// Function-pointer table over W = 0..WMAX.
+template <int T, Epi EPI, int VW, int... Ws>
+vxg_status dispatch_w_impl(int W, const UnpackArgs& a, hipStream_t s,
+                           std::integer_sequence<int, Ws...>) {
+    using Fn = vxg_status (*)(const UnpackArgs&, hipStream_t);
+    static constexpr Fn table[] = {&launch_one<T, Ws, EPI, VW>...};
+    if (W < 0 || W >= int(sizeof...(Ws))) return VXG_ERR_NOT_IMPLEMENTED;
+    return table[W](a, s);
+}
+
+template <int T, Epi EPI, int VW, int WMAX>
+vxg_status dispatch_w(int W, const UnpackArgs& a, hipStream_t s) {
+    return dispatch_w_impl<T, EPI, VW>(W, a, s, std::make_integer_sequence<int, WMAX + 1>{});
+}
+
+template <int T, Epi EPI, int VW, int... Ws>
+vxg_status dispatch_chunks_w_impl(int W, const DictChunkDev* d, uint32_t n, uint64_t g, uint32_t* err,
+                                  hipStream_t s, std::integer_sequence<int, Ws...>) {
+    using Fn = vxg_status (*)(const DictChunkDev*, uint32_t, uint64_t, uint32_t*, hipStream_t);
+    static constexpr Fn table[] = {&launch_chunks_one<T, Ws, EPI, VW>...};
+    if (W < 0 || W >= int(sizeof...(Ws))) return VXG_ERR_NOT_IMPLEMENTED;
+    return table[W](d, n, g, err, s);
+}
+
+}  // namespace vxg

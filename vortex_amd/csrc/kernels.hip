@@ -1,0 +1,605 @@
+// kernels.hip — the non-bitpacking decode kernels of the engine (gfx950).
+//
+//   K2 patch scatter     sparse/mod.rs:132-144 + primitive/mod.rs:168-185 (+ cascade epilogue)
+//   FoR / ZigZag / ALP   for/compress.rs:86-117, zigzag/compress.rs:35-57, alp/compress.rs:98-106
+//                        (standalone forms, used when the child is not BitPacked)
+//   K5 take              primitive/compute/take.rs:58-67, varbinview/compute.rs:68-76 (16-B views)
+//   K4 ALP-RD combine    alp_rd/mod.rs:260-301
+//   K3 Delta             delta/compress.rs:100-166 (undelta + untranspose fused, + slice :111)
+//   K8 RunEnd expand     runend/compress.rs:115-148
+//   K10 fill             array/constant/canonical.rs (broadcast)
+//   views                arrow-cast 53.2 Utf8->Utf8View (varbin/flatten.rs:10-17)
+// All of them are HBM-streaming kernels: 16-byte-per-lane accesses where the layout allows it,
+// grid-stride loops capped at 8 workgroups per CU, no LDS except where a re-layout needs it.
+#include "fl_unpack_impl.hpp"
+
+namespace vxg {
+
+namespace {
+
+constexpr int kBlock = 256;
+
+inline unsigned grid_for(uint64_t n_threads) {
+    uint64_t g = (n_threads + kBlock - 1) / kBlock;
+    const uint64_t cap = 256ull * 8 * 16;  // grid-stride beyond 32K workgroups
+    if (g > cap) g = cap;
+    if (g == 0) g = 1;
+    return unsigned(g);
+}
+
+__device__ __forceinline__ uint64_t load_uint(const void* p, int width, bool sgn, uint64_t i) {
+    switch (width) {
+    case 1: return sgn ? uint64_t(int64_t(static_cast<const int8_t*>(p)[i])) : static_cast<const uint8_t*>(p)[i];
+    case 2: return sgn ? uint64_t(int64_t(static_cast<const int16_t*>(p)[i])) : static_cast<const uint16_t*>(p)[i];
+    case 4: return sgn ? uint64_t(int64_t(static_cast<const int32_t*>(p)[i])) : static_cast<const uint32_t*>(p)[i];
+    default: return static_cast<const uint64_t*>(p)[i];
+    }
+}
+
+template <int W> struct UInt;
+template <> struct UInt<1> { using t = uint8_t; };
+template <> struct UInt<2> { using t = uint16_t; };
+template <> struct UInt<4> { using t = uint32_t; };
+template <> struct UInt<8> { using t = uint64_t; };
+template <> struct UInt<16> { using t = uint4; };
+
+}  // namespace
+
+// ------------------------------------------------------------------ K2 patch scatter
+template <int T, Epi EPI, int VW>
+__global__ __launch_bounds__(kBlock) void patch_kernel(typename EpiOut<T, EPI, VW>::type* __restrict__ out,
+                                                       uint64_t out_len, const void* __restrict__ idx,
+                                                       int idx_width, int idx_signed, uint64_t idx_off,
+                                                       const typename Fl<T>::E* __restrict__ vals,
+                                                       uint64_t n, EpiParams ep) {
+    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+         i += uint64_t(gridDim.x) * blockDim.x) {
+        const uint64_t p = load_uint(idx, idx_width, idx_signed != 0, i) - idx_off;
+        if (p >= out_len) {
+            __hip_atomic_fetch_or(ep.err, kErrPatchOOB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            continue;
+        }
+        out[p] = apply_epi<T, EPI, VW>(vals[i], ep);
+    }
+}
+
+template <int T, Epi EPI, int VW>
+static vxg_status patch_launch(void* out, uint64_t out_len, const void* idx, int iw, bool is,
+                               uint64_t ioff, const void* vals, uint64_t n, const UnpackArgs& a,
+                               hipStream_t s) {
+    using O = typename EpiOut<T, EPI, VW>::type;
+    hipLaunchKernelGGL((patch_kernel<T, EPI, VW>), dim3(grid_for(n)), dim3(kBlock), 0, s,
+                       static_cast<O*>(out), out_len, idx, iw, int(is), ioff,
+                       static_cast<const typename Fl<T>::E*>(vals), n, to_epi(a));
+    return hip_check(hipGetLastError(), "patch_kernel");
+}
+
+template <int T, Epi EPI>
+static vxg_status patch_vw(int vw, void* out, uint64_t out_len, const void* idx, int iw, bool is,
+                           uint64_t ioff, const void* vals, uint64_t n, const UnpackArgs& a,
+                           hipStream_t s) {
+    switch (vw) {
+    case 1: return patch_launch<T, EPI, 1>(out, out_len, idx, iw, is, ioff, vals, n, a, s);
+    case 2: return patch_launch<T, EPI, 2>(out, out_len, idx, iw, is, ioff, vals, n, a, s);
+    case 4: return patch_launch<T, EPI, 4>(out, out_len, idx, iw, is, ioff, vals, n, a, s);
+    case 8: return patch_launch<T, EPI, 8>(out, out_len, idx, iw, is, ioff, vals, n, a, s);
+    case 16: return patch_launch<T, EPI, 16>(out, out_len, idx, iw, is, ioff, vals, n, a, s);
+    default: return VXG_ERR_INVALID_ARGUMENT;
+    }
+}
+
+template <int T>
+static vxg_status patch_t(Epi epi, int vw, void* out, uint64_t out_len, const void* idx, int iw,
+                          bool is, uint64_t ioff, const void* vals, uint64_t n, const UnpackArgs& a,
+                          hipStream_t s) {
+    switch (epi) {
+    case Epi::Plain: return patch_launch<T, Epi::Plain, 0>(out, out_len, idx, iw, is, ioff, vals, n, a, s);
+    case Epi::For: return patch_launch<T, Epi::For, 0>(out, out_len, idx, iw, is, ioff, vals, n, a, s);
+    case Epi::ForZigZag: return patch_launch<T, Epi::ForZigZag, 0>(out, out_len, idx, iw, is, ioff, vals, n, a, s);
+    case Epi::AlpF32:
+        if constexpr (T == 32) return patch_launch<32, Epi::AlpF32, 0>(out, out_len, idx, iw, is, ioff, vals, n, a, s);
+        return VXG_ERR_INVALID_ARGUMENT;
+    case Epi::AlpF64:
+        if constexpr (T == 64) return patch_launch<64, Epi::AlpF64, 0>(out, out_len, idx, iw, is, ioff, vals, n, a, s);
+        return VXG_ERR_INVALID_ARGUMENT;
+    case Epi::Dict: return patch_vw<T, Epi::Dict>(vw, out, out_len, idx, iw, is, ioff, vals, n, a, s);
+    }
+    return VXG_ERR_INVALID_ARGUMENT;
+}
+
+vxg_status launch_patch(int val_width, int idx_width, bool idx_signed, Epi epi, int T, void* out,
+                        uint64_t out_len, const void* indices, uint64_t indices_offset,
+                        const void* values, uint64_t n, const UnpackArgs& ep, hipStream_t s) {
+    if (n == 0) return VXG_OK;
+    switch (T) {
+    case 8: return patch_t<8>(epi, val_width, out, out_len, indices, idx_width, idx_signed, indices_offset, values, n, ep, s);
+    case 16: return patch_t<16>(epi, val_width, out, out_len, indices, idx_width, idx_signed, indices_offset, values, n, ep, s);
+    case 32: return patch_t<32>(epi, val_width, out, out_len, indices, idx_width, idx_signed, indices_offset, values, n, ep, s);
+    case 64: return patch_t<64>(epi, val_width, out, out_len, indices, idx_width, idx_signed, indices_offset, values, n, ep, s);
+    default: return VXG_ERR_INVALID_ARGUMENT;
+    }
+}
+
+// ------------------------------------------------------------------ FoR / ZigZag (16 B / lane)
+template <typename E, bool ZZ>
+__global__ __launch_bounds__(kBlock) void for_kernel(const E* __restrict__ in, uint64_t n, E ref,
+                                                     unsigned shift, E* __restrict__ out) {
+    constexpr int V = 16 / sizeof(E);
+    const uint64_t nv = n / V;
+    const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < nv; i += stride) {
+        uint4 q = reinterpret_cast<const uint4*>(in)[i];
+        E e[V];
+        __builtin_memcpy(e, &q, 16);
+#pragma unroll
+        for (int j = 0; j < V; j++) {
+            E v = E(E(e[j] << shift) + ref);
+            if constexpr (ZZ) v = E((v >> 1) ^ E(E(0) - E(v & 1)));
+            e[j] = v;
+        }
+        __builtin_memcpy(&q, e, 16);
+        reinterpret_cast<uint4*>(out)[i] = q;
+    }
+    for (uint64_t i = nv * V + uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+        E v = E(E(in[i] << shift) + ref);
+        if constexpr (ZZ) v = E((v >> 1) ^ E(E(0) - E(v & 1)));
+        out[i] = v;
+    }
+}
+
+template <typename E>
+static vxg_status for_t(const void* in, uint64_t n, uint64_t ref, unsigned shift, bool zz, void* out,
+                        hipStream_t s) {
+    if ((reinterpret_cast<uintptr_t>(in) | reinterpret_cast<uintptr_t>(out)) & 15)
+        return set_error(VXG_ERR_INVALID_ARGUMENT, "FoR/ZigZag buffers must be 16-byte aligned");
+    const unsigned g = grid_for(n / (16 / sizeof(E)) + 1);
+    if (zz)
+        hipLaunchKernelGGL((for_kernel<E, true>), dim3(g), dim3(kBlock), 0, s,
+                           static_cast<const E*>(in), n, E(ref), shift, static_cast<E*>(out));
+    else
+        hipLaunchKernelGGL((for_kernel<E, false>), dim3(g), dim3(kBlock), 0, s,
+                           static_cast<const E*>(in), n, E(ref), shift, static_cast<E*>(out));
+    return hip_check(hipGetLastError(), "for_kernel");
+}
+
+vxg_status launch_for(int width, const void* in, uint64_t n, uint64_t ref, unsigned shift, bool zz,
+                      void* out, hipStream_t s) {
+    if (n == 0) return VXG_OK;
+    switch (width) {
+    case 1: return for_t<uint8_t>(in, n, ref, shift, zz, out, s);
+    case 2: return for_t<uint16_t>(in, n, ref, shift, zz, out, s);
+    case 4: return for_t<uint32_t>(in, n, ref, shift, zz, out, s);
+    case 8: return for_t<uint64_t>(in, n, ref, shift, zz, out, s);
+    default: return VXG_ERR_INVALID_ARGUMENT;
+    }
+}
+
+vxg_status launch_zigzag(int width, const void* in, uint64_t n, void* out, hipStream_t s) {
+    return launch_for(width, in, n, 0, 0, true, out, s);
+}
+
+// ------------------------------------------------------------------ ALP (standalone)
+template <typename I, typename F>
+__global__ __launch_bounds__(kBlock) void alp_kernel(const I* __restrict__ in, uint64_t n, F a, F b,
+                                                     F* __restrict__ out) {
+    constexpr int V = 16 / sizeof(I);
+    const uint64_t nv = n / V;
+    const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < nv; i += stride) {
+        uint4 q = reinterpret_cast<const uint4*>(in)[i];
+        I e[V];
+        F o[V];
+        __builtin_memcpy(e, &q, 16);
+#pragma unroll
+        for (int j = 0; j < V; j++) {
+            if constexpr (sizeof(F) == 4) o[j] = __fmul_rn(__fmul_rn(F(e[j]), a), b);
+            else o[j] = __dmul_rn(__dmul_rn(F(e[j]), a), b);
+        }
+        __builtin_memcpy(&q, o, 16);
+        reinterpret_cast<uint4*>(out)[i] = q;
+    }
+    for (uint64_t i = nv * V + uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+        if constexpr (sizeof(F) == 4) out[i] = __fmul_rn(__fmul_rn(F(in[i]), a), b);
+        else out[i] = __dmul_rn(__dmul_rn(F(in[i]), a), b);
+    }
+}
+
+vxg_status launch_alp(int float_ptype, const void* enc, uint64_t n, double a, double b, void* out,
+                      hipStream_t s) {
+    if (n == 0) return VXG_OK;
+    if ((reinterpret_cast<uintptr_t>(enc) | reinterpret_cast<uintptr_t>(out)) & 15)
+        return set_error(VXG_ERR_INVALID_ARGUMENT, "ALP buffers must be 16-byte aligned");
+    if (float_ptype == VXG_F32) {
+        hipLaunchKernelGGL((alp_kernel<int32_t, float>), dim3(grid_for(n / 4 + 1)), dim3(kBlock), 0, s,
+                           static_cast<const int32_t*>(enc), n, float(a), float(b), static_cast<float*>(out));
+    } else if (float_ptype == VXG_F64) {
+        hipLaunchKernelGGL((alp_kernel<int64_t, double>), dim3(grid_for(n / 2 + 1)), dim3(kBlock), 0, s,
+                           static_cast<const int64_t*>(enc), n, a, b, static_cast<double*>(out));
+    } else {
+        return set_error(VXG_ERR_MISMATCHED_TYPES, "ALP decodes to f32 or f64 only");
+    }
+    return hip_check(hipGetLastError(), "alp_kernel");
+}
+
+// ------------------------------------------------------------------ K5 take (gather)
+template <typename C, typename V>
+__global__ __launch_bounds__(kBlock) void take_kernel(const V* __restrict__ values, uint64_t n_values,
+                                                      const C* __restrict__ codes, uint64_t n,
+                                                      V* __restrict__ out, uint32_t* err) {
+    const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+        uint64_t c = uint64_t(codes[i]);
+        if (c >= n_values) {
+            __hip_atomic_fetch_or(err, kErrTakeOOB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            c = 0;
+        }
+        out[i] = values[c];
+    }
+}
+
+template <typename C>
+static vxg_status take_c(int vw, const void* values, uint64_t nv, const void* codes, uint64_t n,
+                         void* out, uint32_t* err, hipStream_t s) {
+    const unsigned g = grid_for(n);
+    switch (vw) {
+#define TAKE_CASE(W)                                                                                \
+    case W:                                                                                         \
+        hipLaunchKernelGGL((take_kernel<C, typename UInt<W>::t>), dim3(g), dim3(kBlock), 0, s,      \
+                           static_cast<const typename UInt<W>::t*>(values), nv,                     \
+                           static_cast<const C*>(codes), n, static_cast<typename UInt<W>::t*>(out), \
+                           err);                                                                    \
+        break;
+        TAKE_CASE(1) TAKE_CASE(2) TAKE_CASE(4) TAKE_CASE(8) TAKE_CASE(16)
+#undef TAKE_CASE
+    default: return VXG_ERR_INVALID_ARGUMENT;
+    }
+    return hip_check(hipGetLastError(), "take_kernel");
+}
+
+vxg_status launch_take(int value_width, const void* values, uint64_t n_values, int code_width,
+                       const void* codes, uint64_t n, void* out, uint32_t* err, hipStream_t s) {
+    if (n == 0) return VXG_OK;
+    switch (code_width) {
+    case 1: return take_c<uint8_t>(value_width, values, n_values, codes, n, out, err, s);
+    case 2: return take_c<uint16_t>(value_width, values, n_values, codes, n, out, err, s);
+    case 4: return take_c<uint32_t>(value_width, values, n_values, codes, n, out, err, s);
+    case 8: return take_c<uint64_t>(value_width, values, n_values, codes, n, out, err, s);
+    default: return VXG_ERR_INVALID_ARGUMENT;
+    }
+}
+
+// ------------------------------------------------------------------ K4 ALP-RD
+struct RdDict { uint16_t d[8]; };
+
+template <typename UT>
+__global__ __launch_bounds__(kBlock) void alprd_kernel(const uint16_t* __restrict__ left, RdDict dict,
+                                                       unsigned dict_len, unsigned rbw,
+                                                       const UT* __restrict__ right, uint64_t n,
+                                                       UT* __restrict__ out) {
+    const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+        unsigned c = left[i];
+        const UT l = UT(c < dict_len ? dict.d[c] : 0);
+        out[i] = UT((l << rbw) | right[i]);
+    }
+}
+
+template <typename UT>
+__global__ __launch_bounds__(kBlock) void alprd_exc_kernel(const void* __restrict__ pos, int pos_width,
+                                                           int pos_signed, uint64_t pos_off,
+                                                           const uint16_t* __restrict__ exc, uint64_t n_exc,
+                                                           unsigned rbw, const UT* __restrict__ right,
+                                                           uint64_t n, UT* __restrict__ out, uint32_t* err) {
+    const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n_exc; i += stride) {
+        const uint64_t p = load_uint(pos, pos_width, pos_signed != 0, i) - pos_off;
+        if (p < n) out[p] = UT((UT(exc[i]) << rbw) | right[p]);
+        else __hip_atomic_fetch_or(err, kErrPatchOOB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+vxg_status launch_alprd(int float_ptype, const uint16_t* left, const uint16_t* dict, unsigned dict_len,
+                        unsigned rbw, const void* right, uint64_t n, const void* exc_pos, int pos_width,
+                        bool pos_signed, uint64_t pos_off, const uint16_t* exc, uint64_t n_exc, void* out,
+                        uint32_t* err, hipStream_t s) {
+    RdDict d{};
+    for (unsigned i = 0; i < dict_len && i < 8; i++) d.d[i] = dict[i];
+    if (float_ptype == VXG_F32) {
+        if (n) hipLaunchKernelGGL((alprd_kernel<uint32_t>), dim3(grid_for(n)), dim3(kBlock), 0, s, left, d,
+                                  dict_len, rbw, static_cast<const uint32_t*>(right), n, static_cast<uint32_t*>(out));
+        if (n_exc) hipLaunchKernelGGL((alprd_exc_kernel<uint32_t>), dim3(grid_for(n_exc)), dim3(kBlock), 0, s,
+                                      exc_pos, pos_width, int(pos_signed), pos_off, exc, n_exc, rbw,
+                                      static_cast<const uint32_t*>(right), n, static_cast<uint32_t*>(out), err);
+    } else if (float_ptype == VXG_F64) {
+        if (n) hipLaunchKernelGGL((alprd_kernel<uint64_t>), dim3(grid_for(n)), dim3(kBlock), 0, s, left, d,
+                                  dict_len, rbw, static_cast<const uint64_t*>(right), n, static_cast<uint64_t*>(out));
+        if (n_exc) hipLaunchKernelGGL((alprd_exc_kernel<uint64_t>), dim3(grid_for(n_exc)), dim3(kBlock), 0, s,
+                                      exc_pos, pos_width, int(pos_signed), pos_off, exc, n_exc, rbw,
+                                      static_cast<const uint64_t*>(right), n, static_cast<uint64_t*>(out), err);
+    } else {
+        return set_error(VXG_ERR_MISMATCHED_TYPES, "ALP-RD decodes to f32 or f64 only");
+    }
+    return hip_check(hipGetLastError(), "alprd_kernel");
+}
+
+// ------------------------------------------------------------------ validity bit copy
+// dst (pre-zeroed) bits [dst_off, dst_off+n) |= src bits [src_off, src_off+n); LSB order.
+__global__ __launch_bounds__(kBlock) void copy_bits_kernel(uint32_t* __restrict__ dst, uint64_t dst_off,
+                                                           const uint8_t* __restrict__ src, uint64_t src_off,
+                                                           uint64_t n, int set_all) {
+    const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+    for (uint64_t w = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; w * 32 < n; w += stride) {
+        uint32_t bits = 0;
+        for (int k = 0; k < 32; k++) {
+            const uint64_t i = w * 32 + k;
+            if (i >= n) break;
+            const uint64_t si = src_off + i;
+            const uint32_t b = set_all ? 1u : uint32_t((src[si >> 3] >> (si & 7)) & 1);
+            bits |= b << k;
+        }
+        const uint64_t d = dst_off + w * 32;
+        const uint64_t word = d >> 5;
+        const int sh = int(d & 31);
+        if (bits) {
+            atomicOr(dst + word, bits << sh);
+            if (sh) atomicOr(dst + word + 1, bits >> (32 - sh));
+        }
+    }
+}
+
+vxg_status launch_copy_bits(void* dst, uint64_t dst_off, const uint8_t* src, uint64_t src_off, uint64_t n,
+                            bool set_all, hipStream_t s) {
+    if (n == 0) return VXG_OK;
+    hipLaunchKernelGGL(copy_bits_kernel, dim3(grid_for((n + 31) / 32)), dim3(kBlock), 0, s,
+                       static_cast<uint32_t*>(dst), dst_off, src, src_off, n, int(set_all));
+    return hip_check(hipGetLastError(), "copy_bits_kernel");
+}
+
+// Sparse validity: set bit (idx - off) for every index.
+__global__ __launch_bounds__(kBlock) void set_bits_at_kernel(uint32_t* __restrict__ dst, const void* idx,
+                                                             int iw, int isg, uint64_t off, uint64_t n,
+                                                             uint64_t len) {
+    const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t p = load_uint(idx, iw, isg != 0, i) - off;
+        if (p < len) atomicOr(dst + (p >> 5), 1u << (p & 31));
+    }
+}
+
+vxg_status launch_set_bits_at(void* dst, const void* idx, int iw, bool isg, uint64_t off, uint64_t n,
+                              uint64_t len, hipStream_t s) {
+    if (n == 0) return VXG_OK;
+    hipLaunchKernelGGL(set_bits_at_kernel, dim3(grid_for(n)), dim3(kBlock), 0, s,
+                       static_cast<uint32_t*>(dst), idx, iw, int(isg), off, n, len);
+    return hip_check(hipGetLastError(), "set_bits_at_kernel");
+}
+
+// Sum of an integer column (FSST heap size), int64 result.
+__global__ __launch_bounds__(kBlock) void sum_kernel(const void* p, int w, int sg, uint64_t n,
+                                                     unsigned long long* out) {
+    unsigned long long acc = 0;
+    const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride)
+        acc += (unsigned long long)load_uint(p, w, sg != 0, i);
+    for (int d = 32; d > 0; d >>= 1) acc += __shfl_down(acc, d, 64);
+    if ((threadIdx.x & 63) == 0 && acc) atomicAdd(out, acc);
+}
+
+vxg_status launch_sum(const void* p, int w, bool sg, uint64_t n, void* out_u64, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(out_u64, 0, 8, s);
+    if (e != hipSuccess) return hip_check(e, "memset");
+    if (n == 0) return VXG_OK;
+    hipLaunchKernelGGL(sum_kernel, dim3(grid_for(n) > 1024 ? 1024 : grid_for(n)), dim3(kBlock), 0, s, p, w,
+                       int(sg), n, static_cast<unsigned long long*>(out_u64));
+    return hip_check(hipGetLastError(), "sum_kernel");
+}
+
+// ------------------------------------------------------------------ K3 Delta
+// For lane l of a full block, the untransposed output positions of rows 0..T-1 form the
+// contiguous run out[base_l .. base_l+T) with base_l = transpose(index(0, l)) (SURVEY App. A,
+// invariant 3), so undelta + untranspose is one serial wrapping prefix per lane whose result
+// is written as a contiguous T-element run: thread per (block, lane).
+template <typename E>
+__global__ __launch_bounds__(kBlock) void delta_kernel(const E* __restrict__ bases,
+                                                       const E* __restrict__ deltas, uint64_t n_full_blocks,
+                                                       uint64_t offset, uint64_t len, E* __restrict__ out) {
+    constexpr int T = 8 * sizeof(E), LANES = 1024 / T;
+    const uint64_t gid = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    const uint64_t blk = gid / LANES;
+    const int l = int(gid % LANES);
+    if (blk >= n_full_blocks) return;
+    const E* d = deltas + blk * 1024;
+    // transpose(i) = (i%16)*64 + FL_ORDER[(i/16)%8]*8 + i/128 at i = index(0, l) = l
+    const int base_l = (l % 16) * 64 + fl_order((l / 16) % 8) * 8;
+    E prev = bases[blk * LANES + l];
+    E run[T];
+#pragma unroll
+    for (int r = 0; r < T; r++) {
+        prev = E(d[fl_index(r, l)] + prev);
+        run[r] = prev;
+    }
+    const int64_t o0 = int64_t(blk * 1024 + base_l) - int64_t(offset);
+    if (o0 >= 0 && uint64_t(o0) + T <= len && ((reinterpret_cast<uintptr_t>(out + o0) & 15) == 0)) {
+#pragma unroll
+        for (int k = 0; k < T * int(sizeof(E)) / 16; k++) {
+            uint4 q;
+            __builtin_memcpy(&q, reinterpret_cast<const uint8_t*>(run) + 16 * k, 16);
+            reinterpret_cast<uint4*>(out + o0)[k] = q;
+        }
+    } else {
+#pragma unroll
+        for (int r = 0; r < T; r++) {
+            const int64_t o = o0 + r;
+            if (o >= 0 && uint64_t(o) < len) out[o] = run[r];
+        }
+    }
+}
+
+template <typename E>
+__global__ void delta_tail_kernel(const E* __restrict__ bases, const E* __restrict__ deltas,
+                                  uint64_t n_full_blocks, uint64_t n_deltas, uint64_t offset,
+                                  uint64_t len, E* __restrict__ out) {
+    // remainder block: scalar running sum from bases[last] (delta/compress.rs:153-163)
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    constexpr int LANES = 1024 / (8 * sizeof(E));
+    E base = bases[n_full_blocks * LANES];
+    for (uint64_t i = n_full_blocks * 1024; i < n_deltas; i++) {
+        base = E(deltas[i] + base);
+        if (i >= offset && i - offset < len) out[i - offset] = base;
+    }
+}
+
+template <typename E>
+static vxg_status delta_t(const void* bases, const void* deltas, uint64_t n_deltas, uint64_t offset,
+                          uint64_t len, void* out, hipStream_t s) {
+    constexpr int LANES = 1024 / (8 * sizeof(E));
+    const uint64_t full = n_deltas / 1024;
+    if (full) {
+        const uint64_t threads = full * LANES;
+        hipLaunchKernelGGL((delta_kernel<E>), dim3(unsigned((threads + kBlock - 1) / kBlock)), dim3(kBlock),
+                           0, s, static_cast<const E*>(bases), static_cast<const E*>(deltas), full, offset,
+                           len, static_cast<E*>(out));
+    }
+    if (n_deltas % 1024)
+        hipLaunchKernelGGL((delta_tail_kernel<E>), dim3(1), dim3(64), 0, s, static_cast<const E*>(bases),
+                           static_cast<const E*>(deltas), full, n_deltas, offset, len, static_cast<E*>(out));
+    return hip_check(hipGetLastError(), "delta_kernel");
+}
+
+vxg_status launch_delta(int width, const void* bases, const void* deltas, uint64_t n_deltas,
+                        uint64_t offset, uint64_t len, void* out, hipStream_t s) {
+    switch (width) {
+    case 1: return delta_t<uint8_t>(bases, deltas, n_deltas, offset, len, out, s);
+    case 2: return delta_t<uint16_t>(bases, deltas, n_deltas, offset, len, out, s);
+    case 4: return delta_t<uint32_t>(bases, deltas, n_deltas, offset, len, out, s);
+    case 8: return delta_t<uint64_t>(bases, deltas, n_deltas, offset, len, out, s);
+    default: return VXG_ERR_INVALID_ARGUMENT;
+    }
+}
+
+// ------------------------------------------------------------------ K8 RunEnd expand
+// Thread per 8 consecutive outputs: upper_bound on ends for the first output, then walk.
+template <typename V>
+__global__ __launch_bounds__(kBlock) void runend_kernel(const V* __restrict__ values, const void* __restrict__ ends,
+                                                        int ends_width, uint64_t n_runs, uint64_t offset,
+                                                        uint64_t len, V* __restrict__ out, uint32_t* err) {
+    constexpr int ITEMS = 8;
+    const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+    for (uint64_t t = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; t * ITEMS < len; t += stride) {
+        const uint64_t j0 = t * ITEMS;
+        // first run r with (ends[r] - offset) > j0
+        uint64_t lo = 0, hi = n_runs;
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (load_uint(ends, ends_width, false, mid) - offset > j0) hi = mid; else lo = mid + 1;
+        }
+        uint64_t r = lo;
+        if (r >= n_runs) {
+            __hip_atomic_fetch_or(err, kErrRunEnd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            continue;
+        }
+        uint64_t end = load_uint(ends, ends_width, false, r) - offset;
+#pragma unroll
+        for (int k = 0; k < ITEMS; k++) {
+            const uint64_t j = j0 + k;
+            if (j >= len) break;
+            while (end <= j && r + 1 < n_runs) {
+                r++;
+                end = load_uint(ends, ends_width, false, r) - offset;
+            }
+            out[j] = values[r];
+        }
+    }
+}
+
+vxg_status launch_runend(int value_width, const void* values, int ends_width, const void* ends,
+                         uint64_t n_runs, uint64_t offset, uint64_t len, void* out, uint32_t* err,
+                         hipStream_t s) {
+    if (len == 0) return VXG_OK;
+    if (n_runs == 0) return set_error(VXG_ERR_INVALID_ARGUMENT, "RunEnd with len > 0 has no runs");
+    const unsigned g = grid_for((len + 7) / 8);
+    switch (value_width) {
+#define RE_CASE(W)                                                                                  \
+    case W:                                                                                         \
+        hipLaunchKernelGGL((runend_kernel<typename UInt<W>::t>), dim3(g), dim3(kBlock), 0, s,       \
+                           static_cast<const typename UInt<W>::t*>(values), ends, ends_width,       \
+                           n_runs, offset, len, static_cast<typename UInt<W>::t*>(out), err);       \
+        break;
+        RE_CASE(1) RE_CASE(2) RE_CASE(4) RE_CASE(8) RE_CASE(16)
+#undef RE_CASE
+    default: return VXG_ERR_INVALID_ARGUMENT;
+    }
+    return hip_check(hipGetLastError(), "runend_kernel");
+}
+
+// ------------------------------------------------------------------ K10 fill
+template <typename V>
+__global__ __launch_bounds__(kBlock) void fill_kernel(V v, uint64_t n, V* __restrict__ out) {
+    const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) out[i] = v;
+}
+
+vxg_status launch_fill(int value_width, const uint8_t* scalar16, uint64_t n, void* out, hipStream_t s) {
+    if (n == 0) return VXG_OK;
+    const unsigned g = grid_for(n);
+    switch (value_width) {
+#define FILL_CASE(W)                                                                                \
+    case W: {                                                                                       \
+        typename UInt<W>::t v;                                                                      \
+        __builtin_memcpy(&v, scalar16, W);                                                          \
+        hipLaunchKernelGGL((fill_kernel<typename UInt<W>::t>), dim3(g), dim3(kBlock), 0, s, v, n,   \
+                           static_cast<typename UInt<W>::t*>(out));                                 \
+    } break;
+        FILL_CASE(1) FILL_CASE(2) FILL_CASE(4) FILL_CASE(8) FILL_CASE(16)
+#undef FILL_CASE
+    default: return VXG_ERR_INVALID_ARGUMENT;
+    }
+    return hip_check(hipGetLastError(), "fill_kernel");
+}
+
+// ------------------------------------------------------------------ VarBin -> views
+// arrow-array 53.2 make_view: len<=12 inline (zero padded), else {len, prefix, 0, offset};
+// null rows -> all-zero view (GenericByteViewBuilder::append_null).
+__device__ __forceinline__ uint4 make_view(const uint8_t* __restrict__ heap, uint64_t start, uint32_t len) {
+    uint8_t b[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) b[k] = 0;
+    __builtin_memcpy(b, &len, 4);
+    if (len <= 12) {
+        for (uint32_t k = 0; k < len; k++) b[4 + k] = heap[start + k];
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; k++) b[4 + k] = heap[start + k];
+        const uint32_t off = uint32_t(start);
+        __builtin_memcpy(b + 12, &off, 4);
+    }
+    uint4 q;
+    __builtin_memcpy(&q, b, 16);
+    return q;
+}
+
+__global__ __launch_bounds__(kBlock) void varbin_views_kernel(const uint8_t* __restrict__ heap, const void* offs,
+                                                              int offs_width, uint64_t n,
+                                                              const uint8_t* __restrict__ validity,
+                                                              uint4* __restrict__ views) {
+    const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+        if (validity && !((validity[i >> 3] >> (i & 7)) & 1)) {
+            views[i] = make_uint4(0, 0, 0, 0);
+            continue;
+        }
+        const uint64_t a = load_uint(offs, offs_width, offs_width < 8, i);
+        const uint64_t b = load_uint(offs, offs_width, offs_width < 8, i + 1);
+        views[i] = make_view(heap, a, uint32_t(b - a));
+    }
+}
+
+vxg_status launch_varbin_views(const uint8_t* heap, int offs_width, const void* offsets, uint64_t n,
+                               const uint8_t* validity, uint8_t* views, hipStream_t s) {
+    if (n == 0) return VXG_OK;
+    hipLaunchKernelGGL(varbin_views_kernel, dim3(grid_for(n)), dim3(kBlock), 0, s, heap, offsets,
+                       offs_width, n, validity, reinterpret_cast<uint4*>(views));
+    return hip_check(hipGetLastError(), "varbin_views_kernel");
+}
+
+}  // namespace vxg

@@ -1,0 +1,142 @@
+// vxg_internal.hpp — shared internals of the MI355X decode engine (not part of the C ABI).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+#include "../../include/vortex_gpu.h"
+
+namespace vxg {
+
+// FastLanes FL_ORDER (fastlanes 0.1.8).
+__host__ __device__ constexpr int fl_order(int i) {
+    constexpr int o[8] = {0, 4, 2, 6, 1, 5, 3, 7};
+    return o[i];
+}
+// index(row, lane) = FL_ORDER[row/8]*16 + (row%8)*128 + lane
+__host__ __device__ constexpr int fl_index(int row, int lane) {
+    return fl_order(row / 8) * 16 + (row % 8) * 128 + lane;
+}
+
+inline int ptype_width(int p) {
+    switch (p) {
+    case VXG_U8: case VXG_I8: return 1;
+    case VXG_U16: case VXG_I16: case VXG_F16: return 2;
+    case VXG_U32: case VXG_I32: case VXG_F32: return 4;
+    case VXG_U64: case VXG_I64: case VXG_F64: return 8;
+    default: return 0;
+    }
+}
+inline bool ptype_is_int(int p) { return p >= VXG_U8 && p <= VXG_I64; }
+inline bool ptype_is_signed(int p) { return p >= VXG_I8 && p <= VXG_I64; }
+inline bool ptype_is_unsigned(int p) { return p >= VXG_U8 && p <= VXG_U64; }
+
+// ALP exponent tables: encodings/alp/src/alp/mod.rs:255-351 (same literals => same bits).
+extern const float kF10f[11];
+extern const float kIF10f[11];
+extern const double kF10d[24];
+extern const double kIF10d[24];
+
+// Device error word bits (set by kernels, read by vxg_check via vxg_stream_sync).
+enum : uint32_t { kErrTakeOOB = 1u, kErrPatchOOB = 2u, kErrRunEnd = 4u };
+
+struct Ctx {
+    int device = 0;
+    uint32_t* err_word = nullptr;  // device
+};
+
+vxg_status set_error(vxg_status s, const std::string& msg);
+vxg_status hip_check(hipError_t e, const char* what);
+
+// ---- launchers implemented in the .hip translation units -----------------------------
+// Epilogue kinds of the fused FastLanes unpack.
+enum class Epi : int { Plain = 0, For = 1, ForZigZag = 2, AlpF32 = 3, AlpF64 = 4, Dict = 5 };
+
+struct UnpackArgs {
+    const uint8_t* packed;
+    void* out;
+    uint64_t n_blocks;   // FastLanes blocks covered by the launch
+    uint32_t offset;     // values to skip in block 0 (<1024)
+    uint64_t len;        // values to write
+    uint64_t reference;  // FoR reference bits
+    uint32_t shift;      // FoR shift
+    double alp_a, alp_b; // F10[f], IF10[e] (f32 tables are converted exactly)
+    const void* dict;    // Dict values
+    uint64_t dict_len;
+    uint32_t* err;
+};
+
+// T in {8,16,32,64} bits; value_width only used for Epi::Dict.
+vxg_status launch_fl_unpack(int T, int W, Epi epi, int value_width, const UnpackArgs& a,
+                            hipStream_t s);
+
+struct DictChunkDev {
+    const uint8_t* packed;
+    const void* dict;
+    void* out;
+    uint64_t n_blocks;
+    uint64_t len;
+    uint64_t dict_len;
+    uint64_t first_group;  // first 32-block workgroup index of this chunk
+};
+vxg_status launch_fl_unpack_dict_chunks(int T, int W, int value_width, const DictChunkDev* d_chunks,
+                                        uint32_t n_chunks, uint64_t total_groups, uint32_t* err,
+                                        hipStream_t s);
+
+// Patch scatter with the same epilogue applied to the patch value.
+vxg_status launch_patch(int val_width, int idx_width, bool idx_signed, Epi epi, int T,
+                        void* out, uint64_t out_len, const void* indices, uint64_t indices_offset,
+                        const void* values, uint64_t n, const UnpackArgs& ep, hipStream_t s);
+
+vxg_status launch_for(int width, const void* in, uint64_t n, uint64_t ref, unsigned shift,
+                      bool zigzag, void* out, hipStream_t s);
+vxg_status launch_zigzag(int width, const void* in, uint64_t n, void* out, hipStream_t s);
+vxg_status launch_alp(int float_ptype, const void* enc, uint64_t n, double a, double b, void* out,
+                      hipStream_t s);
+vxg_status launch_take(int value_width, const void* values, uint64_t n_values, int code_width,
+                       const void* codes, uint64_t n, void* out, uint32_t* err, hipStream_t s);
+vxg_status launch_alprd(int float_ptype, const uint16_t* left, const uint16_t* dict, unsigned dict_len,
+                        unsigned right_bw, const void* right, uint64_t n, const void* exc_pos,
+                        int pos_width, bool pos_signed, uint64_t pos_off, const uint16_t* exc,
+                        uint64_t n_exc, void* out, uint32_t* err, hipStream_t s);
+vxg_status launch_copy_bits(void* dst, uint64_t dst_off, const uint8_t* src, uint64_t src_off, uint64_t n,
+                            bool set_all, hipStream_t s);
+vxg_status launch_set_bits_at(void* dst, const void* idx, int iw, bool isg, uint64_t off, uint64_t n,
+                              uint64_t len, hipStream_t s);
+vxg_status launch_sum(const void* p, int w, bool sg, uint64_t n, void* out_u64, hipStream_t s);
+// K1 instantiation units (fl_inst.hip)
+vxg_status fl_plain_8(int W, Epi epi, const UnpackArgs& a, hipStream_t s);
+vxg_status fl_plain_16(int W, Epi epi, const UnpackArgs& a, hipStream_t s);
+vxg_status fl_plain_32(int W, Epi epi, const UnpackArgs& a, hipStream_t s);
+vxg_status fl_plain_64(int W, Epi epi, const UnpackArgs& a, hipStream_t s);
+vxg_status fl_alp(int T, int W, Epi epi, const UnpackArgs& a, hipStream_t s);
+#define VXG_DECL_DICT(VW)                                                                          \
+    vxg_status fl_dict_##VW(int T, int W, const UnpackArgs& a, hipStream_t s);                     \
+    vxg_status fl_dict_chunks_##VW(int T, int W, const DictChunkDev* d, uint32_t n, uint64_t g,    \
+                                   uint32_t* err, hipStream_t s);
+VXG_DECL_DICT(1)
+VXG_DECL_DICT(2)
+VXG_DECL_DICT(4)
+VXG_DECL_DICT(8)
+VXG_DECL_DICT(16)
+#undef VXG_DECL_DICT
+constexpr int kDictFusedMaxW = 16;
+vxg_status launch_delta(int width, const void* bases, const void* deltas, uint64_t n_deltas,
+                        uint64_t offset, uint64_t len, void* out, hipStream_t s);
+vxg_status launch_runend(int value_width, const void* values, int ends_width, const void* ends,
+                         uint64_t n_runs, uint64_t offset, uint64_t len, void* out, uint32_t* err,
+                         hipStream_t s);
+vxg_status launch_fill(int value_width, const uint8_t* scalar16, uint64_t n, void* out,
+                       hipStream_t s);
+uint64_t fsst_scratch_bytes(uint64_t n);
+vxg_status launch_fsst(const uint64_t* symbols, const uint8_t* sym_lens, unsigned n_symbols,
+                       const uint8_t* code_bytes, int offs_width, const void* code_offsets,
+                       int lens_width, bool lens_signed, const void* lens, uint64_t n,
+                       const uint8_t* validity, void* scratch, uint8_t* heap, uint8_t* views,
+                       hipStream_t s);
+vxg_status launch_varbin_views(const uint8_t* heap, int offs_width, const void* offsets, uint64_t n,
+                               const uint8_t* validity, uint8_t* views, hipStream_t s);
+
+}  // namespace vxg
