@@ -53,12 +53,13 @@ def make_c1(rng):
 
 
 def make_c2(rng):
-    """C2: 64 Mi f64 2-decimal prices + 0.1% random exceptions -> ALP->FoR->BitPacked(u64)."""
+    """C2: 64 Mi f64 2-decimal prices + 0.1% random full-precision exceptions in the same
+    range (never 2-decimal, so always ALP patches) -> ALP->FoR->BitPacked(u64, W=24)."""
     import vortex_amd.encode as E
     n = 64 << 20
     vals = np.round(rng.uniform(1, 100000, n) * 100) / 100
     k = n // 1000
-    vals[rng.choice(n, k, replace=False)] = rng.standard_normal(k) * 1e9
+    vals[rng.choice(n, k, replace=False)] = rng.uniform(1, 100000, k) + 1e-7
     arr = E.encode_alp(vals)
     return arr, dict(name="C2", encoding="vortex.alp(fastlanes.for(fastlanes.bitpacked u64)) f64",
                      values=n, read_bytes=arr.nbytes(), write_bytes=vals.nbytes, dtype="f64")
@@ -136,6 +137,7 @@ class Workload:
             self.views = torch.empty(vb.value, dtype=torch.uint8, device=dev)
             self.data = torch.empty(db.value + 16, dtype=torch.uint8, device=dev)
             self.out.views, self.out.data = self.views.data_ptr(), self.data.data_ptr()
+            self.out.data_bytes = db.value
         self.i = 0
 
     def step(self):

@@ -119,8 +119,8 @@ def test_signed_bitpacked_reinterpret(ctx):
 def test_for_bitpacked_fused(ctx, dt):
     rng = np.random.default_rng(5)
     info = np.iinfo(dt)
-    base = int(info.min) // 2 + 7 if info.min < 0 else 1000
-    vals = (base + 4 * rng.integers(0, 50, 9000)).astype(dt)
+    base = int(info.min) // 2 + 8 if info.min < 0 else 1000
+    vals = (base + 4 * rng.integers(0, 25, 9000)).astype(dt)
     arr = E.encode_for_bitpacked(vals)
     assert arr.encoding == A.ENC["FL_FOR"] and arr.meta["shift"] == 2
     assert_primitive_parity(arr, ctx, vals)

@@ -449,6 +449,7 @@ def canonicalize(a: Array, ctx: Context, out_values=None, sync: bool = True) -> 
         views = torch.empty(max(vb.value, 16), dtype=torch.uint8, device=dev)
         data = torch.empty(db.value + 16, dtype=torch.uint8, device=dev)
         out.views, out.data = views.data_ptr(), data.data_ptr()
+        out.data_bytes = db.value
         res.views, res.data = views[: vb.value], data[: db.value]
     if valid_t is not None:
         out.validity = valid_t.data_ptr()

@@ -604,11 +604,16 @@ vxg_status Planner::string_canonical(const vxg_array& a, vxg_canonical& out) {
     out.kind = VXG_ENC_VARBINVIEW;
     out.len = a.len;
     out.dtype = a.dtype;
-    uint64_t vb, db;
-    VXG_TRY(canonical_size(a, vb, db));
-    if (!out.views) VXG_TRY(hip_check(hipMalloc(&out.views, vb ? vb : 16), "views alloc"));
-    if (!out.data) VXG_TRY(hip_check(hipMalloc(&out.data, db + 16), "data alloc"));
-    out.data_bytes = db;
+    // Sizes are only needed to allocate; a caller that passes both buffers (sized with
+    // vxg_canonical_size) pays no device sum + sync on the decode path.
+    if (!out.views || !out.data) {
+        uint64_t vb, db;
+        VXG_TRY(canonical_size(a, vb, db));
+        if (!out.views) VXG_TRY(hip_check(hipMalloc(&out.views, vb ? vb : 16), "views alloc"));
+        if (!out.data) VXG_TRY(hip_check(hipMalloc(&out.data, db + 16), "data alloc"));
+        out.data_bytes = db;
+    }
+    const uint64_t db = out.data_bytes;
     VXG_TRY(validity_into(a, &out.validity));
     if (a.encoding == VXG_ENC_VARBIN) {
         // varbin/flatten.rs:10-17: views over the whole bytes buffer (block 0)

@@ -154,7 +154,7 @@ __global__ __launch_bounds__(kTile) void fsst_decode(const uint64_t* __restrict_
             for (int q = 0; q < 4; q++)
                 w[q] = uint32_t(src[4 * q]) | (uint32_t(src[4 * q + 1]) << 8) |
                        (uint32_t(src[4 * q + 2]) << 16) | (uint32_t(src[4 * q + 3]) << 24);
-            reinterpret_cast<uint4*>(dst + h)[k] = make_uint4(w[0], w[1], w[2], w[3]);
+            nt_store(reinterpret_cast<uint4*>(dst + h) + k, make_uint4(w[0], w[1], w[2], w[3]));
         }
         for (int64_t k = h + body * 16 + tid; k < tile_total; k += kTile) dst[k] = s_heap[k];
         // views from the LDS image
@@ -176,7 +176,7 @@ __global__ __launch_bounds__(kTile) void fsst_decode(const uint64_t* __restrict_
             }
             uint4 q;
             __builtin_memcpy(&q, b, 16);
-            views[i] = q;
+            nt_store(views + i, q);
         }
     } else {
         // direct path: decode straight into HBM
@@ -214,7 +214,7 @@ __global__ __launch_bounds__(kTile) void fsst_decode(const uint64_t* __restrict_
             }
             uint4 q;
             __builtin_memcpy(&q, b, 16);
-            views[i] = q;
+            nt_store(views + i, q);
         }
     }
 }

@@ -138,7 +138,7 @@ __global__ __launch_bounds__(kBlock) void for_kernel(const E* __restrict__ in, u
             e[j] = v;
         }
         __builtin_memcpy(&q, e, 16);
-        reinterpret_cast<uint4*>(out)[i] = q;
+        nt_store(reinterpret_cast<uint4*>(out) + i, q);
     }
     for (uint64_t i = nv * V + uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
         E v = E(E(in[i] << shift) + ref);
@@ -196,7 +196,7 @@ __global__ __launch_bounds__(kBlock) void alp_kernel(const I* __restrict__ in, u
             else o[j] = __dmul_rn(__dmul_rn(F(e[j]), a), b);
         }
         __builtin_memcpy(&q, o, 16);
-        reinterpret_cast<uint4*>(out)[i] = q;
+        nt_store(reinterpret_cast<uint4*>(out) + i, q);
     }
     for (uint64_t i = nv * V + uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
         if constexpr (sizeof(F) == 4) out[i] = __fmul_rn(__fmul_rn(F(in[i]), a), b);
@@ -233,7 +233,7 @@ __global__ __launch_bounds__(kBlock) void take_kernel(const V* __restrict__ valu
             __hip_atomic_fetch_or(err, kErrTakeOOB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             c = 0;
         }
-        out[i] = values[c];
+        nt_store(out + i, values[c]);
     }
 }
 
@@ -419,12 +419,20 @@ __global__ __launch_bounds__(kBlock) void delta_kernel(const E* __restrict__ bas
         run[r] = prev;
     }
     const int64_t o0 = int64_t(blk * 1024 + base_l) - int64_t(offset);
-    if (o0 >= 0 && uint64_t(o0) + T <= len && ((reinterpret_cast<uintptr_t>(out + o0) & 15) == 0)) {
+    constexpr int RUN_BYTES = T * int(sizeof(E));  // 8 B for u8, 32/128/512 B otherwise
+    constexpr int ALIGN = RUN_BYTES < 16 ? RUN_BYTES : 16;
+    if (o0 >= 0 && uint64_t(o0) + T <= len && ((reinterpret_cast<uintptr_t>(out + o0) & (ALIGN - 1)) == 0)) {
+        if constexpr (RUN_BYTES < 16) {
+            uint2 q;
+            __builtin_memcpy(&q, run, 8);
+            *reinterpret_cast<uint2*>(out + o0) = q;
+        } else {
 #pragma unroll
-        for (int k = 0; k < T * int(sizeof(E)) / 16; k++) {
-            uint4 q;
-            __builtin_memcpy(&q, reinterpret_cast<const uint8_t*>(run) + 16 * k, 16);
-            reinterpret_cast<uint4*>(out + o0)[k] = q;
+            for (int k = 0; k < RUN_BYTES / 16; k++) {
+                uint4 q;
+                __builtin_memcpy(&q, reinterpret_cast<const uint8_t*>(run) + 16 * k, 16);
+                nt_store(reinterpret_cast<uint4*>(out + o0) + k, q);
+            }
         }
     } else {
 #pragma unroll
@@ -507,7 +515,7 @@ __global__ __launch_bounds__(kBlock) void runend_kernel(const V* __restrict__ va
                 r++;
                 end = load_uint(ends, ends_width, false, r) - offset;
             }
-            out[j] = values[r];
+            nt_store(out + j, values[r]);
         }
     }
 }
@@ -536,7 +544,7 @@ vxg_status launch_runend(int value_width, const void* values, int ends_width, co
 template <typename V>
 __global__ __launch_bounds__(kBlock) void fill_kernel(V v, uint64_t n, V* __restrict__ out) {
     const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
-    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) out[i] = v;
+    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) nt_store(out + i, v);
 }
 
 vxg_status launch_fill(int value_width, const uint8_t* scalar16, uint64_t n, void* out, hipStream_t s) {

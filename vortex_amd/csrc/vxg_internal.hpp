@@ -20,6 +20,20 @@ __host__ __device__ constexpr int fl_index(int row, int lane) {
     return fl_order(row / 8) * 16 + (row % 8) * 128 + lane;
 }
 
+// Non-temporal (streaming) store of one value: decoded outputs are written once and not
+// re-read by the producing launch (uint4 via a native vector type; scalars directly).
+template <typename V>
+__device__ __forceinline__ void nt_store(V* p, const V& v) {
+    if constexpr (sizeof(V) == 16) {
+        using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
+        u32x4 vv;
+        __builtin_memcpy(&vv, &v, 16);
+        __builtin_nontemporal_store(vv, reinterpret_cast<u32x4*>(p));
+    } else {
+        __builtin_nontemporal_store(v, p);
+    }
+}
+
 inline int ptype_width(int p) {
     switch (p) {
     case VXG_U8: case VXG_I8: return 1;
