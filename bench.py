@@ -65,24 +65,32 @@ def make_c2(rng):
                      values=n, read_bytes=arr.nbytes(), write_bytes=vals.nbytes, dtype="f64")
 
 
-def make_c3_shard(rng, world: int):
-    """C3: Chunked x256 [Dict(codes=BitPacked u64 W=10, values=Primitive u64[1024])], 128 Mi
-    values in total; this rank's shard is 256/world... capped at 32 chunks per GPU (the
-    8-GPU share) so per-GPU work is fixed (weak scaling)."""
+def make_c3_shard(rng, world: int, rank: int):
+    """C3: Chunked[Dict(codes=BitPacked u64 W=10, values=Primitive u64[1024])] with 512 Ki
+    values per chunk.  BASELINE's config is 256 chunks (128 Mi values) over 8 GPUs = 32 chunks
+    per GPU; to keep per-GPU work fixed as N grows (weak scaling) the global array has 32*N
+    chunks, and this rank decodes the contiguous chunk range vortex_amd.shard.plan_shards gives
+    it (balanced by compressed bytes).  Chunk c is generated from seed c, so every rank agrees
+    on the global array without communicating."""
     import vortex_amd.arrays as A
     import vortex_amd.encode as E
+    from vortex_amd.shard import plan_shards
     per_chunk = (128 << 20) // 256
-    n_chunks = 32
+    n_global = 32 * world
+    packed_bytes = (per_chunk // 1024) * 128 * 10 + 1024 * 8
+    mine = plan_shards([packed_bytes] * n_global, world)[rank]
     chunks = []
-    for _ in range(n_chunks):
-        dv = rng.integers(0, 2 ** 63, 1024, dtype=np.uint64)
-        codes = (rng.zipf(1.1, per_chunk) - 1) % 1024
+    for c in mine:
+        r = np.random.default_rng(1000 + c)
+        dv = r.integers(0, 2 ** 63, 1024, dtype=np.uint64)
+        codes = (r.zipf(1.1, per_chunk) - 1) % 1024
         chunks.append(A.dict_array(A.primitive(dv),
                                    A.bitpacked(E.bitpack_buffer(codes.astype(np.uint64), 10), "u64", 10, per_chunk)))
     arr = A.chunked(chunks)
     return arr, dict(name="C3", encoding="vortex.chunked[vortex.dict(codes=fastlanes.bitpacked u64 W=10)] u64",
-                     values=n_chunks * per_chunk, read_bytes=arr.nbytes(), write_bytes=n_chunks * per_chunk * 8,
-                     dtype="u64", chunks_per_gpu=n_chunks)
+                     values=len(mine) * per_chunk, read_bytes=arr.nbytes() - 8 * (len(mine) + 1),
+                     write_bytes=len(mine) * per_chunk * 8, dtype="u64", chunks_per_gpu=len(mine),
+                     chunk_range=[mine.start, mine.stop], global_chunks=n_global)
 
 
 WORDS = (b"furiously regular deposits sleep carefully final accounts ironic packages blithely "
@@ -179,6 +187,64 @@ def run_workload(wl: Workload, steps: int, warmup: int, dist, rank: int):
     return elapsed, float(np.mean(kms)), float(np.median(kms))
 
 
+def run_e2e(arr, info, ctx, reps: int = 5):
+    """Host -> host rate: compressed buffers in pinned host memory are copied H2D, decoded,
+    and the canonical output copied D2H into pinned host memory (PCIe Gen5 x16 both ways).
+    Returns decoded GB/s over the whole round trip and the H2D/D2H byte counts."""
+    import torch
+    import vortex_amd.arrays as A
+    dev = torch.device("cuda", ctx.device)
+
+    def pin(a):
+        return A.Array(a.encoding, a.len, a.dtype, a.ptype, a.nullable, a.validity, dict(a.meta),
+                       [torch.from_numpy(np.ascontiguousarray(b).view(np.uint8).reshape(-1).copy()).pin_memory()
+                        for b in a.buffers], [pin(c) for c in a.children])
+
+    host = pin(arr)
+    dev_tree = host.to(dev)  # allocate device buffers once (shapes fixed)
+
+    def h2d(src, dst):
+        for s, d in zip(src.buffers, dst.buffers):
+            if s.numel():
+                d.copy_(s, non_blocking=True)
+        for s, d in zip(src.children, dst.children):
+            h2d(s, d)
+
+    keep = []
+    node = A.flatten(dev_tree, keep)
+    vb, db = C.c_uint64(), C.c_uint64()
+    chk(ctx.lib.vxg_canonical_size(ctx.handle, C.byref(node), C.byref(vb), C.byref(db)))
+    out = A._lib.VxgCanonical()
+    prim = arr.dtype == A.DTYPE["PRIMITIVE"]
+    if prim:
+        dv = torch.empty(vb.value, dtype=torch.uint8, device=dev)
+        out.values = dv.data_ptr()
+        hv = torch.empty(vb.value, dtype=torch.uint8).pin_memory()
+    else:
+        dv = torch.empty(vb.value, dtype=torch.uint8, device=dev)
+        dd = torch.empty(db.value + 16, dtype=torch.uint8, device=dev)
+        out.views, out.data, out.data_bytes = dv.data_ptr(), dd.data_ptr(), db.value
+        hv = torch.empty(vb.value, dtype=torch.uint8).pin_memory()
+        hd = torch.empty(db.value + 16, dtype=torch.uint8).pin_memory()
+    times = []
+    for _ in range(reps + 1):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        h2d(host, dev_tree)
+        chk(ctx.lib.vxg_canonicalize(ctx.handle, C.byref(node), C.byref(out), ctx.stream_ptr()))
+        hv.copy_(dv, non_blocking=True)
+        if not prim:
+            hd.copy_(dd, non_blocking=True)
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    ctx.sync()
+    t = float(np.median(times[1:]))
+    d2h = vb.value + (0 if prim else db.value)
+    return dict(e2e_ms=round(t * 1e3, 3), e2e_decoded_GBps=round(info["write_bytes"] / t / 1e9, 2),
+                h2d_bytes=arr.nbytes(), d2h_bytes=int(d2h),
+                pcie_GBps_effective=round((arr.nbytes() + d2h) / t / 1e9, 2))
+
+
 def pmc_traffic(name: str):
     """Per-launch HBM bytes of the dominant kernel from committed rocprofv3 PMC summaries
     (profiles/pmc_traffic.json, written by tools/pmc_traffic.py: FETCH_SIZE*2 + WRITE_SIZE,
@@ -226,6 +292,8 @@ def main():
                     help="comma list; c1 is the headline, others go under 'encodings'")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--e2e", action="store_true",
+                    help="also measure host->host (H2D + decode + D2H over PCIe); never the headline value")
     args = ap.parse_args()
 
     import torch
@@ -243,12 +311,13 @@ def main():
     import vortex_amd as V
     ctx = V.Context(local)
     rng = np.random.default_rng(42 + rank)
-    makers = {"c1": make_c1, "c2": make_c2, "c3": lambda r: make_c3_shard(r, world), "c4": make_c4}
+    makers = {"c1": make_c1, "c2": make_c2, "c3": lambda r: make_c3_shard(r, world, rank), "c4": make_c4}
     copies = {"c1": 4, "c2": 1, "c3": 2, "c4": 1}
     results = {}
     for key in [w.strip() for w in args.workloads.split(",") if w.strip()]:
         t0 = time.perf_counter()
         arr, info = makers[key](rng)
+        e2e = run_e2e(arr, info, ctx) if args.e2e else None
         wl = Workload(arr, info, ctx, copies[key])
         del arr
         if rank == 0:
@@ -259,7 +328,7 @@ def main():
         algo = info["read_bytes"] + info["write_bytes"]
         results[key] = dict(info=info, elapsed=elapsed, ms_per_step=per_step * 1e3, kernel_ms_mean=kmean,
                             kernel_ms_median=kmed, algo_bytes=algo,
-                            value=world * info["write_bytes"] * steps / elapsed / 1e9)
+                            value=world * info["write_bytes"] * steps / elapsed / 1e9, e2e=e2e)
         del wl
         torch.cuda.empty_cache()
 
@@ -300,6 +369,8 @@ def main():
                 "hbm_frac_algorithmic": round(r["algo_bytes"] / (r["kernel_ms_mean"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
                 "kernel_ms_mean": round(r["kernel_ms_mean"], 5), "ms_per_step": round(r["ms_per_step"], 5),
                 "read_bytes": i["read_bytes"], "write_bytes": i["write_bytes"]}
+            if r.get("e2e"):
+                line["encodings"][i["name"]]["host_to_host"] = r["e2e"]
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
         print(json.dumps(line), flush=True)

@@ -52,6 +52,24 @@ vxg_status hip_check(hipError_t e, const char* what) {
                      std::string(what) + ": " + hipGetErrorString(e));
 }
 
+static std::mutex g_stage_mu;
+
+vxg_status stage_upload(Ctx& c, const void* src, size_t bytes, void* dst, hipStream_t s) {
+    if (bytes > kStageBytes) {  // rare: large tables take a synchronous copy
+        vxg_status st = hip_check(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s), "table upload");
+        if (st != VXG_OK) return st;
+        return hip_check(hipStreamSynchronize(s), "table upload sync");
+    }
+    std::lock_guard<std::mutex> lk(g_stage_mu);
+    const unsigned slot = c.stage_next++ % kStageSlots;
+    vxg_status st = hip_check(hipEventSynchronize(c.stage_ev[slot]), "stage slot wait");
+    if (st != VXG_OK) return st;
+    std::memcpy(c.stage[slot], src, bytes);
+    st = hip_check(hipMemcpyAsync(dst, c.stage[slot], bytes, hipMemcpyHostToDevice, s), "table upload");
+    if (st != VXG_OK) return st;
+    return hip_check(hipEventRecord(c.stage_ev[slot], s), "stage slot record");
+}
+
 // K1 dispatch over the instantiation units.
 vxg_status launch_fl_unpack(int T, int W, Epi epi, int vw, const UnpackArgs& a, hipStream_t s) {
     if (W < 0 || W > T) return set_error(VXG_ERR_INVALID_ARGUMENT, "bit width out of range");
@@ -344,10 +362,7 @@ vxg_status Planner::decode_chunked_primitive(const vxg_array& a, void* dst) {
         if (grouped) {
             void* d;
             VXG_TRY(temp(n * sizeof(DictChunkDev), &d));
-            VXG_TRY(hip_check(hipMemcpyAsync(d, h.data(), n * sizeof(DictChunkDev), hipMemcpyHostToDevice, s_),
-                              "chunk table upload"));
-            // the host table must stay alive until the async copy has consumed it
-            VXG_TRY(hip_check(hipStreamSynchronize(s_), "chunk table sync"));
+            VXG_TRY(stage_upload(ctx_->c, h.data(), n * sizeof(DictChunkDev), d, s_));
             return launch_fl_unpack_dict_chunks(T, W, vw, static_cast<DictChunkDev*>(d), uint32_t(n), groups,
                                                 ctx_->c.err_word, s_);
         }
@@ -745,9 +760,13 @@ vxg_status vxg_open(int device, vxg_ctx** out) {
     c->c.device = device;
     hipError_t e = hipMalloc(&c->c.err_word, 16);
     if (e == hipSuccess) e = hipMemset(c->c.err_word, 0, 16);
+    for (int i = 0; i < kStageSlots && e == hipSuccess; i++) {
+        e = hipHostMalloc(&c->c.stage[i], kStageBytes, hipHostMallocDefault);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&c->c.stage_ev[i], hipEventDisableTiming);
+    }
     if (e != hipSuccess) {
-        delete c;
-        return hip_check(e, "error word");
+        vxg_close(c);
+        return hip_check(e, "context setup");
     }
     *out = c;
     return VXG_OK;
@@ -756,7 +775,12 @@ vxg_status vxg_open(int device, vxg_ctx** out) {
 vxg_status vxg_close(vxg_ctx* ctx) {
     if (!ctx) return VXG_OK;
     (void)hipSetDevice(ctx->c.device);
-    (void)hipFree(ctx->c.err_word);
+    (void)hipDeviceSynchronize();
+    if (ctx->c.err_word) (void)hipFree(ctx->c.err_word);
+    for (int i = 0; i < kStageSlots; i++) {
+        if (ctx->c.stage_ev[i]) (void)hipEventDestroy(ctx->c.stage_ev[i]);
+        if (ctx->c.stage[i]) (void)hipHostFree(ctx->c.stage[i]);
+    }
     delete ctx;
     return VXG_OK;
 }
@@ -886,9 +910,7 @@ vxg_status vxg_bitunpack_dict_chunks(vxg_ctx* ctx, int codes_ptype, unsigned bit
     }
     void* d;
     VXG_TRY(hip_check(hipMallocAsync(&d, n_chunks * sizeof(DictChunkDev) + 16, S(stream)), "chunk table"));
-    VXG_TRY(hip_check(hipMemcpyAsync(d, h.data(), n_chunks * sizeof(DictChunkDev), hipMemcpyHostToDevice,
-                                     S(stream)), "chunk table upload"));
-    VXG_TRY(hip_check(hipStreamSynchronize(S(stream)), "chunk table sync"));
+    VXG_TRY(stage_upload(ctx->c, h.data(), n_chunks * sizeof(DictChunkDev), d, S(stream)));
     vxg_status st = launch_fl_unpack_dict_chunks(unsigned_T(codes_ptype), int(bit_width), int(value_width),
                                                  static_cast<DictChunkDev*>(d), n_chunks, groups,
                                                  ctx->c.err_word, S(stream));

@@ -56,10 +56,22 @@ extern const double kIF10d[24];
 // Device error word bits (set by kernels, read by vxg_check via vxg_stream_sync).
 enum : uint32_t { kErrTakeOOB = 1u, kErrPatchOOB = 2u, kErrRunEnd = 4u };
 
+// Pinned host staging ring for small per-launch tables (chunk descriptors): the host copy is
+// reused only after the event recorded behind its async H2D copy has completed, so uploads
+// never synchronise the stream.
+constexpr int kStageSlots = 8;
+constexpr size_t kStageBytes = 1 << 20;
+
 struct Ctx {
     int device = 0;
     uint32_t* err_word = nullptr;  // device
+    void* stage[kStageSlots] = {};
+    hipEvent_t stage_ev[kStageSlots] = {};
+    unsigned stage_next = 0;
 };
+
+// Copy `bytes` of host memory to device `dst` on stream `s` without synchronising.
+vxg_status stage_upload(Ctx& c, const void* src, size_t bytes, void* dst, hipStream_t s);
 
 vxg_status set_error(vxg_status s, const std::string& msg);
 vxg_status hip_check(hipError_t e, const char* what);
