@@ -165,20 +165,27 @@ def run_workload(wl: Workload, steps: int, warmup: int, dist, rank: int):
     for _ in range(warmup):
         wl.step()
     wl.ctx.sync()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    # timed region: exactly `steps` steps, barrier + synchronize on both sides, no events
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for s in range(steps):
-        ev[s][0].record()
         wl.step()
-        ev[s][1].record()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     wl.ctx.sync()  # surfaces device-side errors (OOB codes, ...)
+    # separate pass for the per-launch device time: HIP events on the decode stream (torch's
+    # current stream, which is the stream vxg_canonicalize is given) around each step
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    for s in range(steps):
+        ev[s][0].record()
+        wl.step()
+        ev[s][1].record()
+    torch.cuda.synchronize()
+    wl.ctx.sync()
     kms = [a.elapsed_time(b) for a, b in ev]
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")

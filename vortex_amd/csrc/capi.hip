@@ -8,6 +8,7 @@
 // does not recognise is decoded child-first into temporaries exactly like the reference.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
@@ -52,24 +53,6 @@ vxg_status hip_check(hipError_t e, const char* what) {
                      std::string(what) + ": " + hipGetErrorString(e));
 }
 
-static std::mutex g_stage_mu;
-
-vxg_status stage_upload(Ctx& c, const void* src, size_t bytes, void* dst, hipStream_t s) {
-    if (bytes > kStageBytes) {  // rare: large tables take a synchronous copy
-        vxg_status st = hip_check(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s), "table upload");
-        if (st != VXG_OK) return st;
-        return hip_check(hipStreamSynchronize(s), "table upload sync");
-    }
-    std::lock_guard<std::mutex> lk(g_stage_mu);
-    const unsigned slot = c.stage_next++ % kStageSlots;
-    vxg_status st = hip_check(hipEventSynchronize(c.stage_ev[slot]), "stage slot wait");
-    if (st != VXG_OK) return st;
-    std::memcpy(c.stage[slot], src, bytes);
-    st = hip_check(hipMemcpyAsync(dst, c.stage[slot], bytes, hipMemcpyHostToDevice, s), "table upload");
-    if (st != VXG_OK) return st;
-    return hip_check(hipEventRecord(c.stage_ev[slot], s), "stage slot record");
-}
-
 // K1 dispatch over the instantiation units.
 vxg_status launch_fl_unpack(int T, int W, Epi epi, int vw, const UnpackArgs& a, hipStream_t s) {
     if (W < 0 || W > T) return set_error(VXG_ERR_INVALID_ARGUMENT, "bit width out of range");
@@ -101,15 +84,15 @@ vxg_status launch_fl_unpack(int T, int W, Epi epi, int vw, const UnpackArgs& a, 
     return VXG_ERR_INVALID_ARGUMENT;
 }
 
-vxg_status launch_fl_unpack_dict_chunks(int T, int W, int vw, const DictChunkDev* d, uint32_t n,
-                                        uint64_t g, uint32_t* err, hipStream_t s) {
+vxg_status launch_fl_unpack_dict_chunks(int T, int W, int vw, const DictChunkTable& d, uint64_t g,
+                                        uint32_t* err, hipStream_t s) {
     if (W > kDictFusedMaxW) return VXG_ERR_NOT_IMPLEMENTED;
     switch (vw) {
-    case 1: return fl_dict_chunks_1(T, W, d, n, g, err, s);
-    case 2: return fl_dict_chunks_2(T, W, d, n, g, err, s);
-    case 4: return fl_dict_chunks_4(T, W, d, n, g, err, s);
-    case 8: return fl_dict_chunks_8(T, W, d, n, g, err, s);
-    case 16: return fl_dict_chunks_16(T, W, d, n, g, err, s);
+    case 1: return fl_dict_chunks_1(T, W, d, g, err, s);
+    case 2: return fl_dict_chunks_2(T, W, d, g, err, s);
+    case 4: return fl_dict_chunks_4(T, W, d, g, err, s);
+    case 8: return fl_dict_chunks_8(T, W, d, g, err, s);
+    case 16: return fl_dict_chunks_16(T, W, d, g, err, s);
     }
     return set_error(VXG_ERR_INVALID_ARGUMENT, "bad dictionary value width");
 }
@@ -119,6 +102,25 @@ vxg_status launch_fl_unpack_dict_chunks(int T, int W, int vw, const DictChunkDev
 using namespace vxg;
 
 namespace {
+
+// Launch Dict(codes = BitPacked) chunks in batches of kArgChunks descriptors passed as the
+// kernel argument (no device table, no upload, no host synchronisation).
+vxg_status launch_chunk_batches(int T, int W, int vw, const std::vector<DictChunkDev>& chunks, uint32_t* err,
+                                hipStream_t s) {
+    for (size_t b = 0; b < chunks.size(); b += kArgChunks) {
+        DictChunkTable tab{};
+        uint64_t groups = 0;
+        tab.n = uint32_t(std::min<size_t>(kArgChunks, chunks.size() - b));
+        for (uint32_t i = 0; i < tab.n; i++) {
+            tab.c[i] = chunks[b + i];
+            tab.c[i].first_group = groups;
+            groups += (tab.c[i].n_blocks + 31) / 32;
+        }
+        vxg_status st = launch_fl_unpack_dict_chunks(T, W, vw, tab, groups, err, s);
+        if (st != VXG_OK) return st;
+    }
+    return VXG_OK;
+}
 
 #define VXG_TRY(expr)                         \
     do {                                      \
@@ -345,27 +347,19 @@ vxg_status Planner::decode_chunked_primitive(const vxg_array& a, void* dst) {
     uint64_t off = 0;
     if (grouped) {
         std::vector<DictChunkDev> h(n);
-        uint64_t groups = 0;
-        for (uint64_t i = 0; i < n; i++) {
+        for (uint64_t i = 0; i < n && grouped; i++) {
             const vxg_array& c = a.children[i + 1];
             const vxg_array& codes = *child(c, 1);
             const vxg_array& values = *child(c, 0);
             const uint64_t nblk = (c.len + 1023) / 1024;
             if (W > 0 && codes.buffers[0].len != nblk * 128ull * W)
                 return set_error(VXG_ERR_INVALID_ARGUMENT, "Chunk packed length mismatch");
+            if (((off * w) & 15) != 0) grouped = false;  // 16-B vector stores need aligned slices
             h[i] = DictChunkDev{static_cast<const uint8_t*>(codes.buffers[0].ptr), values.buffers[0].ptr,
-                                static_cast<uint8_t*>(dst) + off * w, nblk, c.len, values.len, groups};
-            if (((off * w) & 15) != 0) { grouped = false; break; }
-            groups += (nblk + 31) / 32;
+                                static_cast<uint8_t*>(dst) + off * w, nblk, c.len, values.len, 0};
             off += c.len;
         }
-        if (grouped) {
-            void* d;
-            VXG_TRY(temp(n * sizeof(DictChunkDev), &d));
-            VXG_TRY(stage_upload(ctx_->c, h.data(), n * sizeof(DictChunkDev), d, s_));
-            return launch_fl_unpack_dict_chunks(T, W, vw, static_cast<DictChunkDev*>(d), uint32_t(n), groups,
-                                                ctx_->c.err_word, s_);
-        }
+        if (grouped) return launch_chunk_batches(T, W, vw, h, ctx_->c.err_word, s_);
         off = 0;
     }
     for (uint64_t i = 0; i < n; i++) {
@@ -760,10 +754,6 @@ vxg_status vxg_open(int device, vxg_ctx** out) {
     c->c.device = device;
     hipError_t e = hipMalloc(&c->c.err_word, 16);
     if (e == hipSuccess) e = hipMemset(c->c.err_word, 0, 16);
-    for (int i = 0; i < kStageSlots && e == hipSuccess; i++) {
-        e = hipHostMalloc(&c->c.stage[i], kStageBytes, hipHostMallocDefault);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&c->c.stage_ev[i], hipEventDisableTiming);
-    }
     if (e != hipSuccess) {
         vxg_close(c);
         return hip_check(e, "context setup");
@@ -777,10 +767,6 @@ vxg_status vxg_close(vxg_ctx* ctx) {
     (void)hipSetDevice(ctx->c.device);
     (void)hipDeviceSynchronize();
     if (ctx->c.err_word) (void)hipFree(ctx->c.err_word);
-    for (int i = 0; i < kStageSlots; i++) {
-        if (ctx->c.stage_ev[i]) (void)hipEventDestroy(ctx->c.stage_ev[i]);
-        if (ctx->c.stage[i]) (void)hipHostFree(ctx->c.stage[i]);
-    }
     delete ctx;
     return VXG_OK;
 }
@@ -897,7 +883,6 @@ vxg_status vxg_bitunpack_dict_chunks(vxg_ctx* ctx, int codes_ptype, unsigned bit
     if (bit_width > unsigned(kDictFusedMaxW))
         return set_error(VXG_ERR_NOT_IMPLEMENTED, "fused dict decode supports code widths <= 16");
     std::vector<DictChunkDev> h(n_chunks);
-    uint64_t groups = 0;
     for (uint32_t i = 0; i < n_chunks; i++) {
         const vxg_dict_chunk& c = chunks_host[i];
         if (c.n_blocks != (c.len + 1023) / 1024)
@@ -905,17 +890,10 @@ vxg_status vxg_bitunpack_dict_chunks(vxg_ctx* ctx, int codes_ptype, unsigned bit
         if ((reinterpret_cast<uintptr_t>(c.out) | reinterpret_cast<uintptr_t>(c.packed)) & 15)
             return set_error(VXG_ERR_INVALID_ARGUMENT, "chunk buffers must be 16-byte aligned");
         h[i] = DictChunkDev{static_cast<const uint8_t*>(c.packed), c.dict_values, c.out, c.n_blocks, c.len,
-                            c.dict_len, groups};
-        groups += (c.n_blocks + 31) / 32;
+                            c.dict_len, 0};
     }
-    void* d;
-    VXG_TRY(hip_check(hipMallocAsync(&d, n_chunks * sizeof(DictChunkDev) + 16, S(stream)), "chunk table"));
-    VXG_TRY(stage_upload(ctx->c, h.data(), n_chunks * sizeof(DictChunkDev), d, S(stream)));
-    vxg_status st = launch_fl_unpack_dict_chunks(unsigned_T(codes_ptype), int(bit_width), int(value_width),
-                                                 static_cast<DictChunkDev*>(d), n_chunks, groups,
-                                                 ctx->c.err_word, S(stream));
-    (void)hipFreeAsync(d, S(stream));
-    return st;
+    return launch_chunk_batches(unsigned_T(codes_ptype), int(bit_width), int(value_width), h, ctx->c.err_word,
+                                S(stream));
 }
 
 vxg_status vxg_patch(vxg_ctx* ctx, int ptype, void* out, uint64_t out_len, int indices_ptype, const void* indices,

@@ -35,10 +35,9 @@ static vxg_status dict_w(int W, const UnpackArgs& a, hipStream_t s) {
     return dispatch_w<T, Epi::Dict, FL_VW, WM>(W, a, s);
 }
 template <int T>
-static vxg_status chunks_w(int W, const DictChunkDev* d, uint32_t n, uint64_t g, uint32_t* err,
-                           hipStream_t s) {
+static vxg_status chunks_w(int W, const DictChunkTable& d, uint64_t g, uint32_t* err, hipStream_t s) {
     constexpr int WM = T < kDictMaxW ? T : kDictMaxW;
-    return dispatch_chunks_w_impl<T, Epi::Dict, FL_VW>(W, d, n, g, err, s,
+    return dispatch_chunks_w_impl<T, Epi::Dict, FL_VW>(W, d, g, err, s,
                                                        std::make_integer_sequence<int, WM + 1>{});
 }
 vxg_status FL_CAT(fl_dict_, FL_VW)(int T, int W, const UnpackArgs& a, hipStream_t s) {
@@ -50,13 +49,13 @@ vxg_status FL_CAT(fl_dict_, FL_VW)(int T, int W, const UnpackArgs& a, hipStream_
     default: return VXG_ERR_INVALID_ARGUMENT;
     }
 }
-vxg_status FL_CAT(fl_dict_chunks_, FL_VW)(int T, int W, const DictChunkDev* d, uint32_t n,
-                                          uint64_t g, uint32_t* err, hipStream_t s) {
+vxg_status FL_CAT(fl_dict_chunks_, FL_VW)(int T, int W, const DictChunkTable& d, uint64_t g,
+                                          uint32_t* err, hipStream_t s) {
     switch (T) {
-    case 8: return chunks_w<8>(W, d, n, g, err, s);
-    case 16: return chunks_w<16>(W, d, n, g, err, s);
-    case 32: return chunks_w<32>(W, d, n, g, err, s);
-    case 64: return chunks_w<64>(W, d, n, g, err, s);
+    case 8: return chunks_w<8>(W, d, g, err, s);
+    case 16: return chunks_w<16>(W, d, g, err, s);
+    case 32: return chunks_w<32>(W, d, g, err, s);
+    case 64: return chunks_w<64>(W, d, g, err, s);
     default: return VXG_ERR_INVALID_ARGUMENT;
     }
 }

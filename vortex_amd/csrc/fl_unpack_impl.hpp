@@ -280,17 +280,17 @@ __global__ __launch_bounds__(256) void fl_unpack_kernel(const uint8_t* __restric
 // Many independent chunks (e.g. Chunked[Dict(BitPacked)]) in one launch; each workgroup of
 // 256 threads covers 32 blocks of exactly one chunk.
 template <int T, int W, Epi EPI, int VW>
-__global__ __launch_bounds__(256) void fl_unpack_chunks_kernel(const DictChunkDev* __restrict__ chunks,
-                                                               uint32_t n_chunks, EpiParams ep0) {
+__global__ __launch_bounds__(256) void fl_unpack_chunks_kernel(DictChunkTable tab, EpiParams ep0) {
     using O = typename EpiOut<T, EPI, VW>::type;
-    // binary search the chunk owning this workgroup
-    uint32_t lo = 0, hi = n_chunks;
+    // the chunk table is a kernel argument (no upload, no host sync); workgroup-uniform
+    // binary search on first_group
+    uint32_t lo = 0, hi = tab.n;
     const uint64_t g = blockIdx.x;
     while (hi - lo > 1) {
-        uint32_t mid = (lo + hi) >> 1;
-        if (chunks[mid].first_group <= g) lo = mid; else hi = mid;
+        const uint32_t mid = (lo + hi) >> 1;
+        if (tab.c[mid].first_group <= g) lo = mid; else hi = mid;
     }
-    const DictChunkDev c = chunks[lo];
+    const DictChunkDev c = tab.c[lo];
     const uint64_t blk = (g - c.first_group) * 32 + (threadIdx.x >> 3);
     const int t = int(threadIdx.x & 7);
     if (blk >= c.n_blocks) return;
@@ -299,7 +299,7 @@ __global__ __launch_bounds__(256) void fl_unpack_chunks_kernel(const DictChunkDe
     ep.dict_len = c.dict_len;
     const bool full = (blk + 1) * 1024 <= c.len;
     unpack_block<T, W, EPI, VW, kOutNT>(c.packed + blk * (128 * W), t, static_cast<O*>(c.out),
-                                int64_t(blk * 1024), full, c.len, ep);
+                                        int64_t(blk * 1024), full, c.len, ep);
 }
 
 inline EpiParams to_epi(const UnpackArgs& a) {
@@ -325,13 +325,12 @@ vxg_status launch_one(const UnpackArgs& a, hipStream_t s) {
 }
 
 template <int T, int W, Epi EPI, int VW>
-vxg_status launch_chunks_one(const DictChunkDev* d_chunks, uint32_t n_chunks, uint64_t total_groups,
-                             uint32_t* err, hipStream_t s) {
+vxg_status launch_chunks_one(const DictChunkTable& tab, uint64_t total_groups, uint32_t* err, hipStream_t s) {
     if (total_groups == 0) return VXG_OK;
     EpiParams ep{};
     ep.err = err;
     hipLaunchKernelGGL((fl_unpack_chunks_kernel<T, W, EPI, VW>), dim3(unsigned(total_groups)),
-                       dim3(256), 0, s, d_chunks, n_chunks, ep);
+                       dim3(256), 0, s, tab, ep);
     return hip_check(hipGetLastError(), "fl_unpack_chunks_kernel launch");
 }
 
@@ -351,12 +350,12 @@ vxg_status dispatch_w(int W, const UnpackArgs& a, hipStream_t s) {
 }
 
 template <int T, Epi EPI, int VW, int... Ws>
-vxg_status dispatch_chunks_w_impl(int W, const DictChunkDev* d, uint32_t n, uint64_t g, uint32_t* err,
+vxg_status dispatch_chunks_w_impl(int W, const DictChunkTable& tab, uint64_t g, uint32_t* err,
                                   hipStream_t s, std::integer_sequence<int, Ws...>) {
-    using Fn = vxg_status (*)(const DictChunkDev*, uint32_t, uint64_t, uint32_t*, hipStream_t);
+    using Fn = vxg_status (*)(const DictChunkTable&, uint64_t, uint32_t*, hipStream_t);
     static constexpr Fn table[] = {&launch_chunks_one<T, Ws, EPI, VW>...};
     if (W < 0 || W >= int(sizeof...(Ws))) return VXG_ERR_NOT_IMPLEMENTED;
-    return table[W](d, n, g, err, s);
+    return table[W](tab, g, err, s);
 }
 
 }  // namespace vxg

@@ -6,13 +6,16 @@
 //
 // Design: per-string code slices never straddle an escape, so the bulk decode equals the
 // concatenation of per-string decodes placed at the exclusive prefix sum of the lengths.
-//   kernel 1 (tile_sums):   one 256-string tile per workgroup -> sum of lengths
-//   kernel 2 (scan_tiles):  single workgroup exclusive scan of the tile sums (chunked loop)
-//   kernel 3 (decode):      per tile: (a) block-scan lengths -> output offsets, (b) stage the
-//                           tile's contiguous code bytes into LDS with coalesced loads,
-//                           (c) thread-per-string decode from LDS into an LDS heap image using
-//                           the symbol table held in LDS, (d) coalesced copy of the heap image
-//                           to HBM, (e) 16-byte views written coalesced (inline <= 12 bytes).
+//   kernel 1 (tile_sums):   one 256-string tile per workgroup -> sum of its lengths
+//   kernel 2 (scan_blocks): 1024 tiles per workgroup -> exclusive tile prefix inside the
+//                           1024-tile block + one total per block (coalesced, fully parallel)
+//   kernel 3 (decode):      per tile: (a) block prefix = sum of the preceding block totals
+//                           (one wave, parallel loads), (b) block-scan of lengths -> offsets,
+//                           (c) stage the tile's contiguous code bytes into LDS with coalesced
+//                           loads, (d) thread-per-string decode from LDS into an LDS heap image
+//                           with the symbol table in LDS, (e) coalesced copy-out of the image,
+//                           (f) 16-byte views (inline <= 12 bytes) built with compile-time byte
+//                           positions (no runtime-indexed register arrays -> no scratch).
 //   Tiles whose codes or output do not fit the LDS images take a direct-to-HBM path.
 #include "vxg_internal.hpp"
 
@@ -23,6 +26,7 @@ namespace {
 constexpr int kTile = 256;            // strings per tile = threads per workgroup
 constexpr int kCodeLds = 16 * 1024;   // staged code bytes per tile
 constexpr int kHeapLds = 32 * 1024;   // staged output bytes per tile
+constexpr int kScanBlock = 1024;      // tiles per scan_blocks workgroup
 
 __device__ __forceinline__ int64_t load_int(const void* p, int width, bool sgn, uint64_t i) {
     switch (width) {
@@ -33,7 +37,14 @@ __device__ __forceinline__ int64_t load_int(const void* p, int width, bool sgn, 
     }
 }
 
-// Block-wide exclusive scan of one int64 per thread (256 threads = 4 waves).
+__device__ __forceinline__ int64_t wave_sum(int64_t x) {
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) x += __shfl_xor(x, d, 64);
+    return x;
+}
+
+// Block-wide exclusive scan of one int64 per thread (NW waves).
+template <int NW>
 __device__ __forceinline__ int64_t block_exclusive_scan(int64_t v, int64_t* wave_sums, int64_t& total) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     int64_t x = v;
@@ -44,54 +55,61 @@ __device__ __forceinline__ int64_t block_exclusive_scan(int64_t v, int64_t* wave
     }
     if (lane == 63) wave_sums[wave] = x;
     __syncthreads();
-    int64_t before = 0;
-    for (int w = 0; w < wave; w++) before += wave_sums[w];
-    total = wave_sums[0] + wave_sums[1] + wave_sums[2] + wave_sums[3];
+    int64_t before = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < NW; w++) {
+        const int64_t s = wave_sums[w];
+        before += w < wave ? s : 0;
+        tot += s;
+    }
+    total = tot;
     __syncthreads();
     return before + x - v;
+}
+
+// arrow-array 53.2 make_view: len <= 12 -> [len][bytes, zero padded]; else
+// [len][first 4 bytes][buffer_index = 0][offset].  `get(j)` returns byte j of the string (only
+// called for j < 12 inline / j < 4 prefix, and masked by j < len).
+template <typename Get>
+__device__ __forceinline__ uint4 build_view(uint32_t len, uint32_t offset, Get get) {
+    uint32_t w1 = 0, w2 = 0, w3 = 0;
+    if (len <= 12) {
+#pragma unroll
+        for (int j = 0; j < 12; j++) {
+            const uint32_t b = uint32_t(j) < len ? uint32_t(get(j)) : 0u;
+            if (j < 4) w1 |= b << (8 * j);
+            else if (j < 8) w2 |= b << (8 * (j - 4));
+            else w3 |= b << (8 * (j - 8));
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; j++) w1 |= uint32_t(get(j)) << (8 * j);
+        w3 = offset;
+    }
+    return make_uint4(len, w1, w2, w3);
 }
 
 }  // namespace
 
 __global__ __launch_bounds__(kTile) void fsst_tile_sums(const void* lens, int lens_width, int lens_signed,
                                                         uint64_t n, int64_t* __restrict__ tile_sums) {
-    __shared__ int64_t ws[4];
+    __shared__ int64_t ws[kTile / 64];
     const uint64_t i = uint64_t(blockIdx.x) * kTile + threadIdx.x;
-    const int64_t v = i < n ? load_int(lens, lens_width, lens_signed != 0, i) : 0;
-    int64_t tot;
-    (void)block_exclusive_scan(v, ws, tot);
-    if (threadIdx.x == 0) tile_sums[blockIdx.x] = tot;
+    const int64_t v = wave_sum(i < n ? load_int(lens, lens_width, lens_signed != 0, i) : 0);
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) tile_sums[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
 }
 
-// Exclusive scan of the tile sums by ONE 1024-thread workgroup: thread k sums a contiguous
-// run of ceil(n_tiles/1024) tiles, the 1024 partials are block-scanned (16 waves), then each
-// thread rewrites its run.  Two passes over n_tiles (~23 K for C4) instead of a serial
-// 256-wide loop (70 us -> a few us).
-constexpr int kScanThreads = 1024;
-__global__ __launch_bounds__(kScanThreads) void fsst_scan_tiles(int64_t* __restrict__ tile_sums, uint64_t n_tiles) {
-    __shared__ int64_t wsum[kScanThreads / 64];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint64_t per = (n_tiles + kScanThreads - 1) / kScanThreads;
-    const uint64_t lo = uint64_t(tid) * per;
-    const uint64_t hi = lo + per < n_tiles ? lo + per : n_tiles;
-    int64_t s = 0;
-    for (uint64_t i = lo; i < hi; i++) s += tile_sums[i];
-    int64_t x = s;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const int64_t y = __shfl_up(x, d, 64);
-        if (lane >= d) x += y;
-    }
-    if (lane == 63) wsum[wave] = x;
-    __syncthreads();
-    int64_t before = 0;
-    for (int w = 0; w < wave; w++) before += wsum[w];
-    int64_t run = before + x - s;  // exclusive prefix of this thread's run
-    for (uint64_t i = lo; i < hi; i++) {
-        const int64_t v = tile_sums[i];
-        tile_sums[i] = run;
-        run += v;
-    }
+__global__ __launch_bounds__(kScanBlock) void fsst_scan_blocks(int64_t* __restrict__ tile_sums, uint64_t n_tiles,
+                                                               int64_t* __restrict__ block_totals) {
+    __shared__ int64_t ws[kScanBlock / 64];
+    const uint64_t i = uint64_t(blockIdx.x) * kScanBlock + threadIdx.x;
+    const int64_t v = i < n_tiles ? tile_sums[i] : 0;
+    int64_t tot;
+    const int64_t ex = block_exclusive_scan<kScanBlock / 64>(v, ws, tot);
+    if (i < n_tiles) tile_sums[i] = ex;
+    if (threadIdx.x == 0) block_totals[blockIdx.x] = tot;
 }
 
 __global__ __launch_bounds__(kTile) void fsst_decode(const uint64_t* __restrict__ symbols,
@@ -101,10 +119,12 @@ __global__ __launch_bounds__(kTile) void fsst_decode(const uint64_t* __restrict_
                                                      int lens_signed, uint64_t n,
                                                      const uint8_t* __restrict__ validity,
                                                      const int64_t* __restrict__ tile_prefix,
+                                                     const int64_t* __restrict__ block_totals,
                                                      uint8_t* __restrict__ heap, uint4* __restrict__ views) {
     __shared__ uint64_t s_sym[256];
     __shared__ uint8_t s_len[256];
-    __shared__ int64_t ws[4];
+    __shared__ int64_t ws[kTile / 64];
+    __shared__ int64_t s_block_prefix;
     __shared__ __attribute__((aligned(16))) uint8_t s_codes[kCodeLds];
     __shared__ __attribute__((aligned(16))) uint8_t s_heap[kHeapLds + 16];
 
@@ -113,14 +133,21 @@ __global__ __launch_bounds__(kTile) void fsst_decode(const uint64_t* __restrict_
         s_sym[k] = k < int(n_symbols) ? symbols[k] : 0;
         s_len[k] = k < int(n_symbols) ? sym_lens[k] : 0;
     }
+    if (tid < 64) {  // (a) prefix of the preceding 1024-tile blocks, one wave
+        const uint64_t nb = blockIdx.x / kScanBlock;
+        int64_t acc = 0;
+        for (uint64_t b = tid; b < nb; b += 64) acc += block_totals[b];
+        acc = wave_sum(acc);
+        if (tid == 0) s_block_prefix = acc;
+    }
     const uint64_t i = uint64_t(blockIdx.x) * kTile + tid;
     const bool live = i < n;
     const int64_t my_len = live ? load_int(lens, lens_width, lens_signed != 0, i) : 0;
     int64_t tile_total;
-    const int64_t my_rel = block_exclusive_scan(my_len, ws, tile_total);   // offset inside tile
-    const int64_t tile_out0 = tile_prefix[blockIdx.x];
-    const uint64_t last = (uint64_t(blockIdx.x) + 1) * kTile < n ? (uint64_t(blockIdx.x) + 1) * kTile : n;
+    const int64_t my_rel = block_exclusive_scan<kTile / 64>(my_len, ws, tile_total);  // (b)
+    const int64_t tile_out0 = tile_prefix[blockIdx.x] + s_block_prefix;
     const uint64_t first = uint64_t(blockIdx.x) * kTile;
+    const uint64_t last = first + kTile < n ? first + kTile : n;
     // code offsets are relative to code_offs[0] (sliced_bytes(), varbin/mod.rs:130-136)
     const int64_t c_base = load_int(code_offs, offs_width, offs_width < 8, 0);
     const int64_t c0 = load_int(code_offs, offs_width, offs_width < 8, first) - c_base;
@@ -130,18 +157,18 @@ __global__ __launch_bounds__(kTile) void fsst_decode(const uint64_t* __restrict_
     const uint8_t* gcodes = codes + c_base;
     const bool stage = (c1 - c0) <= kCodeLds && tile_total <= kHeapLds;
 
-    if (stage) {
+    if (stage) {  // (c)
         for (int64_t k = tid; k < c1 - c0; k += kTile) s_codes[k] = gcodes[c0 + k];
     }
     __syncthreads();
 
     bool valid = live;
     if (live && validity) valid = (validity[i >> 3] >> (i & 7)) & 1;
+    const uint32_t vlen = valid ? uint32_t(my_len) : 0u;
 
     if (stage) {
-        // decode from LDS codes into the LDS heap image
-        // writes are clamped to this string's [my_rel, my_rel + my_len) so corrupt lengths
-        // can never touch another string's bytes or leave the LDS image
+        // (d) writes are clamped to this string's [my_rel, my_rel + my_len), so corrupt
+        // lengths can never touch another string's bytes or leave the LDS image
         int64_t o = my_rel;
         const int64_t o_end = my_rel + my_len;
         for (int64_t k = my_c0 - c0; k < my_c1 - c0; k++) {
@@ -159,44 +186,27 @@ __global__ __launch_bounds__(kTile) void fsst_decode(const uint64_t* __restrict_
             }
         }
         __syncthreads();
-        // coalesced copy-out of [tile_out0, tile_out0 + tile_total)
+        // (e) coalesced copy-out of [tile_out0, tile_out0 + tile_total)
         uint8_t* dst = heap + tile_out0;
         const int64_t head = (16 - (reinterpret_cast<uintptr_t>(dst) & 15)) & 15;
         const int64_t h = head < tile_total ? head : tile_total;
         for (int64_t k = tid; k < h; k += kTile) dst[k] = s_heap[k];
         const int64_t body = (tile_total - h) / 16;
         for (int64_t k = tid; k < body; k += kTile) {
-            uint32_t w[4];
             const uint8_t* src = s_heap + h + 16 * k;
+            uint32_t w[4];
 #pragma unroll
             for (int q = 0; q < 4; q++)
                 w[q] = uint32_t(src[4 * q]) | (uint32_t(src[4 * q + 1]) << 8) |
                        (uint32_t(src[4 * q + 2]) << 16) | (uint32_t(src[4 * q + 3]) << 24);
-            // plain stores: these 16-B chunks do not cover whole 128-B lines per instruction,
-            // and non-temporal stores made this kernel 10x slower (660 vs 66 us on C4, r01)
             reinterpret_cast<uint4*>(dst + h)[k] = make_uint4(w[0], w[1], w[2], w[3]);
         }
         for (int64_t k = h + body * 16 + tid; k < tile_total; k += kTile) dst[k] = s_heap[k];
-        // views from the LDS image
+        // (f) views from the LDS image (reads past the string stay inside s_heap's slack)
         if (live) {
-            uint8_t b[16];
-#pragma unroll
-            for (int k = 0; k < 16; k++) b[k] = 0;
-            if (valid) {
-                const uint32_t len = uint32_t(my_len);
-                __builtin_memcpy(b, &len, 4);
-                if (len <= 12) {
-                    for (uint32_t k = 0; k < len; k++) b[4 + k] = s_heap[my_rel + k];
-                } else {
-#pragma unroll
-                    for (int k = 0; k < 4; k++) b[4 + k] = s_heap[my_rel + k];
-                    const uint32_t off = uint32_t(tile_out0 + my_rel);
-                    __builtin_memcpy(b + 12, &off, 4);
-                }
-            }
-            uint4 q;
-            __builtin_memcpy(&q, b, 16);
-            views[i] = q;
+            const uint8_t* sp = s_heap + my_rel;
+            views[i] = valid ? build_view(vlen, uint32_t(tile_out0 + my_rel), [&](int j) { return sp[j]; })
+                             : make_uint4(0, 0, 0, 0);
         }
     } else {
         // direct path: decode straight into HBM
@@ -217,29 +227,18 @@ __global__ __launch_bounds__(kTile) void fsst_decode(const uint64_t* __restrict_
             }
         }
         if (live) {
-            uint8_t b[16];
-#pragma unroll
-            for (int k = 0; k < 16; k++) b[k] = 0;
-            if (valid) {
-                const uint32_t len = uint32_t(my_len);
-                __builtin_memcpy(b, &len, 4);
-                if (len <= 12) {
-                    for (uint32_t k = 0; k < len; k++) b[4 + k] = heap[o_start + k];
-                } else {
-#pragma unroll
-                    for (int k = 0; k < 4; k++) b[4 + k] = heap[o_start + k];
-                    const uint32_t off = uint32_t(o_start);
-                    __builtin_memcpy(b + 12, &off, 4);
-                }
-            }
-            uint4 q;
-            __builtin_memcpy(&q, b, 16);
-            views[i] = q;
+            const uint8_t* hp = heap + o_start;
+            views[i] = valid ? build_view(vlen, uint32_t(o_start),
+                                          [&](int j) { return uint32_t(j) < vlen ? hp[j] : uint8_t(0); })
+                             : make_uint4(0, 0, 0, 0);
         }
     }
 }
 
-uint64_t fsst_scratch_bytes(uint64_t n) { return ((n + kTile - 1) / kTile + 1) * sizeof(int64_t); }
+uint64_t fsst_scratch_bytes(uint64_t n) {
+    const uint64_t n_tiles = (n + kTile - 1) / kTile;
+    return (n_tiles + (n_tiles + kScanBlock - 1) / kScanBlock + 2) * sizeof(int64_t);
+}
 
 vxg_status launch_fsst(const uint64_t* symbols, const uint8_t* sym_lens, unsigned n_symbols,
                        const uint8_t* code_bytes, int offs_width, const void* code_offsets,
@@ -249,13 +248,15 @@ vxg_status launch_fsst(const uint64_t* symbols, const uint8_t* sym_lens, unsigne
     if (n == 0) return VXG_OK;
     if (n_symbols > 255) return set_error(VXG_ERR_INVALID_ARGUMENT, "FSST symbol table > 255 entries");
     const uint64_t n_tiles = (n + kTile - 1) / kTile;
+    const uint64_t n_blocks = (n_tiles + kScanBlock - 1) / kScanBlock;
     int64_t* tiles = static_cast<int64_t*>(scratch);
+    int64_t* blocks = tiles + n_tiles;
     hipLaunchKernelGGL(fsst_tile_sums, dim3(unsigned(n_tiles)), dim3(kTile), 0, s, lens, lens_width,
                        int(lens_signed), n, tiles);
-    hipLaunchKernelGGL(fsst_scan_tiles, dim3(1), dim3(kScanThreads), 0, s, tiles, n_tiles);
+    hipLaunchKernelGGL(fsst_scan_blocks, dim3(unsigned(n_blocks)), dim3(kScanBlock), 0, s, tiles, n_tiles, blocks);
     hipLaunchKernelGGL(fsst_decode, dim3(unsigned(n_tiles)), dim3(kTile), 0, s, symbols, sym_lens,
                        n_symbols, code_bytes, code_offsets, offs_width, lens, lens_width,
-                       int(lens_signed), n, validity, tiles, heap, reinterpret_cast<uint4*>(views));
+                       int(lens_signed), n, validity, tiles, blocks, heap, reinterpret_cast<uint4*>(views));
     return hip_check(hipGetLastError(), "fsst kernels");
 }
 

@@ -568,22 +568,25 @@ vxg_status launch_fill(int value_width, const uint8_t* scalar16, uint64_t n, voi
 // ------------------------------------------------------------------ VarBin -> views
 // arrow-array 53.2 make_view: len<=12 inline (zero padded), else {len, prefix, 0, offset};
 // null rows -> all-zero view (GenericByteViewBuilder::append_null).
+// Byte positions are compile-time (unrolled j) so nothing is a runtime-indexed register array
+// (which hipcc places in scratch); reads are guarded by j < len.
 __device__ __forceinline__ uint4 make_view(const uint8_t* __restrict__ heap, uint64_t start, uint32_t len) {
-    uint8_t b[16];
-#pragma unroll
-    for (int k = 0; k < 16; k++) b[k] = 0;
-    __builtin_memcpy(b, &len, 4);
+    const uint8_t* p = heap + start;
+    uint32_t w1 = 0, w2 = 0, w3 = 0;
     if (len <= 12) {
-        for (uint32_t k = 0; k < len; k++) b[4 + k] = heap[start + k];
+#pragma unroll
+        for (int j = 0; j < 12; j++) {
+            const uint32_t b = uint32_t(j) < len ? uint32_t(p[j]) : 0u;
+            if (j < 4) w1 |= b << (8 * j);
+            else if (j < 8) w2 |= b << (8 * (j - 4));
+            else w3 |= b << (8 * (j - 8));
+        }
     } else {
 #pragma unroll
-        for (int k = 0; k < 4; k++) b[4 + k] = heap[start + k];
-        const uint32_t off = uint32_t(start);
-        __builtin_memcpy(b + 12, &off, 4);
+        for (int j = 0; j < 4; j++) w1 |= uint32_t(p[j]) << (8 * j);
+        w3 = uint32_t(start);
     }
-    uint4 q;
-    __builtin_memcpy(&q, b, 16);
-    return q;
+    return make_uint4(len, w1, w2, w3);
 }
 
 __global__ __launch_bounds__(kBlock) void varbin_views_kernel(const uint8_t* __restrict__ heap, const void* offs,

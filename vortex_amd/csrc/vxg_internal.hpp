@@ -56,22 +56,10 @@ extern const double kIF10d[24];
 // Device error word bits (set by kernels, read by vxg_check via vxg_stream_sync).
 enum : uint32_t { kErrTakeOOB = 1u, kErrPatchOOB = 2u, kErrRunEnd = 4u };
 
-// Pinned host staging ring for small per-launch tables (chunk descriptors): the host copy is
-// reused only after the event recorded behind its async H2D copy has completed, so uploads
-// never synchronise the stream.
-constexpr int kStageSlots = 8;
-constexpr size_t kStageBytes = 1 << 20;
-
 struct Ctx {
     int device = 0;
     uint32_t* err_word = nullptr;  // device
-    void* stage[kStageSlots] = {};
-    hipEvent_t stage_ev[kStageSlots] = {};
-    unsigned stage_next = 0;
 };
-
-// Copy `bytes` of host memory to device `dst` on stream `s` without synchronising.
-vxg_status stage_upload(Ctx& c, const void* src, size_t bytes, void* dst, hipStream_t s);
 
 vxg_status set_error(vxg_status s, const std::string& msg);
 vxg_status hip_check(hipError_t e, const char* what);
@@ -107,9 +95,14 @@ struct DictChunkDev {
     uint64_t dict_len;
     uint64_t first_group;  // first 32-block workgroup index of this chunk
 };
-vxg_status launch_fl_unpack_dict_chunks(int T, int W, int value_width, const DictChunkDev* d_chunks,
-                                        uint32_t n_chunks, uint64_t total_groups, uint32_t* err,
-                                        hipStream_t s);
+// Up to kArgChunks chunk descriptors travel as a kernel argument (1.8 KB kernarg).
+constexpr int kArgChunks = 32;
+struct DictChunkTable {
+    DictChunkDev c[kArgChunks];
+    uint32_t n;
+};
+vxg_status launch_fl_unpack_dict_chunks(int T, int W, int value_width, const DictChunkTable& tab,
+                                        uint64_t total_groups, uint32_t* err, hipStream_t s);
 
 // Patch scatter with the same epilogue applied to the patch value.
 vxg_status launch_patch(int val_width, int idx_width, bool idx_signed, Epi epi, int T,
@@ -140,7 +133,7 @@ vxg_status fl_plain_64(int W, Epi epi, const UnpackArgs& a, hipStream_t s);
 vxg_status fl_alp(int T, int W, Epi epi, const UnpackArgs& a, hipStream_t s);
 #define VXG_DECL_DICT(VW)                                                                          \
     vxg_status fl_dict_##VW(int T, int W, const UnpackArgs& a, hipStream_t s);                     \
-    vxg_status fl_dict_chunks_##VW(int T, int W, const DictChunkDev* d, uint32_t n, uint64_t g,    \
+    vxg_status fl_dict_chunks_##VW(int T, int W, const DictChunkTable& d, uint64_t g,              \
                                    uint32_t* err, hipStream_t s);
 VXG_DECL_DICT(1)
 VXG_DECL_DICT(2)
