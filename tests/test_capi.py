@@ -1,0 +1,82 @@
+"""CPU: the C-ABI libraries load and export exactly what include/*.h declares (no GPU calls)."""
+import ctypes as C
+import re
+import subprocess
+from pathlib import Path
+
+import pytest
+
+import vortex_amd._lib as L
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def declared(header: str, prefix: str) -> set:
+    text = (ROOT / "include" / header).read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return set(re.findall(rf"\b({prefix}_[a-z0-9_]+)\s*\(", text))
+
+
+def exported(lib: Path, prefix: str) -> set:
+    out = subprocess.run(["nm", "-D", "--defined-only", str(lib)], capture_output=True, text=True,
+                         check=True).stdout
+    return {ln.split()[-1] for ln in out.splitlines() if ln.split() and ln.split()[-1].startswith(prefix + "_")}
+
+
+def test_gpu_lib_exports_match_header():
+    decl = declared("vortex_gpu.h", "vxg")
+    assert decl == set(L.GPU_SIGNATURES), "ctypes signatures out of sync with vortex_gpu.h"
+    assert exported(L.GPU_LIB_PATH, "vxg") == decl
+    lib = L.gpu_lib()  # loads (HIP runtime present in the image; no device needed)
+    for name in decl:
+        assert hasattr(lib, name)
+    assert lib.vxg_abi_version() == 1
+
+
+def test_enc_lib_exports_match_header():
+    decl = declared("vortex_enc.h", "vxe")
+    assert decl == set(L.ENC_SIGNATURES)
+    assert exported(L.ENC_LIB_PATH, "vxe") == decl
+    L.enc_lib()
+
+
+def test_struct_layouts_match_c(tmp_path):
+    """ctypes mirrors must have the C compiler's sizes AND field offsets for the header."""
+    fields = {"vxg_array": (L.VxgArray, ["encoding", "len", "meta", "n_buffers", "n_children", "buffers",
+                                         "children"]),
+              "vxg_canonical": (L.VxgCanonical, ["kind", "len", "values", "views", "data", "data_bytes",
+                                                 "validity"]),
+              "vxg_dict_chunk": (L.VxgDictChunk, ["packed", "out", "n_blocks", "dict_len"])}
+    src = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{ROOT}/include/vortex_gpu.h"', "int main(){",
+           'printf("vxg_meta %zu\\n", sizeof(vxg_meta));']
+    for st, (_, fs) in fields.items():
+        src.append(f'printf("{st} %zu\\n", sizeof({st}));')
+        for f in fs:
+            src.append(f'printf("{st}.{f} %zu\\n", offsetof({st}, {f}));')
+    src.append("return 0;}")
+    (tmp_path / "sz.c").write_text("\n".join(src))
+    subprocess.run(["gcc", str(tmp_path / "sz.c"), "-o", str(tmp_path / "sz")], check=True)
+    got = dict(ln.split() for ln in subprocess.run([str(tmp_path / "sz")], capture_output=True, text=True,
+                                                    check=True).stdout.splitlines())
+    assert int(got["vxg_meta"]) == C.sizeof(L.VxgMeta)
+    for st, (cls, fs) in fields.items():
+        assert int(got[st]) == C.sizeof(cls), st
+        for f in fs:
+            assert int(got[f"{st}.{f}"]) == getattr(cls, f).offset, (st, f)
+
+
+def test_encoding_ids_match_reference():
+    # vortex-array/src/encoding/mod.rs:106-147
+    ref = dict(BOOL=2, PRIMITIVE=3, STRUCT=4, VARBIN=5, VARBINVIEW=6, SPARSE=8, CONSTANT=9, CHUNKED=10,
+               ALP=17, DICT=20, FL_BITPACKED=21, FL_DELTA=22, FL_FOR=23, FSST=24, RUN_END=27, ZIGZAG=29, ALP_RD=30)
+    assert L.ENC == ref
+    hdr = (ROOT / "include" / "vortex_gpu.h").read_text()
+    for k, v in ref.items():
+        assert re.search(rf"VXG_ENC_{k} = {v}\b", hdr), k
+
+
+def test_missing_library_fails_loudly(tmp_path, monkeypatch):
+    monkeypatch.setattr(L, "_gpu", None)
+    monkeypatch.setattr(L, "GPU_LIB_PATH", tmp_path / "absent.so")
+    with pytest.raises(ImportError, match="no CPU fallback"):
+        L.gpu_lib()
