@@ -299,6 +299,73 @@ def test_fsst(ctx, n):
     assert_string_parity(E.encode_fsst(strings), ctx, strings)
 
 
+def _fsst_handmade(strings, symbols):
+    """FSST array from a fixed symbol table and a greedy longest-match coder that escapes every
+    other byte (code 255 + literal) — the trainer would learn 0xFF runs as symbols instead."""
+    syms = [s for s in symbols]
+    codes, coffs, lens = bytearray(), [0], []
+    for s in strings:
+        s = s or b""
+        k = 0
+        while k < len(s):
+            best = max((j for j, y in enumerate(syms) if s.startswith(y, k)), key=lambda j: len(syms[j]),
+                       default=None)
+            if best is None:
+                codes += bytes([255, s[k]])
+                k += 1
+            else:
+                codes.append(best)
+                k += len(syms[best])
+        coffs.append(len(codes))
+        lens.append(len(s))
+    valid = np.array([s is not None for s in strings])
+    sym_u64 = np.array([int.from_bytes(y.ljust(8, b"\0"), "little") for y in syms], np.uint64)
+    code_vb = A.varbin(A.primitive(np.array(coffs, np.int32)), A.primitive(np.frombuffer(bytes(codes), np.uint8)),
+                       utf8=False, validity=None if valid.all() else valid)
+    return A.fsst(A.primitive(sym_u64), A.primitive(np.array([len(y) for y in syms], np.uint8)), code_vb,
+                  A.primitive(np.array(lens, np.int32)))
+
+
+def test_fsst_escape_runs(ctx):
+    # runs of 0xFF bytes escape as 255 255 pairs: code segments start inside such runs, and an
+    # escape can be the last byte of a 16-byte segment (its literal in the next segment)
+    rng = np.random.default_rng(7)
+    strings = []
+    for i in range(3000):  # ~2.6 KB of codes per 256-string tile: the staged (LDS) path
+        k = int(rng.integers(0, 14))
+        s = bytes(rng.choice([0xFF, 0xFE, 0x41, 0x20], size=k, p=[0.7, 0.1, 0.1, 0.1]).astype(np.uint8))
+        strings.append(None if i % 97 == 3 else s)
+    strings[10] = b"\xff" * 200
+    arr = _fsst_handmade(strings, [b"A ", b"\xfe\xfe\xfe", b"AAAAAAAA", b" "])
+    codes = arr.children[2].children[1].buffers[0]
+    assert (codes == 255).mean() > 0.5
+    assert_string_parity(arr, ctx, strings)
+
+
+@pytest.mark.parametrize("compress_children", [False, True])
+def test_fsst_many_scan_blocks(ctx, compress_children):
+    # > 1024 tiles of 256 strings: the decode adds the totals of preceding scan blocks
+    rng = np.random.default_rng(11)
+    n = 300_000
+    lens = rng.integers(0, 30, n)
+    offs = np.zeros(n + 1, np.int64)
+    np.cumsum(lens, out=offs[1:])
+    heap = rng.choice(np.frombuffer(b"abcdefgh ijkl", np.uint8), size=int(offs[-1]))
+    arr = E.encode_fsst_from_heap(heap, offs, compress_children=compress_children)
+    assert_string_parity(arr, ctx)
+
+
+def test_fsst_inconsistent_lengths_is_an_error(ctx):
+    strings = [b"carefully final deposits"] * 600
+    arr = E.encode_fsst(strings, compress_children=False)
+    lens = arr.children[3].buffers[0].copy()
+    lens[5] += 3  # codes no longer decode to uncompressed_lengths
+    bad = A.fsst(arr.children[0], arr.children[1], arr.children[2], A.primitive(lens))
+    with pytest.raises(V.VortexGpuError) as ei:
+        gpu(bad, ctx)
+    assert ei.value.kind == "InvalidArgument"
+
+
 def test_fsst_long_strings_direct_path(ctx):
     # strings large enough that a 256-string tile overflows the LDS images
     rng = np.random.default_rng(1)

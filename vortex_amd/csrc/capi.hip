@@ -655,7 +655,7 @@ vxg_status Planner::string_canonical(const vxg_array& a, vxg_canonical& out) {
                            unsigned(sym->len), static_cast<const uint8_t*>(pcb), width(*child(*codes, 0)), pco,
                            width(*ulen), ptype_is_signed(ulen->ptype), pul, a.len,
                            static_cast<const uint8_t*>(out.validity), scratch, static_cast<uint8_t*>(out.data),
-                           static_cast<uint8_t*>(out.views), s_);
+                           static_cast<uint8_t*>(out.views), ctx_->c.err_word, s_);
     }
     if (a.encoding == VXG_ENC_DICT) {
         // Dict over string values: take on the 16-B views, buffers kept (varbinview/compute.rs:68-76)
@@ -754,6 +754,15 @@ vxg_status vxg_open(int device, vxg_ctx** out) {
     c->c.device = device;
     hipError_t e = hipMalloc(&c->c.err_word, 16);
     if (e == hipSuccess) e = hipMemset(c->c.err_word, 0, 16);
+    if (e == hipSuccess) {
+        // Planner temporaries come from the device's stream-ordered pool; keep freed blocks
+        // cached instead of returning them to the driver at every synchronisation (the default
+        // threshold 0 made each canonicalize re-map its temporaries: ~25 us of host time).
+        hipMemPool_t pool;
+        uint64_t keep = ~0ull;
+        if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess)
+            (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+    }
     if (e != hipSuccess) {
         vxg_close(c);
         return hip_check(e, "context setup");
@@ -801,6 +810,8 @@ vxg_status vxg_stream_sync(vxg_ctx* ctx, void* stream) {
         if (err & kErrTakeOOB) return set_error(VXG_ERR_OUT_OF_BOUNDS, "take: index out of bounds");
         if (err & kErrPatchOOB) return set_error(VXG_ERR_OUT_OF_BOUNDS, "patch index out of bounds");
         if (err & kErrRunEnd) return set_error(VXG_ERR_INVALID_ARGUMENT, "RunEnd ends do not cover the array");
+        if (err & kErrFsst)
+            return set_error(VXG_ERR_INVALID_ARGUMENT, "FSST codes do not decode to uncompressed_lengths");
     }
     return VXG_OK;
 }
@@ -980,7 +991,7 @@ vxg_status vxg_fsst_decode(vxg_ctx* ctx, const uint64_t* symbols, const uint8_t*
         return set_error(VXG_ERR_MISMATCHED_TYPES, "FSST offsets/lengths must be integers");
     return launch_fsst(symbols, sym_lens, n_symbols, code_bytes, ptype_width(offs_ptype), code_offsets,
                        ptype_width(lens_ptype), ptype_is_signed(lens_ptype), lens, n, validity, scratch, heap, views,
-                       S(stream));
+                       ctx->c.err_word, S(stream));
 }
 
 vxg_status vxg_fill(vxg_ctx* ctx, unsigned value_width, const void* scalar_host, uint64_t n, void* out,

@@ -54,7 +54,7 @@ extern const double kF10d[24];
 extern const double kIF10d[24];
 
 // Device error word bits (set by kernels, read by vxg_check via vxg_stream_sync).
-enum : uint32_t { kErrTakeOOB = 1u, kErrPatchOOB = 2u, kErrRunEnd = 4u };
+enum : uint32_t { kErrTakeOOB = 1u, kErrPatchOOB = 2u, kErrRunEnd = 4u, kErrFsst = 8u };
 
 struct Ctx {
     int device = 0;
@@ -154,7 +154,7 @@ vxg_status launch_fsst(const uint64_t* symbols, const uint8_t* sym_lens, unsigne
                        const uint8_t* code_bytes, int offs_width, const void* code_offsets,
                        int lens_width, bool lens_signed, const void* lens, uint64_t n,
                        const uint8_t* validity, void* scratch, uint8_t* heap, uint8_t* views,
-                       hipStream_t s);
+                       uint32_t* err, hipStream_t s);
 vxg_status launch_varbin_views(const uint8_t* heap, int offs_width, const void* offsets, uint64_t n,
                                const uint8_t* validity, uint8_t* views, hipStream_t s);
 
