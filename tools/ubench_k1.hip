@@ -60,9 +60,10 @@ __global__ __launch_bounds__(256) void k_two(const uint8_t* __restrict__ packed,
 #pragma unroll
     for (int w = 0; w < W; w++) p1[w] = load16<T>(packed + (blk0 + 1) * (128 * W) + 128 * w + 16 * t);
     EpiParams ep{};
-    process_rows<T, W, Epi::Plain, 0, NT>(p0, t * 4, out, int64_t(blk0 * 1024), true, n_blocks * 1024, ep,
+    bool oob = false;
+    process_rows<T, W, Epi::Plain, 0, NT, true>(p0, t * 4, out, int64_t(blk0 * 1024), n_blocks * 1024, ep, oob,
                                           std::make_integer_sequence<int, T>{});
-    process_rows<T, W, Epi::Plain, 0, NT>(p1, t * 4, out, int64_t((blk0 + 1) * 1024), true, n_blocks * 1024, ep,
+    process_rows<T, W, Epi::Plain, 0, NT, true>(p1, t * 4, out, int64_t((blk0 + 1) * 1024), n_blocks * 1024, ep, oob,
                                           std::make_integer_sequence<int, T>{});
 }
 

@@ -196,6 +196,7 @@ class Planner {
     vxg_status decode_into(const vxg_array& a, void* dst);
     // Canonical primitive values of `a` as a device pointer (aliases PRIMITIVE buffers).
     vxg_status view_primitive(const vxg_array& a, const void** p);
+    vxg_status int_column(const vxg_array& a, IntCol& c);
 
     vxg_status decode_bitpacked(const vxg_array& bp, Epi epi, int vw, UnpackArgs a, void* dst);
     vxg_status apply_sparse_patches(const vxg_array& sparse, int T, Epi epi, int vw, const UnpackArgs& a,
@@ -227,6 +228,42 @@ vxg_status Planner::view_primitive(const vxg_array& a, const void** p) {
     return VXG_OK;
 }
 
+vxg_status Planner::int_column(const vxg_array& a, IntCol& c) {
+    // An integer child read in place by a consumer kernel: a patch-free 32/64-bit
+    // [FoR](BitPacked) column stays packed (elements unpacked where used); anything else is
+    // canonicalized to a primitive buffer first.
+    if (!ptype_is_int(a.ptype)) return set_error(VXG_ERR_MISMATCHED_TYPES, "expected an integer array");
+    c = IntCol{};
+    c.width = width(a);
+    c.sgn = ptype_is_signed(a.ptype);
+    const vxg_array* bp = nullptr;
+    if (a.encoding == VXG_ENC_FL_FOR && child(a, 0) && child(a, 0)->encoding == VXG_ENC_FL_BITPACKED) {
+        bp = child(a, 0);
+        c.reference = a.meta.for_.reference;
+        c.shift = a.meta.for_.shift;
+    } else if (a.encoding == VXG_ENC_FL_BITPACKED) {
+        bp = &a;
+    }
+    if (bp && !bp->meta.bitpacked.has_patches && width(*bp) == c.width && (c.width == 4 || c.width == 8) &&
+        bp->len == a.len) {
+        const vxg_buffer* packed = buf(*bp, 0);
+        const unsigned W = bp->meta.bitpacked.bit_width, off = bp->meta.bitpacked.offset;
+        const uint64_t nblk = (bp->len + off + 1023) / 1024;
+        if (off > 1023) return set_error(VXG_ERR_INVALID_ARGUMENT, "Offset must be less than full block, i.e. 1024");
+        if (W > unsigned(8 * c.width)) return set_error(VXG_ERR_INVALID_ARGUMENT, "Unsupported bit width");
+        const uint64_t have = packed ? packed->len : 0;
+        if (W > 0 && have != nblk * 128ull * W)  // bitpacking/mod.rs:80-88
+            return set_error(VXG_ERR_INVALID_ARGUMENT, "Expected " + std::to_string(nblk * 128ull * W) +
+                                                           " packed bytes, got " + std::to_string(have));
+        c.packed = true;
+        c.p = packed ? packed->ptr : nullptr;
+        c.W = W;
+        c.offset = off;
+        return VXG_OK;
+    }
+    return view_primitive(a, &c.p);
+}
+
 vxg_status Planner::apply_sparse_patches(const vxg_array& sp, int T, Epi epi, int vw, const UnpackArgs& a,
                                          void* dst, uint64_t out_len) {
     // bitpacking/compress.rs:191-207 / alp/compress.rs:80-96: only SparseArray patches.
@@ -236,11 +273,11 @@ vxg_status Planner::apply_sparse_patches(const vxg_array& sp, int T, Epi epi, in
     const vxg_array* val = child(sp, 1);
     if (!idx || !val) return set_error(VXG_ERR_INVALID_ARGUMENT, "Sparse patches need indices and values");
     if (idx->len != val->len) return set_error(VXG_ERR_INVALID_ARGUMENT, "Sparse indices/values length mismatch");
-    const void *pi, *pv;
-    VXG_TRY(view_primitive(*idx, &pi));
+    const void* pv;
+    IntCol ic;  // a packed index column is unpacked by the scatter itself (no temporary)
+    VXG_TRY(int_column(*idx, ic));
     VXG_TRY(view_primitive(*val, &pv));
-    return launch_patch(vw, width(*idx), ptype_is_signed(idx->ptype), epi, T, dst, out_len, pi,
-                        sp.meta.sparse.indices_offset, pv, idx->len, a, s_);
+    return launch_patch(vw, ic, epi, T, dst, out_len, sp.meta.sparse.indices_offset, pv, idx->len, a, s_);
 }
 
 vxg_status Planner::decode_bitpacked(const vxg_array& bp, Epi epi, int vw, UnpackArgs a, void* dst) {
@@ -643,17 +680,17 @@ vxg_status Planner::string_canonical(const vxg_array& a, vxg_canonical& out) {
         const vxg_array* ulen = child(a, 3);
         if (!sym || !slen || !codes || !ulen || codes->encoding != VXG_ENC_VARBIN)
             return set_error(VXG_ERR_INVALID_ARGUMENT, "FSSTArray needs symbols, lengths, VarBin codes, lengths");
-        const void *psym, *pslen, *pco, *pcb, *pul;
+        const void *psym, *pslen, *pcb;
         VXG_TRY(view_primitive(*sym, &psym));
         VXG_TRY(view_primitive(*slen, &pslen));
-        VXG_TRY(view_primitive(*child(*codes, 0), &pco));
         VXG_TRY(view_primitive(*child(*codes, 1), &pcb));
-        VXG_TRY(view_primitive(*ulen, &pul));
+        IntCol offs, lens;  // read in place by the FSST kernels (packed columns stay packed)
+        VXG_TRY(int_column(*child(*codes, 0), offs));
+        VXG_TRY(int_column(*ulen, lens));
         void* scratch;
         VXG_TRY(temp(fsst_scratch_bytes(a.len), &scratch));
         return launch_fsst(static_cast<const uint64_t*>(psym), static_cast<const uint8_t*>(pslen),
-                           unsigned(sym->len), static_cast<const uint8_t*>(pcb), width(*child(*codes, 0)), pco,
-                           width(*ulen), ptype_is_signed(ulen->ptype), pul, a.len,
+                           unsigned(sym->len), static_cast<const uint8_t*>(pcb), offs, lens, a.len,
                            static_cast<const uint8_t*>(out.validity), scratch, static_cast<uint8_t*>(out.data),
                            static_cast<uint8_t*>(out.views), ctx_->c.err_word, s_);
     }
@@ -914,8 +951,11 @@ vxg_status vxg_patch(vxg_ctx* ctx, int ptype, void* out, uint64_t out_len, int i
     if (!w || !ptype_is_int(indices_ptype)) return set_error(VXG_ERR_INVALID_ARGUMENT, "bad ptype");
     UnpackArgs a{};
     a.err = ctx->c.err_word;
-    return launch_patch(0, ptype_width(indices_ptype), ptype_is_signed(indices_ptype), Epi::Plain, 8 * w, out,
-                        out_len, indices, indices_offset, values, n_patches, a, S(stream));
+    IntCol ic{};
+    ic.p = indices;
+    ic.width = ptype_width(indices_ptype);
+    ic.sgn = ptype_is_signed(indices_ptype);
+    return launch_patch(0, ic, Epi::Plain, 8 * w, out, out_len, indices_offset, values, n_patches, a, S(stream));
 }
 
 vxg_status vxg_for_decode(vxg_ctx* ctx, int ptype, const void* in, uint64_t n, uint64_t reference,
@@ -989,8 +1029,14 @@ vxg_status vxg_fsst_decode(vxg_ctx* ctx, const uint64_t* symbols, const uint8_t*
     VXG_TRY(use_device(ctx));
     if (!ptype_is_int(offs_ptype) || !ptype_is_int(lens_ptype))
         return set_error(VXG_ERR_MISMATCHED_TYPES, "FSST offsets/lengths must be integers");
-    return launch_fsst(symbols, sym_lens, n_symbols, code_bytes, ptype_width(offs_ptype), code_offsets,
-                       ptype_width(lens_ptype), ptype_is_signed(lens_ptype), lens, n, validity, scratch, heap, views,
+    IntCol offs{}, ls{};
+    offs.p = code_offsets;
+    offs.width = ptype_width(offs_ptype);
+    offs.sgn = ptype_is_signed(offs_ptype);
+    ls.p = lens;
+    ls.width = ptype_width(lens_ptype);
+    ls.sgn = ptype_is_signed(lens_ptype);
+    return launch_fsst(symbols, sym_lens, n_symbols, code_bytes, offs, ls, n, validity, scratch, heap, views,
                        ctx->c.err_word, S(stream));
 }
 

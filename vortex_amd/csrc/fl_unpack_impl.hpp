@@ -134,10 +134,11 @@ template <int T, int VW> struct EpiOut<T, Epi::AlpF32, VW> { using type = float;
 template <int T, int VW> struct EpiOut<T, Epi::AlpF64, VW> { using type = double; };
 template <int T, int VW> struct EpiOut<T, Epi::Dict, VW> { using type = typename VType<VW>::t; };
 
-// Apply the epilogue to one element.
+// Apply the epilogue to one element.  Dict: an out-of-range code reads entry 0 and sets `oob`
+// (reported once per thread, not one branch + atomic per element).
 template <int T, Epi EPI, int VW>
 __device__ __forceinline__ typename EpiOut<T, EPI, VW>::type apply_epi(typename Fl<T>::E e,
-                                                                      const EpiParams& ep) {
+                                                                      const EpiParams& ep, bool& oob) {
     using E = typename Fl<T>::E;
     if constexpr (EPI == Epi::Plain) {
         return e;
@@ -159,13 +160,20 @@ __device__ __forceinline__ typename EpiOut<T, EPI, VW>::type apply_epi(typename 
         return __dmul_rn(x, ep.alp_b);
     } else {  // Dict gather
         using VT = typename VType<VW>::t;
-        uint64_t c = uint64_t(e);
-        if (c >= ep.dict_len) {
-            __hip_atomic_fetch_or(ep.err, kErrTakeOOB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            c = 0;
-        }
-        return static_cast<const VT*>(ep.dict)[c];
+        const uint64_t c = uint64_t(e);
+        const bool bad = c >= ep.dict_len;
+        oob |= bad;
+        return static_cast<const VT*>(ep.dict)[bad ? 0 : c];
     }
+}
+
+template <int T, Epi EPI, int VW>
+__device__ __forceinline__ typename EpiOut<T, EPI, VW>::type apply_epi(typename Fl<T>::E e,
+                                                                      const EpiParams& ep) {
+    bool oob = false;
+    const auto r = apply_epi<T, EPI, VW>(e, ep, oob);
+    if (oob) __hip_atomic_fetch_or(ep.err, kErrTakeOOB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return r;
 }
 
 // Output store policy of the K1 launches (1 = non-temporal streaming stores).
@@ -200,42 +208,42 @@ __device__ __forceinline__ void store_bytes(uint8_t* dst, const void* src) {
     }
 }
 
-// One output row R of this thread's 16-byte lane slice.
-template <int T, int W, Epi EPI, int VW, int NT, int R>
+// One output row R of this thread's 16-byte lane slice.  FULL (compile time): the block lands
+// entirely inside [0, len) with 16-byte alignment -> one unconditional 16-byte store.
+template <int T, int W, Epi EPI, int VW, int NT, int R, bool FULL>
 __device__ __forceinline__ void process_row(const Vec16<T>* p, int lane0,
                                             typename EpiOut<T, EPI, VW>::type* __restrict__ out,
-                                            int64_t out_base, bool full, uint64_t len,
-                                            const EpiParams& ep) {
+                                            int64_t out_base, uint64_t len, const EpiParams& ep, bool& oob) {
     using E = typename Fl<T>::E;
     using O = typename EpiOut<T, EPI, VW>::type;
     constexpr int EPV = 16 / int(sizeof(E));  // elements per 16-byte lane slice
     const Vec16<T> v = extract_row<T, W, R>(p);
     const int idx = fl_index(R, lane0);
-    if (full) {
+    if constexpr (FULL) {
         O* dst = out + (out_base + idx);
         if constexpr (EPI == Epi::Plain) {
             store_bytes<16, NT>(reinterpret_cast<uint8_t*>(dst), v.w);
         } else {
             O o[EPV];
 #pragma unroll
-            for (int j = 0; j < EPV; j++) o[j] = apply_epi<T, EPI, VW>(v.elem(j), ep);
+            for (int j = 0; j < EPV; j++) o[j] = apply_epi<T, EPI, VW>(v.elem(j), ep, oob);
             store_bytes<EPV * int(sizeof(O)), NT>(reinterpret_cast<uint8_t*>(dst), o);
         }
     } else {
 #pragma unroll
         for (int j = 0; j < EPV; j++) {
             const int64_t o = out_base + idx + j;
-            if (o >= 0 && uint64_t(o) < len) out[o] = apply_epi<T, EPI, VW>(v.elem(j), ep);
+            if (o >= 0 && uint64_t(o) < len) out[o] = apply_epi<T, EPI, VW>(v.elem(j), ep, oob);
         }
     }
 }
 
-template <int T, int W, Epi EPI, int VW, int NT, int... Rs>
+template <int T, int W, Epi EPI, int VW, int NT, bool FULL, int... Rs>
 __device__ __forceinline__ void process_rows(const Vec16<T>* p, int lane0,
                                              typename EpiOut<T, EPI, VW>::type* __restrict__ out,
-                                             int64_t out_base, bool full, uint64_t len,
-                                             const EpiParams& ep, std::integer_sequence<int, Rs...>) {
-    (process_row<T, W, EPI, VW, NT, Rs>(p, lane0, out, out_base, full, len, ep), ...);
+                                             int64_t out_base, uint64_t len, const EpiParams& ep, bool& oob,
+                                             std::integer_sequence<int, Rs...>) {
+    (process_row<T, W, EPI, VW, NT, Rs, FULL>(p, lane0, out, out_base, len, ep, oob), ...);
 }
 
 // Decode one FastLanes block: this thread's 16-byte lane slice `t` of every word row.
@@ -254,11 +262,32 @@ __device__ __forceinline__ void unpack_block(const uint8_t* __restrict__ blk_pac
 #pragma unroll
         for (int w = 0; w < W; w++) p[w] = load16<T>(blk_packed + 128 * w + 16 * t);
     }
-    process_rows<T, W, EPI, VW, NT>(p, t * EPV, out, out_base, full, len, ep,
-                                std::make_integer_sequence<int, T>{});
+    bool oob = false;
+    if (full)  // unswitched: the full-block path is straight-line code
+        process_rows<T, W, EPI, VW, NT, true>(p, t * EPV, out, out_base, len, ep, oob,
+                                              std::make_integer_sequence<int, T>{});
+    else
+        process_rows<T, W, EPI, VW, NT, false>(p, t * EPV, out, out_base, len, ep, oob,
+                                               std::make_integer_sequence<int, T>{});
+    if constexpr (EPI == Epi::Dict)
+        if (oob) __hip_atomic_fetch_or(ep.err, kErrTakeOOB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int T, int W, Epi EPI, int VW>
+// Dictionaries up to this size are staged into LDS by every workgroup of a Dict launch: a
+// gather of 64 random 8-byte entries from global memory touches up to 64 cache lines (one
+// TA cycle each), from LDS it is one ds_read_b64 with bank conflicts.
+constexpr int kDictLdsBytes = 16 * 1024;
+
+template <int VW>
+__device__ __forceinline__ void stage_dict(uint8_t* s_dict, const void* dict, uint64_t dict_len) {
+    // 16-byte aligned chunks (the last may run past the dictionary inside its aligned chunk)
+    const int n16 = int((dict_len * VW + 15) / 16);
+    for (int q = threadIdx.x; q < n16; q += blockDim.x)
+        reinterpret_cast<uint4*>(s_dict)[q] = static_cast<const uint4*>(dict)[q];
+    __syncthreads();
+}
+
+template <int T, int W, Epi EPI, int VW, bool LDSD = false>
 __global__ __launch_bounds__(256) void fl_unpack_kernel(const uint8_t* __restrict__ packed,
                                                         void* __restrict__ out_v, uint64_t n_blocks,
                                                         uint32_t offset, uint64_t len,
@@ -267,6 +296,11 @@ __global__ __launch_bounds__(256) void fl_unpack_kernel(const uint8_t* __restric
     const uint64_t gid = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
     const uint64_t blk = gid >> 3;
     const int t = int(gid & 7);
+    if constexpr (LDSD) {
+        __shared__ __attribute__((aligned(16))) uint8_t s_dict[kDictLdsBytes];
+        stage_dict<VW>(s_dict, ep.dict, ep.dict_len);
+        ep.dict = s_dict;
+    }
     if (blk >= n_blocks) return;
     const int64_t out_base = int64_t(blk * 1024) - int64_t(offset);
     const bool full = offset == 0 && (blk + 1) * 1024 <= len;
@@ -279,7 +313,7 @@ __global__ __launch_bounds__(256) void fl_unpack_kernel(const uint8_t* __restric
 
 // Many independent chunks (e.g. Chunked[Dict(BitPacked)]) in one launch; each workgroup of
 // 256 threads covers 32 blocks of exactly one chunk.
-template <int T, int W, Epi EPI, int VW>
+template <int T, int W, Epi EPI, int VW, bool LDSD = false>
 __global__ __launch_bounds__(256) void fl_unpack_chunks_kernel(DictChunkTable tab, EpiParams ep0) {
     using O = typename EpiOut<T, EPI, VW>::type;
     // the chunk table is a kernel argument (no upload, no host sync); workgroup-uniform
@@ -293,10 +327,15 @@ __global__ __launch_bounds__(256) void fl_unpack_chunks_kernel(DictChunkTable ta
     const DictChunkDev c = tab.c[lo];
     const uint64_t blk = (g - c.first_group) * 32 + (threadIdx.x >> 3);
     const int t = int(threadIdx.x & 7);
-    if (blk >= c.n_blocks) return;
     EpiParams ep = ep0;
     ep.dict = c.dict;
     ep.dict_len = c.dict_len;
+    if constexpr (LDSD) {  // the whole workgroup is in chunk `lo`
+        __shared__ __attribute__((aligned(16))) uint8_t s_dict[kDictLdsBytes];
+        stage_dict<VW>(s_dict, c.dict, c.dict_len);
+        ep.dict = s_dict;
+    }
+    if (blk >= c.n_blocks) return;
     const bool full = (blk + 1) * 1024 <= c.len;
     unpack_block<T, W, EPI, VW, kOutNT>(c.packed + blk * (128 * W), t, static_cast<O*>(c.out),
                                         int64_t(blk * 1024), full, c.len, ep);
@@ -319,6 +358,13 @@ vxg_status launch_one(const UnpackArgs& a, hipStream_t s) {
     if (a.n_blocks == 0) return VXG_OK;
     const uint64_t threads = a.n_blocks * 8;
     const uint64_t grid = (threads + 255) / 256;
+    if constexpr (EPI == Epi::Dict) {
+        if (a.dict_len * VW <= uint64_t(kDictLdsBytes) && (reinterpret_cast<uintptr_t>(a.dict) & 15) == 0) {
+            hipLaunchKernelGGL((fl_unpack_kernel<T, W, EPI, VW, true>), dim3(unsigned(grid)), dim3(256), 0, s,
+                               a.packed, a.out, a.n_blocks, a.offset, a.len, to_epi(a));
+            return hip_check(hipGetLastError(), "fl_unpack_kernel launch");
+        }
+    }
     hipLaunchKernelGGL((fl_unpack_kernel<T, W, EPI, VW>), dim3(unsigned(grid)), dim3(256), 0, s,
                        a.packed, a.out, a.n_blocks, a.offset, a.len, to_epi(a));
     return hip_check(hipGetLastError(), "fl_unpack_kernel launch");
@@ -329,8 +375,16 @@ vxg_status launch_chunks_one(const DictChunkTable& tab, uint64_t total_groups, u
     if (total_groups == 0) return VXG_OK;
     EpiParams ep{};
     ep.err = err;
-    hipLaunchKernelGGL((fl_unpack_chunks_kernel<T, W, EPI, VW>), dim3(unsigned(total_groups)),
-                       dim3(256), 0, s, tab, ep);
+    bool lds = true;
+    for (uint32_t k = 0; k < tab.n; k++)
+        lds = lds && tab.c[k].dict_len * VW <= uint64_t(kDictLdsBytes) &&
+              (reinterpret_cast<uintptr_t>(tab.c[k].dict) & 15) == 0;
+    if (lds)
+        hipLaunchKernelGGL((fl_unpack_chunks_kernel<T, W, EPI, VW, true>), dim3(unsigned(total_groups)),
+                           dim3(256), 0, s, tab, ep);
+    else
+        hipLaunchKernelGGL((fl_unpack_chunks_kernel<T, W, EPI, VW>), dim3(unsigned(total_groups)),
+                           dim3(256), 0, s, tab, ep);
     return hip_check(hipGetLastError(), "fl_unpack_chunks_kernel launch");
 }
 

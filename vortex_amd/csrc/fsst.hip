@@ -24,7 +24,7 @@
 //   A tile whose codes do not decode to exactly the sum of its lengths raises an error (the
 //   reference would slice a shifted stream); tiles too large for the LDS images take a
 //   per-string direct-to-HBM path that checks every string.
-#include "vxg_internal.hpp"
+#include "intcol.hpp"
 
 namespace vxg {
 
@@ -38,16 +38,6 @@ constexpr int kCodeLds = 6 * 1024;    // staged code bytes per tile
 constexpr int kHeapLds = 10 * 1024;   // staged output bytes per tile
 constexpr int kScanBlock = 1024;      // tiles per scan_blocks workgroup
 constexpr int kSumTiles = 16;         // tiles per tile_sums workgroup
-
-// Integer load with compile-time width/signedness.  (A runtime width switch compiles to a
-// branch nest that waits vmcnt(0) after every load.)
-template <int WIDTH, bool SGN>
-__device__ __forceinline__ int64_t ld(const void* p, uint64_t i) {
-    if constexpr (WIDTH == 1) return SGN ? int64_t(static_cast<const int8_t*>(p)[i]) : int64_t(static_cast<const uint8_t*>(p)[i]);
-    else if constexpr (WIDTH == 2) return SGN ? int64_t(static_cast<const int16_t*>(p)[i]) : int64_t(static_cast<const uint16_t*>(p)[i]);
-    else if constexpr (WIDTH == 4) return SGN ? int64_t(static_cast<const int32_t*>(p)[i]) : int64_t(static_cast<const uint32_t*>(p)[i]);
-    else return static_cast<const int64_t*>(p)[i];
-}
 
 __device__ __forceinline__ int64_t wave_sum(int64_t x) {
 #pragma unroll
@@ -124,8 +114,8 @@ __device__ __forceinline__ uint32_t byte_of(const uint4& v, int j) {
 
 }  // namespace
 
-template <int LW, bool LSG>
-__global__ __launch_bounds__(kTile) void fsst_tile_sums(const void* lens, uint64_t n, uint64_t n_tiles,
+template <class LenAcc>
+__global__ __launch_bounds__(kTile) void fsst_tile_sums(LenAcc lens, uint64_t n, uint64_t n_tiles,
                                                         int64_t* __restrict__ tile_sums) {
     // 16 tiles per workgroup; in round r wave w sums tile 4r + w: each lane adds 4 consecutive
     // lengths (64 lanes x 4 = one 256-string tile), then ONE wave reduction per tile.
@@ -139,7 +129,7 @@ __global__ __launch_bounds__(kTile) void fsst_tile_sums(const void* lens, uint64
 #pragma unroll
         for (int e = 0; e < 4; e++) {
             const uint64_t i = base + e;
-            const int64_t x = ld<LW, LSG>(lens, i < n ? i : n - 1);
+            const int64_t x = lens(i < n ? i : n - 1);
             acc += i < n ? x : 0;
         }
         v[r] = acc;
@@ -163,11 +153,11 @@ __global__ __launch_bounds__(kScanBlock) void fsst_scan_blocks(int64_t* __restri
     if (threadIdx.x == 0) block_totals[blockIdx.x] = tot;
 }
 
-template <int OW, int LW, bool LSG>
+template <class OffAcc, class LenAcc>
 __global__ __launch_bounds__(kTile) void fsst_decode(const uint64_t* __restrict__ symbols,
                                                      const uint8_t* __restrict__ sym_lens, unsigned n_symbols,
-                                                     const uint8_t* __restrict__ codes, const void* code_offs,
-                                                     const void* lens, uint64_t n,
+                                                     const uint8_t* __restrict__ codes, OffAcc code_offs,
+                                                     LenAcc lens, uint64_t n,
                                                      const uint8_t* __restrict__ validity,
                                                      const int64_t* __restrict__ tile_prefix,
                                                      const int64_t* __restrict__ block_totals,
@@ -177,6 +167,7 @@ __global__ __launch_bounds__(kTile) void fsst_decode(const uint64_t* __restrict_
     __shared__ uint8_t s_len[256];
     __shared__ int64_t ws[kTile / 64];
     __shared__ int64_t s_block_prefix;
+    __shared__ int64_t s_coff[3];  // code_offs[0], code_offs[first], code_offs[last]
     __shared__ __attribute__((aligned(16))) uint8_t s_codes[kCodeLds + 48];
     __shared__ __attribute__((aligned(16))) uint32_t s_heap32[(kHeapLds + 48) / 4];
     uint8_t* const s_heap = reinterpret_cast<uint8_t*>(s_heap32);
@@ -184,7 +175,6 @@ __global__ __launch_bounds__(kTile) void fsst_decode(const uint64_t* __restrict_
     const int tid = threadIdx.x;
     // Prologue: every global load below is unconditional (indices clamped, results selected
     // afterwards) so they issue back to back and retire under ONE wait.
-    constexpr bool OSG = OW < 8;  // i32 offsets (VarBinBuilder<i32>, fsst/compress.rs:94)
     const uint64_t i = uint64_t(blockIdx.x) * kTile + tid;
     const bool live = i < n;
     const uint64_t ii = live ? i : n - 1;
@@ -193,10 +183,8 @@ __global__ __launch_bounds__(kTile) void fsst_decode(const uint64_t* __restrict_
     const uint64_t sk = uint32_t(tid) < n_symbols ? uint32_t(tid) : 0;
     const uint64_t sym_v = symbols[sk];
     const uint8_t slen_v = sym_lens[sk];
-    const int64_t len_v = ld<LW, LSG>(lens, ii);
-    const int64_t c_base = ld<OW, OSG>(code_offs, 0);
-    const int64_t cf = ld<OW, OSG>(code_offs, first);
-    const int64_t cl = ld<OW, OSG>(code_offs, last);
+    const int64_t len_v = lens(ii);
+    if (tid < 3) s_coff[tid] = code_offs(tid == 0 ? 0 : (tid == 1 ? first : last));  // read after the scan's barrier
     const int64_t tp = tile_prefix[blockIdx.x];
     const uint8_t vbyte = validity ? validity[ii >> 3] : uint8_t(0xFF);
     // symbol slot 255 is the escape: length 1, its byte comes from the code stream
@@ -220,6 +208,7 @@ __global__ __launch_bounds__(kTile) void fsst_decode(const uint64_t* __restrict_
     int64_t tile_total;
     const int64_t my_rel = block_exclusive_scan<kTile / 64>(my_len, ws, tile_total);
     const int64_t tile_out0 = tp + s_block_prefix;
+    const int64_t c_base = s_coff[0], cf = s_coff[1], cl = s_coff[2];
     // code offsets are relative to code_offs[0] (sliced_bytes(), varbin/mod.rs:130-136)
     const int64_t c0 = cf - c_base;
     const int64_t c1 = cl - c_base;
@@ -353,8 +342,8 @@ __global__ __launch_bounds__(kTile) void fsst_decode(const uint64_t* __restrict_
     } else {
         // direct path: per-string decode straight into HBM (codes of string i are
         // [offs[i], offs[i+1]); each must decode to exactly lengths[i] bytes)
-        const int64_t my_c0 = live ? ld<OW, OSG>(code_offs, ii) - c_base : 0;
-        const int64_t my_c1 = live ? ld<OW, OSG>(code_offs, ii + 1) - c_base : 0;
+        const int64_t my_c0 = live ? code_offs(ii) - c_base : 0;
+        const int64_t my_c1 = live ? code_offs(ii + 1) - c_base : 0;
         const uint8_t* gcodes = codes + c_base;
         int64_t o = tile_out0 + my_rel;
         const int64_t o_start = o, o_end = o + my_len;
@@ -388,8 +377,7 @@ uint64_t fsst_scratch_bytes(uint64_t n) {
 }
 
 vxg_status launch_fsst(const uint64_t* symbols, const uint8_t* sym_lens, unsigned n_symbols,
-                       const uint8_t* code_bytes, int offs_width, const void* code_offsets,
-                       int lens_width, bool lens_signed, const void* lens, uint64_t n,
+                       const uint8_t* code_bytes, const IntCol& offs, const IntCol& lens, uint64_t n,
                        const uint8_t* validity, void* scratch, uint8_t* heap, uint8_t* views,
                        uint32_t* err, hipStream_t s) {
     if (n == 0) return VXG_OK;
@@ -399,43 +387,37 @@ vxg_status launch_fsst(const uint64_t* symbols, const uint8_t* sym_lens, unsigne
     const uint64_t n_sum_wgs = (n_tiles + kSumTiles - 1) / kSumTiles;
     int64_t* tiles = static_cast<int64_t*>(scratch);
     int64_t* blocks = tiles + n_tiles;
-    const bool lsg = lens_signed;
-    auto run = [&](auto ow_c, auto lw_c, auto lsg_c) {
-        constexpr int OW = decltype(ow_c)::value, LW = decltype(lw_c)::value;
-        constexpr bool LSG = decltype(lsg_c)::value;
-        hipLaunchKernelGGL((fsst_tile_sums<LW, LSG>), dim3(unsigned(n_sum_wgs)), dim3(kTile), 0, s, lens, n, n_tiles,
+    auto run = [&](auto off_acc, auto len_acc) {
+        using OA = decltype(off_acc);
+        using LA = decltype(len_acc);
+        hipLaunchKernelGGL((fsst_tile_sums<LA>), dim3(unsigned(n_sum_wgs)), dim3(kTile), 0, s, len_acc, n, n_tiles,
                            tiles);
         hipLaunchKernelGGL(fsst_scan_blocks, dim3(unsigned(n_blocks)), dim3(kScanBlock), 0, s, tiles, n_tiles,
                            blocks);
-        hipLaunchKernelGGL((fsst_decode<OW, LW, LSG>), dim3(unsigned(n_tiles)), dim3(kTile), 0, s, symbols, sym_lens,
-                           n_symbols, code_bytes, code_offsets, lens, n, validity, tiles, blocks, heap,
+        hipLaunchKernelGGL((fsst_decode<OA, LA>), dim3(unsigned(n_tiles)), dim3(kTile), 0, s, symbols, sym_lens,
+                           n_symbols, code_bytes, off_acc, len_acc, n, validity, tiles, blocks, heap,
                            reinterpret_cast<uint4*>(views), err);
     };
-    using I4 = std::integral_constant<int, 4>;
-    using I8 = std::integral_constant<int, 8>;
-    using I2 = std::integral_constant<int, 2>;
-    using I1 = std::integral_constant<int, 1>;
-    using T_ = std::true_type;
-    using F_ = std::false_type;
-    auto with_lens = [&](auto ow_c) -> vxg_status {
-        switch (lens_width) {
-        case 1: lsg ? run(ow_c, I1{}, T_{}) : run(ow_c, I1{}, F_{}); break;
-        case 2: lsg ? run(ow_c, I2{}, T_{}) : run(ow_c, I2{}, F_{}); break;
-        case 4: lsg ? run(ow_c, I4{}, T_{}) : run(ow_c, I4{}, F_{}); break;
-        case 8: run(ow_c, I8{}, T_{}); break;
-        default: return set_error(VXG_ERR_MISMATCHED_TYPES, "FSST lengths must be 1/2/4/8-byte integers");
+    // accessor = plain width 1/2/4/8 or packed T = 32/64
+    auto with = [](const IntCol& c, auto&& f) -> bool {
+        if (c.packed) {
+            if (c.width == 4) return f(PackedCol<32>(c)), true;
+            if (c.width == 8) return f(PackedCol<64>(c)), true;
+            return false;
         }
-        return VXG_OK;
+        switch (c.width) {
+        case 1: return f(PlainCol<1>(c)), true;
+        case 2: return f(PlainCol<2>(c)), true;
+        case 4: return f(PlainCol<4>(c)), true;
+        case 8: return f(PlainCol<8>(c)), true;
+        default: return false;
+        }
     };
-    vxg_status st;
-    switch (offs_width) {
-    case 1: st = with_lens(I1{}); break;
-    case 2: st = with_lens(I2{}); break;
-    case 4: st = with_lens(I4{}); break;
-    case 8: st = with_lens(I8{}); break;
-    default: return set_error(VXG_ERR_MISMATCHED_TYPES, "FSST code offsets must be 1/2/4/8-byte integers");
-    }
-    if (st != VXG_OK) return st;
+    bool ok = true;
+    const bool ok_off = with(offs, [&](auto oa) { ok = with(lens, [&](auto la) { run(oa, la); }); });
+    if (!ok_off || !ok)
+        return set_error(VXG_ERR_MISMATCHED_TYPES, "FSST offsets/lengths must be 1/2/4/8-byte integers "
+                                                    "(packed: 32/64-bit)");
     return hip_check(hipGetLastError(), "fsst kernels");
 }
 

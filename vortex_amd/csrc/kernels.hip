@@ -12,6 +12,7 @@
 // All of them are HBM-streaming kernels: 16-byte-per-lane accesses where the layout allows it,
 // grid-stride loops capped at 8 workgroups per CU, no LDS except where a re-layout needs it.
 #include "fl_unpack_impl.hpp"
+#include "intcol.hpp"
 
 namespace vxg {
 
@@ -48,13 +49,13 @@ template <> struct UInt<16> { using t = uint4; };
 // ------------------------------------------------------------------ K2 patch scatter
 template <int T, Epi EPI, int VW>
 __global__ __launch_bounds__(kBlock) void patch_kernel(typename EpiOut<T, EPI, VW>::type* __restrict__ out,
-                                                       uint64_t out_len, const void* __restrict__ idx,
-                                                       int idx_width, int idx_signed, uint64_t idx_off,
+                                                       uint64_t out_len, IntCol idx, uint64_t idx_off,
                                                        const typename Fl<T>::E* __restrict__ vals,
                                                        uint64_t n, EpiParams ep) {
+    // indices read in place (a packed FoR/BitPacked index column is unpacked per patch)
     for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
          i += uint64_t(gridDim.x) * blockDim.x) {
-        const uint64_t p = load_uint(idx, idx_width, idx_signed != 0, i) - idx_off;
+        const uint64_t p = uint64_t(intcol_get(idx, i)) - idx_off;
         if (p >= out_len) {
             __hip_atomic_fetch_or(ep.err, kErrPatchOOB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             continue;
@@ -64,58 +65,55 @@ __global__ __launch_bounds__(kBlock) void patch_kernel(typename EpiOut<T, EPI, V
 }
 
 template <int T, Epi EPI, int VW>
-static vxg_status patch_launch(void* out, uint64_t out_len, const void* idx, int iw, bool is,
-                               uint64_t ioff, const void* vals, uint64_t n, const UnpackArgs& a,
-                               hipStream_t s) {
+static vxg_status patch_launch(void* out, uint64_t out_len, const IntCol& idx, uint64_t ioff,
+                               const void* vals, uint64_t n, const UnpackArgs& a, hipStream_t s) {
     using O = typename EpiOut<T, EPI, VW>::type;
     hipLaunchKernelGGL((patch_kernel<T, EPI, VW>), dim3(grid_for(n)), dim3(kBlock), 0, s,
-                       static_cast<O*>(out), out_len, idx, iw, int(is), ioff,
+                       static_cast<O*>(out), out_len, idx, ioff,
                        static_cast<const typename Fl<T>::E*>(vals), n, to_epi(a));
     return hip_check(hipGetLastError(), "patch_kernel");
 }
 
 template <int T, Epi EPI>
-static vxg_status patch_vw(int vw, void* out, uint64_t out_len, const void* idx, int iw, bool is,
-                           uint64_t ioff, const void* vals, uint64_t n, const UnpackArgs& a,
-                           hipStream_t s) {
+static vxg_status patch_vw(int vw, void* out, uint64_t out_len, const IntCol& idx, uint64_t ioff,
+                           const void* vals, uint64_t n, const UnpackArgs& a, hipStream_t s) {
     switch (vw) {
-    case 1: return patch_launch<T, EPI, 1>(out, out_len, idx, iw, is, ioff, vals, n, a, s);
-    case 2: return patch_launch<T, EPI, 2>(out, out_len, idx, iw, is, ioff, vals, n, a, s);
-    case 4: return patch_launch<T, EPI, 4>(out, out_len, idx, iw, is, ioff, vals, n, a, s);
-    case 8: return patch_launch<T, EPI, 8>(out, out_len, idx, iw, is, ioff, vals, n, a, s);
-    case 16: return patch_launch<T, EPI, 16>(out, out_len, idx, iw, is, ioff, vals, n, a, s);
+    case 1: return patch_launch<T, EPI, 1>(out, out_len, idx, ioff, vals, n, a, s);
+    case 2: return patch_launch<T, EPI, 2>(out, out_len, idx, ioff, vals, n, a, s);
+    case 4: return patch_launch<T, EPI, 4>(out, out_len, idx, ioff, vals, n, a, s);
+    case 8: return patch_launch<T, EPI, 8>(out, out_len, idx, ioff, vals, n, a, s);
+    case 16: return patch_launch<T, EPI, 16>(out, out_len, idx, ioff, vals, n, a, s);
     default: return VXG_ERR_INVALID_ARGUMENT;
     }
 }
 
 template <int T>
-static vxg_status patch_t(Epi epi, int vw, void* out, uint64_t out_len, const void* idx, int iw,
-                          bool is, uint64_t ioff, const void* vals, uint64_t n, const UnpackArgs& a,
-                          hipStream_t s) {
+static vxg_status patch_t(Epi epi, int vw, void* out, uint64_t out_len, const IntCol& idx, uint64_t ioff,
+                          const void* vals, uint64_t n, const UnpackArgs& a, hipStream_t s) {
     switch (epi) {
-    case Epi::Plain: return patch_launch<T, Epi::Plain, 0>(out, out_len, idx, iw, is, ioff, vals, n, a, s);
-    case Epi::For: return patch_launch<T, Epi::For, 0>(out, out_len, idx, iw, is, ioff, vals, n, a, s);
-    case Epi::ForZigZag: return patch_launch<T, Epi::ForZigZag, 0>(out, out_len, idx, iw, is, ioff, vals, n, a, s);
+    case Epi::Plain: return patch_launch<T, Epi::Plain, 0>(out, out_len, idx, ioff, vals, n, a, s);
+    case Epi::For: return patch_launch<T, Epi::For, 0>(out, out_len, idx, ioff, vals, n, a, s);
+    case Epi::ForZigZag: return patch_launch<T, Epi::ForZigZag, 0>(out, out_len, idx, ioff, vals, n, a, s);
     case Epi::AlpF32:
-        if constexpr (T == 32) return patch_launch<32, Epi::AlpF32, 0>(out, out_len, idx, iw, is, ioff, vals, n, a, s);
+        if constexpr (T == 32) return patch_launch<32, Epi::AlpF32, 0>(out, out_len, idx, ioff, vals, n, a, s);
         return VXG_ERR_INVALID_ARGUMENT;
     case Epi::AlpF64:
-        if constexpr (T == 64) return patch_launch<64, Epi::AlpF64, 0>(out, out_len, idx, iw, is, ioff, vals, n, a, s);
+        if constexpr (T == 64) return patch_launch<64, Epi::AlpF64, 0>(out, out_len, idx, ioff, vals, n, a, s);
         return VXG_ERR_INVALID_ARGUMENT;
-    case Epi::Dict: return patch_vw<T, Epi::Dict>(vw, out, out_len, idx, iw, is, ioff, vals, n, a, s);
+    case Epi::Dict: return patch_vw<T, Epi::Dict>(vw, out, out_len, idx, ioff, vals, n, a, s);
     }
     return VXG_ERR_INVALID_ARGUMENT;
 }
 
-vxg_status launch_patch(int val_width, int idx_width, bool idx_signed, Epi epi, int T, void* out,
-                        uint64_t out_len, const void* indices, uint64_t indices_offset,
-                        const void* values, uint64_t n, const UnpackArgs& ep, hipStream_t s) {
+vxg_status launch_patch(int val_width, const IntCol& indices, Epi epi, int T, void* out, uint64_t out_len,
+                        uint64_t indices_offset, const void* values, uint64_t n, const UnpackArgs& ep,
+                        hipStream_t s) {
     if (n == 0) return VXG_OK;
     switch (T) {
-    case 8: return patch_t<8>(epi, val_width, out, out_len, indices, idx_width, idx_signed, indices_offset, values, n, ep, s);
-    case 16: return patch_t<16>(epi, val_width, out, out_len, indices, idx_width, idx_signed, indices_offset, values, n, ep, s);
-    case 32: return patch_t<32>(epi, val_width, out, out_len, indices, idx_width, idx_signed, indices_offset, values, n, ep, s);
-    case 64: return patch_t<64>(epi, val_width, out, out_len, indices, idx_width, idx_signed, indices_offset, values, n, ep, s);
+    case 8: return patch_t<8>(epi, val_width, out, out_len, indices, indices_offset, values, n, ep, s);
+    case 16: return patch_t<16>(epi, val_width, out, out_len, indices, indices_offset, values, n, ep, s);
+    case 32: return patch_t<32>(epi, val_width, out, out_len, indices, indices_offset, values, n, ep, s);
+    case 64: return patch_t<64>(epi, val_width, out, out_len, indices, indices_offset, values, n, ep, s);
     default: return VXG_ERR_INVALID_ARGUMENT;
     }
 }

@@ -104,10 +104,23 @@ struct DictChunkTable {
 vxg_status launch_fl_unpack_dict_chunks(int T, int W, int value_width, const DictChunkTable& tab,
                                         uint64_t total_groups, uint32_t* err, hipStream_t s);
 
+// An integer column a consumer kernel (FSST, patch scatter) reads in place: a plain array of `width`-byte integers,
+// or a patch-free [FoR](BitPacked) column of T = 8*width bits (T = 32/64) whose elements are
+// unpacked where they are used (fastlanes unpack_single, bitpacking/compress.rs:295-306).
+struct IntCol {
+    const void* p;
+    int width;           // bytes of the logical integer type (1, 2, 4, 8)
+    bool sgn;
+    bool packed;
+    uint32_t W;          // packed: bit width
+    uint32_t shift;      // packed: FoR shift
+    uint32_t offset;     // packed: BitPacked slice offset (< 1024)
+    uint64_t reference;  // packed: FoR reference (0 for a bare BitPacked column)
+};
 // Patch scatter with the same epilogue applied to the patch value.
-vxg_status launch_patch(int val_width, int idx_width, bool idx_signed, Epi epi, int T,
-                        void* out, uint64_t out_len, const void* indices, uint64_t indices_offset,
-                        const void* values, uint64_t n, const UnpackArgs& ep, hipStream_t s);
+vxg_status launch_patch(int val_width, const IntCol& indices, Epi epi, int T, void* out, uint64_t out_len,
+                        uint64_t indices_offset, const void* values, uint64_t n, const UnpackArgs& ep,
+                        hipStream_t s);
 
 vxg_status launch_for(int width, const void* in, uint64_t n, uint64_t ref, unsigned shift,
                       bool zigzag, void* out, hipStream_t s);
@@ -151,8 +164,7 @@ vxg_status launch_fill(int value_width, const uint8_t* scalar16, uint64_t n, voi
                        hipStream_t s);
 uint64_t fsst_scratch_bytes(uint64_t n);
 vxg_status launch_fsst(const uint64_t* symbols, const uint8_t* sym_lens, unsigned n_symbols,
-                       const uint8_t* code_bytes, int offs_width, const void* code_offsets,
-                       int lens_width, bool lens_signed, const void* lens, uint64_t n,
+                       const uint8_t* code_bytes, const IntCol& offs, const IntCol& lens, uint64_t n,
                        const uint8_t* validity, void* scratch, uint8_t* heap, uint8_t* views,
                        uint32_t* err, hipStream_t s);
 vxg_status launch_varbin_views(const uint8_t* heap, int offs_width, const void* offsets, uint64_t n,
