@@ -161,37 +161,34 @@ def chk(st):
 
 
 def run_workload(wl: Workload, steps: int, warmup: int, dist, rank: int):
+    """Warmup, then exactly `steps` back-to-back steps between barrier + synchronize.  Two HIP
+    events on the decode stream (torch's current stream, the stream vxg_canonicalize is given)
+    bracket the timed steps: (e1 - e0) / steps is the device time per step (per launch for a
+    one-kernel step like C1) without per-step event gaps."""
     import torch
     for _ in range(warmup):
         wl.step()
     wl.ctx.sync()
-    # timed region: exactly `steps` steps, barrier + synchronize on both sides, no events
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    e0.record()
     for s in range(steps):
         wl.step()
+    e1.record()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     wl.ctx.sync()  # surfaces device-side errors (OOB codes, ...)
-    # separate pass for the per-launch device time: HIP events on the decode stream (torch's
-    # current stream, which is the stream vxg_canonicalize is given) around each step
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
-    for s in range(steps):
-        ev[s][0].record()
-        wl.step()
-        ev[s][1].record()
-    torch.cuda.synchronize()
-    wl.ctx.sync()
-    kms = [a.elapsed_time(b) for a, b in ev]
+    kms = e0.elapsed_time(e1) / steps
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    return elapsed, float(np.mean(kms)), float(np.median(kms))
+    return elapsed, kms, kms
 
 
 def run_e2e(arr, info, ctx, reps: int = 5):
