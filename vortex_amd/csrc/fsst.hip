@@ -24,6 +24,7 @@
 //   A tile whose codes do not decode to exactly the sum of its lengths raises an error (the
 //   reference would slice a shifted stream); tiles too large for the LDS images take a
 //   per-string direct-to-HBM path that checks every string.
+#include "fl_unpack_impl.hpp"
 #include "intcol.hpp"
 
 namespace vxg {
@@ -36,8 +37,7 @@ constexpr int kTile = 256;            // strings per tile = threads per workgrou
 // resident per CU.  Larger tiles take the direct path.
 constexpr int kCodeLds = 6 * 1024;    // staged code bytes per tile
 constexpr int kHeapLds = 10 * 1024;   // staged output bytes per tile
-constexpr int kScanBlock = 1024;      // tiles per scan_blocks workgroup
-constexpr int kSumTiles = 16;         // tiles per tile_sums workgroup
+constexpr int kScanTiles = 128;       // tiles per pre-pass workgroup (= 32 FastLanes blocks)
 
 __device__ __forceinline__ int64_t wave_sum(int64_t x) {
 #pragma unroll
@@ -114,43 +114,134 @@ __device__ __forceinline__ uint32_t byte_of(const uint4& v, int j) {
 
 }  // namespace
 
-template <class LenAcc>
-__global__ __launch_bounds__(kTile) void fsst_tile_sums(LenAcc lens, uint64_t n, uint64_t n_tiles,
-                                                        int64_t* __restrict__ tile_sums) {
-    // 16 tiles per workgroup; in round r wave w sums tile 4r + w: each lane adds 4 consecutive
-    // lengths (64 lanes x 4 = one 256-string tile), then ONE wave reduction per tile.
-    const uint64_t t0 = uint64_t(blockIdx.x) * kSumTiles;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    int64_t v[kSumTiles / 4];
-#pragma unroll
-    for (int r = 0; r < kSumTiles / 4; r++) {  // 16 independent loads in flight per lane
-        const uint64_t base = (t0 + 4 * r + wave) * kTile + 4 * lane;
-        int64_t acc = 0;
-#pragma unroll
-        for (int e = 0; e < 4; e++) {
-            const uint64_t i = base + e;
-            const int64_t x = lens(i < n ? i : n - 1);
-            acc += i < n ? x : 0;
-        }
-        v[r] = acc;
-    }
-#pragma unroll
-    for (int r = 0; r < kSumTiles / 4; r++) {
-        const int64_t s = wave_sum(v[r]);
-        const uint64_t t = t0 + 4 * r + wave;
-        if (lane == 0 && t < n_tiles) tile_sums[t] = s;
-    }
+// Inclusive scan of one int32 per lane across the wave: DPP row shifts inside 16-lane rows,
+// then row broadcasts (no LDS round trips).
+__device__ __forceinline__ int wave_incl_scan(int x) {
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);  // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);  // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true);  // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true);  // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+    return x;
 }
 
-__global__ __launch_bounds__(kScanBlock) void fsst_scan_blocks(int64_t* __restrict__ tile_sums, uint64_t n_tiles,
-                                                               int64_t* __restrict__ block_totals) {
-    __shared__ int64_t ws[kScanBlock / 64];
-    const uint64_t i = uint64_t(blockIdx.x) * kScanBlock + threadIdx.x;
-    const int64_t v = i < n_tiles ? tile_sums[i] : 0;
+// Exclusive block scan of one int32 per thread (kTile/64 waves); `ws` must not be reused
+// before the next barrier.
+__device__ __forceinline__ int block_excl_scan32(int v, int* ws, int& total) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int x = wave_incl_scan(v);
+    if (lane == 63) ws[wave] = x;
+    __syncthreads();
+    int before = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < kTile / 64; w++) {
+        const int s = ws[w];
+        before += w < wave ? s : 0;
+        tot += s;
+    }
+    total = tot;
+    return before + x - v;
+}
+
+// Pre-pass: per workgroup of 128 tiles, the tile length sums, their exclusive scan
+// (tile_prefix) and the workgroup total (block_totals).  The decode adds the totals of the
+// preceding workgroups (<= a few hundred) itself.
+template <class LenAcc>
+__device__ __forceinline__ void scan_tile_sums(const int64_t* s_ts, int64_t* ws, uint64_t n_tiles,
+                                               int64_t* __restrict__ tile_prefix, int64_t* __restrict__ block_totals) {
+    const int tid = threadIdx.x;
     int64_t tot;
-    const int64_t ex = block_exclusive_scan<kScanBlock / 64>(v, ws, tot);
-    if (i < n_tiles) tile_sums[i] = ex;
-    if (threadIdx.x == 0) block_totals[blockIdx.x] = tot;
+    const int64_t ex = block_exclusive_scan<kTile / 64>(tid < kScanTiles ? s_ts[tid] : 0, ws, tot);
+    const uint64_t tt = uint64_t(blockIdx.x) * kScanTiles + tid;
+    if (tid < kScanTiles && tt < n_tiles) tile_prefix[tt] = ex;
+    if (tid == 0) block_totals[blockIdx.x] = tot;
+}
+
+// Any length column: wave w sums tile 4r + w in round r (4 consecutive lengths per lane).
+template <class LenAcc>
+__global__ __launch_bounds__(kTile) void fsst_tile_scan(LenAcc lens, uint64_t n, uint64_t n_tiles,
+                                                        int64_t* __restrict__ tile_prefix,
+                                                        int64_t* __restrict__ block_totals) {
+    __shared__ int64_t s_ts[kScanTiles];
+    __shared__ int64_t ws[kTile / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t t0 = uint64_t(blockIdx.x) * kScanTiles;
+    for (int r0 = 0; r0 < kScanTiles / 4; r0 += 8) {
+        int64_t v[8];
+#pragma unroll
+        for (int r = 0; r < 8; r++) {  // 32 independent loads in flight per lane
+            const uint64_t base = (t0 + 4 * (r0 + r) + wave) * kTile + 4 * lane;
+            int64_t acc = 0;
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+                const uint64_t i = base + e;
+                const int64_t x = lens(i < n ? i : n - 1);
+                acc += i < n ? x : 0;
+            }
+            v[r] = acc;
+        }
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+            const int64_t sum = wave_sum(v[r]);
+            if (lane == 0) s_ts[4 * (r0 + r) + wave] = sum;
+        }
+    }
+    __syncthreads();
+    scan_tile_sums<LenAcc>(s_ts, ws, n_tiles, tile_prefix, block_totals);
+}
+
+// Patch-free FoR(BitPacked u32/i32) lengths with offset 0 (the reference cascade): decode
+// whole FastLanes blocks K1-style (8 threads per block, W x 16-byte loads, SWAR rows).  Row R
+// of a block holds strings (R % 8) * 128 + ..., i.e. tile (R % 8) / 2 of the block, so each
+// thread accumulates 4 tile partial sums, reduced across its 8 threads.
+template <int W, int... Rs>
+__device__ __forceinline__ void fl32_tile_rows(const Vec16<32>* p, int t, uint64_t blk0, uint64_t n, uint32_t shift,
+                                               uint32_t reference, bool sgn, int64_t* acc,
+                                               std::integer_sequence<int, Rs...>) {
+    auto row = [&](auto rc) {
+        constexpr int R = decltype(rc)::value;
+        const Vec16<32> v = extract_row<32, W, R>(p);
+        const int idx0 = fl_index(R, 4 * t);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t u = uint32_t(v.elem(j) << shift) + reference;
+            const int64_t x = sgn ? int64_t(int32_t(u)) : int64_t(u);
+            acc[(R % 8) / 2] += blk0 + uint64_t(idx0 + j) < n ? x : 0;
+        }
+    };
+    (row(std::integral_constant<int, Rs>{}), ...);
+}
+
+template <int W>
+__global__ __launch_bounds__(kTile) void fsst_tile_scan_fl32(const uint8_t* __restrict__ packed, uint32_t shift,
+                                                             uint32_t reference, bool sgn, uint64_t n,
+                                                             uint64_t n_tiles, int64_t* __restrict__ tile_prefix,
+                                                             int64_t* __restrict__ block_totals) {
+    __shared__ int64_t s_ts[kScanTiles];
+    __shared__ int64_t ws[kTile / 64];
+    const int tid = threadIdx.x, t = tid & 7;
+    const uint64_t blk = uint64_t(blockIdx.x) * (kScanTiles / 4) + (tid >> 3);
+    int64_t acc[4] = {0, 0, 0, 0};
+    if (blk * 1024 < n) {
+        Vec16<32> p[W > 0 ? W : 1];
+        if constexpr (W > 0) {
+#pragma unroll
+            for (int w = 0; w < W; w++) p[w] = load16<32>(packed + blk * (128 * W) + 128 * w + 16 * t);
+        }
+        fl32_tile_rows<W>(p, t, blk * 1024, n, shift, reference, sgn, acc, std::make_integer_sequence<int, 32>{});
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+#pragma unroll
+        for (int d = 1; d < 8; d <<= 1) acc[k] += __shfl_xor(acc[k], d, 64);
+    }
+    if (t == 0) {
+#pragma unroll
+        for (int k = 0; k < 4; k++) s_ts[(tid >> 3) * 4 + k] = acc[k];
+    }
+    __syncthreads();
+    scan_tile_sums<void>(s_ts, ws, n_tiles, tile_prefix, block_totals);
 }
 
 template <class OffAcc, class LenAcc>
@@ -165,72 +256,83 @@ __global__ __launch_bounds__(kTile) void fsst_decode(const uint64_t* __restrict_
                                                      uint32_t* __restrict__ err) {
     __shared__ uint64_t s_sym[256];
     __shared__ uint8_t s_len[256];
-    __shared__ int64_t ws[kTile / 64];
+    __shared__ int ws_a[kTile / 64], ws_b[kTile / 64];
+    __shared__ unsigned ws_bad[kTile / 64];
+    __shared__ int64_t ws64[kTile / 64];
     __shared__ int64_t s_block_prefix;
     __shared__ int64_t s_coff[3];  // code_offs[0], code_offs[first], code_offs[last]
     __shared__ __attribute__((aligned(16))) uint8_t s_codes[kCodeLds + 48];
     __shared__ __attribute__((aligned(16))) uint32_t s_heap32[(kHeapLds + 48) / 4];
     uint8_t* const s_heap = reinterpret_cast<uint8_t*>(s_heap32);
 
-    const int tid = threadIdx.x;
-    // Prologue: every global load below is unconditional (indices clamped, results selected
-    // afterwards) so they issue back to back and retire under ONE wait.
-    const uint64_t i = uint64_t(blockIdx.x) * kTile + tid;
-    const bool live = i < n;
-    const uint64_t ii = live ? i : n - 1;
-    const uint64_t first = uint64_t(blockIdx.x) * kTile;
-    const uint64_t last = first + kTile < n ? first + kTile : n;
-    const uint64_t sk = uint32_t(tid) < n_symbols ? uint32_t(tid) : 0;
-    const uint64_t sym_v = symbols[sk];
-    const uint8_t slen_v = sym_lens[sk];
-    const int64_t len_v = lens(ii);
-    if (tid < 3) s_coff[tid] = code_offs(tid == 0 ? 0 : (tid == 1 ? first : last));  // read after the scan's barrier
-    const int64_t tp = tile_prefix[blockIdx.x];
-    const uint8_t vbyte = validity ? validity[ii >> 3] : uint8_t(0xFF);
-    // symbol slot 255 is the escape: length 1, its byte comes from the code stream
-    // (kTile == 256 symbol slots.)  Symbols are stored zero-padded past their length, so a
-    // code can OR all 8 bytes; a length > 8 is corrupt input.
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint32_t tile = blockIdx.x;
     {
+        const uint32_t sk = uint32_t(tid) < n_symbols ? uint32_t(tid) : 0;
+        const uint64_t sym_v = symbols[sk];
+        const uint32_t sl = sym_lens[sk];
+        // slot 255 is the escape (length 1, its byte comes from the code stream).  Symbols are
+        // stored zero-padded past their length, so a code can OR all 8 bytes; a length > 8
+        // is corrupt input.
         const bool has = uint32_t(tid) < n_symbols;
-        const uint32_t sl = slen_v;
         if (has && sl > 8) __hip_atomic_fetch_or(err, kErrFsst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s_sym[tid] = has ? (sl >= 8 ? sym_v : sym_v & ((1ull << (8 * sl)) - 1)) : 0;
         s_len[tid] = has ? uint8_t(min(sl, 8u)) : uint8_t(tid == 255 ? 1 : 0);
     }
-    if (tid < 64) {  // (a) prefix of the preceding 1024-tile blocks, one wave
-        const uint64_t nb = blockIdx.x / kScanBlock;
+    // Prologue: every global load is unconditional (indices clamped, results selected
+    // afterwards) so they retire under one wait.
+    const uint64_t first = uint64_t(tile) * kTile;
+    const uint64_t i = first + tid;
+    const bool live = i < n;
+    const uint64_t ii = live ? i : n - 1;
+    const uint64_t last = first + kTile < n ? first + kTile : n;
+    const int64_t len_v = lens(ii);
+    if (tid < 3) s_coff[tid] = code_offs(tid == 0 ? 0 : (tid == 1 ? first : last));  // read after a barrier
+    const uint8_t vbyte = validity ? validity[ii >> 3] : uint8_t(0xFF);
+    const int64_t tp = tile_prefix[tile];
+    if (wave == 0) {  // prefix of the preceding scan blocks (<= a few hundred totals), one wave
+        const uint32_t nb = tile / kScanTiles;
         int64_t acc = 0;
-        for (uint64_t b = tid; b < nb; b += 64) acc += block_totals[b];
+        for (uint32_t b = lane; b < nb; b += 64) acc += block_totals[b];
         acc = wave_sum(acc);
-        if (tid == 0) s_block_prefix = acc;
+        if (lane == 0) s_block_prefix = acc;
     }
     const int64_t my_len = live ? len_v : 0;
-    int64_t tile_total;
-    const int64_t my_rel = block_exclusive_scan<kTile / 64>(my_len, ws, tile_total);
+
+    // (a) length scan: int32 with DPP when every length is in [0, kHeapLds] (then a staged
+    // tile is possible), int64 otherwise (direct path).
+    const bool bad = my_len < 0 || my_len > kHeapLds;
+    const unsigned long long bm = __ballot(bad);
+    if (lane == 0) ws_bad[wave] = bm != 0;
+    int t32;
+    const int rel32 = block_excl_scan32(bad ? 0 : int(my_len), ws_a, t32);
+    const bool any_bad = (ws_bad[0] | ws_bad[1] | ws_bad[2] | ws_bad[3]) != 0;
+    int64_t my_rel = rel32, tile_total = t32;
+    if (any_bad) my_rel = block_exclusive_scan<kTile / 64>(my_len, ws64, tile_total);  // uniform branch
     const int64_t tile_out0 = tp + s_block_prefix;
+
     const int64_t c_base = s_coff[0], cf = s_coff[1], cl = s_coff[2];
     // code offsets are relative to code_offs[0] (sliced_bytes(), varbin/mod.rs:130-136)
-    const int64_t c0 = cf - c_base;
-    const int64_t c1 = cl - c_base;
+    const int64_t c0 = cf - c_base, c1 = cl - c_base;
     const bool valid = live && ((vbyte >> (ii & 7)) & 1);
     const uint32_t vlen = valid ? uint32_t(my_len) : 0u;
-    const bool stage = (c1 - c0) <= kCodeLds && tile_total <= kHeapLds && tile_total >= 0 && c1 >= c0;
+    const bool stage = !any_bad && (c1 - c0) <= kCodeLds && c1 >= c0 && tile_total <= kHeapLds;
 
     if (stage) {
-        // LDS images sit at the same offset mod 16 as their global counterparts, so staging
-        // loads and copy-out stores move whole aligned 16-byte chunks.
-        const int64_t cabs0 = c_base + c0, cabs1 = c_base + c1;  // tile codes in `codes`
+        // (b) stage the tile's codes at the same offset mod 16 as in `codes` (an aligned 16-byte
+        // chunk holding a tile byte never crosses a page, so it is read whole; bytes outside
+        // the tile are ignored), and zero the output image (+16 slack for view reads)
+        const int64_t cabs0 = c_base + c0;
         const int cshift = int((reinterpret_cast<uintptr_t>(codes) + cabs0) & 15);
-        const int hshift = int((reinterpret_cast<uintptr_t>(heap) + tile_out0) & 15);
-        const int ncode = int(cabs1 - cabs0);
-        const int span = cshift + ncode;  // tile codes at s_codes[cshift, span)
-        {   // (b) an aligned 16-byte chunk holding at least one tile byte never crosses a page
-            // boundary, so it is read whole; bytes outside the tile are ignored below.
+        const int hshift = int((reinterpret_cast<uintptr_t>(heap) + tile_out0) & 15);  // image byte hshift = heap[tile_out0]
+        const int span = cshift + int(c1 - c0);  // tile codes at s_codes[cshift, span)
+        const int ttot = int(tile_total);
+        {
             const uint8_t* a0 = codes + (cabs0 - cshift);
             const int nchunk = (span + 15) >> 4;
             for (int q = tid; q < nchunk; q += kTile)
                 *reinterpret_cast<uint4*>(s_codes + 16 * q) = *reinterpret_cast<const uint4*>(a0 + 16 * q);
-            const int nz = (hshift + int(tile_total) + 16 + 15) >> 4;  // zero the image (+16 slack)
+            const int nz = (hshift + ttot + 16 + 15) >> 4;
             for (int q = tid; q < nz; q += kTile) reinterpret_cast<uint4*>(s_heap32)[q] = make_uint4(0, 0, 0, 0);
         }
         __syncthreads();
@@ -276,17 +378,17 @@ __global__ __launch_bounds__(kTile) void fsst_decode(const uint64_t* __restrict_
                 }
             }
         }
-        int64_t dec_total;
-        const int64_t seg_rel = block_exclusive_scan<kTile / 64>(sum, ws, dec_total);
-        if (tid == 0 && dec_total != tile_total)
+        int dec_total;
+        const int seg_rel = block_excl_scan32(sum, ws_b, dec_total);
+        if (tid == 0 && dec_total != ttot)
             __hip_atomic_fetch_or(err, kErrFsst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // pass 2: every code ORs its (zero-padded) bytes into <= 3 dwords of the image.  All 16
         // symbol reads of a chunk are issued before its first ds_or; the ORs are unconditional
         // (zero for literals / outside the tile) so the chunk runs without branches.  Offsets
         // are clamped to the tile's end (only corrupt input, already flagged, reaches it).
         {
-            int o = hshift + int(seg_rel);
-            const int o_end = hshift + int(tile_total);
+            int o = hshift + seg_rel;
+            const int o_end = hshift + ttot;
 #pragma unroll
             for (int h = 0; h < 2; h++) {
                 if (h < nch) {
@@ -321,19 +423,20 @@ __global__ __launch_bounds__(kTile) void fsst_decode(const uint64_t* __restrict_
             }
         }
         __syncthreads();
-        // (d) copy-out of [tile_out0, tile_out0 + tile_total): whole aligned 16-byte chunks via
-        // ds_read_b128 + global_store_dwordx4; the ragged first/last chunk byte by byte (they
-        // are shared with the neighbouring tiles)
-        const int64_t g0 = tile_out0, g1 = tile_out0 + tile_total;
-        const int64_t a0 = g0 - hshift;  // aligned chunk containing g0
-        const int nchunk = int((g1 - a0 + 15) / 16);
-        for (int q = tid; q < nchunk; q += kTile) {
-            const int64_t g = a0 + 16 * q;
-            if (g >= g0 && g + 16 <= g1) {
-                *reinterpret_cast<uint4*>(heap + g) = *reinterpret_cast<const uint4*>(s_heap + 16 * q);
-            } else {
-                for (int b = 0; b < 16; b++)
-                    if (g + b >= g0 && g + b < g1) heap[g + b] = s_heap[16 * q + b];
+        // (d) copy-out of [tile_out0, tile_out0 + ttot): the image sits at the same offset mod 16
+        // as its destination, so whole aligned chunks move as ds_read_b128 + 16-byte stores;
+        // the ragged first/last chunk byte by byte (shared with the neighbouring tiles)
+        {
+            uint8_t* const gbase = heap + (tile_out0 - hshift);
+            const int nchunk = (hshift + ttot + 15) >> 4;
+            for (int q = tid; q < nchunk; q += kTile) {
+                const int lb = 16 * q;
+                if (lb >= hshift && lb + 16 <= hshift + ttot) {
+                    nt_store(reinterpret_cast<uint4*>(gbase + lb), *reinterpret_cast<const uint4*>(s_heap + lb));
+                } else {
+                    for (int b = 0; b < 16; b++)
+                        if (lb + b >= hshift && lb + b < hshift + ttot) gbase[lb + b] = s_heap[lb + b];
+                }
             }
         }
         if (live)
@@ -373,7 +476,16 @@ __global__ __launch_bounds__(kTile) void fsst_decode(const uint64_t* __restrict_
 
 uint64_t fsst_scratch_bytes(uint64_t n) {
     const uint64_t n_tiles = (n + kTile - 1) / kTile;
-    return (n_tiles + (n_tiles + kScanBlock - 1) / kScanBlock + 2) * sizeof(int64_t);
+    return (n_tiles + (n_tiles + kScanTiles - 1) / kScanTiles + 2) * sizeof(int64_t);
+}
+
+template <int... Ws>
+static void launch_tile_scan_fl32(int W, dim3 grid, hipStream_t s, const IntCol& c, uint64_t n, uint64_t n_tiles,
+                                  int64_t* tiles, int64_t* blocks, std::integer_sequence<int, Ws...>) {
+    using Fn = void (*)(const uint8_t*, uint32_t, uint32_t, bool, uint64_t, uint64_t, int64_t*, int64_t*);
+    static constexpr Fn table[] = {&fsst_tile_scan_fl32<Ws>...};
+    hipLaunchKernelGGL(table[W], grid, dim3(kTile), 0, s, static_cast<const uint8_t*>(c.p), c.shift,
+                       uint32_t(c.reference), c.sgn, n, n_tiles, tiles, blocks);
 }
 
 vxg_status launch_fsst(const uint64_t* symbols, const uint8_t* sym_lens, unsigned n_symbols,
@@ -383,17 +495,20 @@ vxg_status launch_fsst(const uint64_t* symbols, const uint8_t* sym_lens, unsigne
     if (n == 0) return VXG_OK;
     if (n_symbols > 255) return set_error(VXG_ERR_INVALID_ARGUMENT, "FSST symbol table > 255 entries");
     const uint64_t n_tiles = (n + kTile - 1) / kTile;
-    const uint64_t n_blocks = (n_tiles + kScanBlock - 1) / kScanBlock;
-    const uint64_t n_sum_wgs = (n_tiles + kSumTiles - 1) / kSumTiles;
+    if (n_tiles > 0xFFFFFFFFull) return set_error(VXG_ERR_INVALID_ARGUMENT, "FSST array too long");
+    const uint64_t n_scan = (n_tiles + kScanTiles - 1) / kScanTiles;
     int64_t* tiles = static_cast<int64_t*>(scratch);
     int64_t* blocks = tiles + n_tiles;
+    const bool fl32 = lens.packed && lens.width == 4 && lens.offset == 0 && lens.W <= 32;
+    if (fl32)
+        launch_tile_scan_fl32(int(lens.W), dim3(unsigned(n_scan)), s, lens, n, n_tiles, tiles, blocks,
+                              std::make_integer_sequence<int, 33>{});
     auto run = [&](auto off_acc, auto len_acc) {
         using OA = decltype(off_acc);
         using LA = decltype(len_acc);
-        hipLaunchKernelGGL((fsst_tile_sums<LA>), dim3(unsigned(n_sum_wgs)), dim3(kTile), 0, s, len_acc, n, n_tiles,
-                           tiles);
-        hipLaunchKernelGGL(fsst_scan_blocks, dim3(unsigned(n_blocks)), dim3(kScanBlock), 0, s, tiles, n_tiles,
-                           blocks);
+        if (!fl32)
+            hipLaunchKernelGGL((fsst_tile_scan<LA>), dim3(unsigned(n_scan)), dim3(kTile), 0, s, len_acc, n, n_tiles,
+                               tiles, blocks);
         hipLaunchKernelGGL((fsst_decode<OA, LA>), dim3(unsigned(n_tiles)), dim3(kTile), 0, s, symbols, sym_lens,
                            n_symbols, code_bytes, off_acc, len_acc, n, validity, tiles, blocks, heap,
                            reinterpret_cast<uint4*>(views), err);
