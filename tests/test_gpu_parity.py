@@ -269,6 +269,42 @@ def test_chunked_grouped_dict(ctx):
     assert_primitive_parity(arr, ctx, np.concatenate(expect))
 
 
+@pytest.mark.parametrize("kind", ["bitpacked", "for", "zigzag", "alp64", "alp32", "dict8"])
+def test_chunked_grouped_every_epilogue(ctx, kind):
+    """Chunked arrays whose chunks are one K1 decode each share launches (chunk tables of up
+    to 32 per kernel, grouped by (T, W, epilogue)): 70 chunks -> several batches, per-chunk
+    widths / FoR references / ALP exponents differ, ragged chunk lengths, and patches (inner
+    BitPacked patches and outer ALP patches) applied after the grouped launches."""
+    rng = np.random.default_rng(len(kind))
+    chunks, expect = [], []
+    for c in range(70):
+        n = 4096 * (1 + c % 3) + (c * 37) % 1000
+        if kind == "bitpacked":
+            v = rng.integers(0, 1 << (3 + c % 5), n, dtype=np.uint64).astype(np.uint32)
+            v[rng.choice(n, 3, replace=False)] = 2 ** 31 + c   # patches
+            arr = E.encode_bitpacked(v)
+        elif kind == "for":
+            v = (rng.integers(-500, 500, n) + 10_000 * c).astype(np.int64)
+            arr = E.encode_for_bitpacked(v)
+        elif kind == "zigzag":
+            v = rng.integers(-(1 << (4 + c % 4)), 1 << (4 + c % 4), n).astype(np.int32)
+            arr = E.encode_zigzag(v)
+        elif kind == "alp64":
+            v = np.round(rng.uniform(0, 10 ** (1 + c % 5), n), 2 + c % 2)
+            v[rng.choice(n, 2, replace=False)] = rng.standard_normal(2) * 1e300
+            arr = E.encode_alp(v)
+        elif kind == "alp32":
+            v = (np.round(rng.uniform(0, 100, n), 1)).astype(np.float32)
+            arr = E.encode_alp(v)
+        else:
+            dv = rng.integers(0, 2 ** 63, 17 + c, dtype=np.uint64)
+            v = dv[rng.integers(0, dv.size, n)]
+            arr = E.encode_dict(v)
+        chunks.append(arr)
+        expect.append(v)
+    assert_primitive_parity(A.chunked(chunks), ctx, np.concatenate(expect))
+
+
 def test_chunked_mixed_with_validity(ctx):
     a = E.encode_bitpacked(np.arange(3000, dtype=np.uint32) % 77, validity=(np.arange(3000) % 5 != 0))
     b = A.primitive(np.arange(1001, dtype=np.uint32), validity=None)

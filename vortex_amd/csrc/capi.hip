@@ -13,6 +13,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "vxg_internal.hpp"
@@ -54,47 +55,34 @@ vxg_status hip_check(hipError_t e, const char* what) {
 }
 
 // K1 dispatch over the instantiation units.
-vxg_status launch_fl_unpack(int T, int W, Epi epi, int vw, const UnpackArgs& a, hipStream_t s) {
+vxg_status launch_fl_unpack(int T, int W, Epi epi, int vw, const ChunkTable& t, uint64_t g, hipStream_t s) {
     if (W < 0 || W > T) return set_error(VXG_ERR_INVALID_ARGUMENT, "bit width out of range");
     switch (epi) {
     case Epi::Plain:
     case Epi::For:
     case Epi::ForZigZag:
         switch (T) {
-        case 8: return fl_plain_8(W, epi, a, s);
-        case 16: return fl_plain_16(W, epi, a, s);
-        case 32: return fl_plain_32(W, epi, a, s);
-        case 64: return fl_plain_64(W, epi, a, s);
+        case 8: return fl_plain_8(W, epi, t, g, s);
+        case 16: return fl_plain_16(W, epi, t, g, s);
+        case 32: return fl_plain_32(W, epi, t, g, s);
+        case 64: return fl_plain_64(W, epi, t, g, s);
         }
         return set_error(VXG_ERR_INVALID_ARGUMENT, "bad FastLanes width");
     case Epi::AlpF32:
     case Epi::AlpF64:
-        return fl_alp(T, W, epi, a, s);
+        return fl_alp(T, W, epi, t, g, s);
     case Epi::Dict:
         if (W > kDictFusedMaxW) return VXG_ERR_NOT_IMPLEMENTED;
         switch (vw) {
-        case 1: return fl_dict_1(T, W, a, s);
-        case 2: return fl_dict_2(T, W, a, s);
-        case 4: return fl_dict_4(T, W, a, s);
-        case 8: return fl_dict_8(T, W, a, s);
-        case 16: return fl_dict_16(T, W, a, s);
+        case 1: return fl_dict_1(T, W, t, g, s);
+        case 2: return fl_dict_2(T, W, t, g, s);
+        case 4: return fl_dict_4(T, W, t, g, s);
+        case 8: return fl_dict_8(T, W, t, g, s);
+        case 16: return fl_dict_16(T, W, t, g, s);
         }
         return set_error(VXG_ERR_INVALID_ARGUMENT, "bad dictionary value width");
     }
     return VXG_ERR_INVALID_ARGUMENT;
-}
-
-vxg_status launch_fl_unpack_dict_chunks(int T, int W, int vw, const DictChunkTable& d, uint64_t g,
-                                        uint32_t* err, hipStream_t s) {
-    if (W > kDictFusedMaxW) return VXG_ERR_NOT_IMPLEMENTED;
-    switch (vw) {
-    case 1: return fl_dict_chunks_1(T, W, d, g, err, s);
-    case 2: return fl_dict_chunks_2(T, W, d, g, err, s);
-    case 4: return fl_dict_chunks_4(T, W, d, g, err, s);
-    case 8: return fl_dict_chunks_8(T, W, d, g, err, s);
-    case 16: return fl_dict_chunks_16(T, W, d, g, err, s);
-    }
-    return set_error(VXG_ERR_INVALID_ARGUMENT, "bad dictionary value width");
 }
 
 }  // namespace vxg
@@ -103,21 +91,45 @@ using namespace vxg;
 
 namespace {
 
-// Launch Dict(codes = BitPacked) chunks in batches of kArgChunks descriptors passed as the
-// kernel argument (no device table, no upload, no host synchronisation).
-vxg_status launch_chunk_batches(int T, int W, int vw, const std::vector<DictChunkDev>& chunks, uint32_t* err,
-                                hipStream_t s) {
-    for (size_t b = 0; b < chunks.size(); b += kArgChunks) {
-        DictChunkTable tab{};
+// One K1 decode (a whole BitPacked-rooted cascade of one array or one chunk) and the kernel
+// it needs.  Jobs with the same kernel share launches.
+struct K1Job {
+    int T, W;
+    Epi epi;
+    int vw;
+    ChunkDev d;
+};
+
+bool same_kernel(const K1Job& a, const K1Job& b) {
+    return a.T == b.T && a.W == b.W && a.epi == b.epi && a.vw == b.vw;
+}
+
+// Launch K1 jobs grouped by kernel (T, W, epilogue, value width), kArgChunks chunks per launch
+// with the chunk table as the kernel argument (no device table, no upload, no host sync).
+vxg_status launch_k1_jobs(std::vector<K1Job>& jobs, uint32_t* err, hipStream_t s) {
+    std::stable_sort(jobs.begin(), jobs.end(), [](const K1Job& a, const K1Job& b) {
+        return std::make_tuple(a.T, a.W, int(a.epi), a.vw) < std::make_tuple(b.T, b.W, int(b.epi), b.vw);
+    });
+    size_t i = 0;
+    while (i < jobs.size()) {
+        size_t j = i;
+        while (j < jobs.size() && j - i < size_t(kArgChunks) && same_kernel(jobs[i], jobs[j])) j++;
+        ChunkTable tab{};
+        tab.err = err;
         uint64_t groups = 0;
-        tab.n = uint32_t(std::min<size_t>(kArgChunks, chunks.size() - b));
-        for (uint32_t i = 0; i < tab.n; i++) {
-            tab.c[i] = chunks[b + i];
-            tab.c[i].first_group = groups;
-            groups += (tab.c[i].n_blocks + 31) / 32;
+        for (size_t k = i; k < j; k++) {
+            if (jobs[k].d.n_blocks == 0) continue;
+            ChunkDev& c = tab.c[tab.n++];
+            c = jobs[k].d;
+            c.first_group = groups;
+            groups += (c.n_blocks + 31) / 32;
         }
-        vxg_status st = launch_fl_unpack_dict_chunks(T, W, vw, tab, groups, err, s);
-        if (st != VXG_OK) return st;
+        if (groups > 0xFFFFFFFFull) return set_error(VXG_ERR_INVALID_ARGUMENT, "array too long for one launch");
+        if (tab.n) {
+            vxg_status st = launch_fl_unpack(jobs[i].T, jobs[i].W, jobs[i].epi, jobs[i].vw, tab, groups, s);
+            if (st != VXG_OK) return st;
+        }
+        i = j;
     }
     return VXG_OK;
 }
@@ -135,26 +147,46 @@ vxg_status use_device(vxg_ctx* ctx) {
     return hip_check(hipSetDevice(ctx->c.device), "hipSetDevice");
 }
 
-vxg_status bitunpack_common(vxg_ctx* ctx, int T, unsigned W, unsigned offset, uint64_t len,
-                            const void* packed, uint64_t packed_bytes, Epi epi, int vw,
-                            UnpackArgs a, void* out, void* stream) {
+// Validate one BitPacked buffer (bitpacking/mod.rs:54-130) and describe its K1 decode.
+vxg_status make_k1_job(int T, unsigned W, unsigned offset, uint64_t len, const void* packed, uint64_t packed_bytes,
+                       Epi epi, int vw, const UnpackArgs& a, void* out, K1Job& j) {
     if (offset > 1023) return set_error(VXG_ERR_INVALID_ARGUMENT, "Offset must be less than full block, i.e. 1024");
     if (W > unsigned(T)) return set_error(VXG_ERR_INVALID_ARGUMENT, "Unsupported bit width");
     const uint64_t nblk = (len + offset + 1023) / 1024;
     if (W > 0 && packed_bytes != nblk * 128ull * W)  // bitpacking/mod.rs:80-88
         return set_error(VXG_ERR_INVALID_ARGUMENT, "Expected " + std::to_string(nblk * 128ull * W) +
                                                        " packed bytes, got " + std::to_string(packed_bytes));
-    a.packed = static_cast<const uint8_t*>(packed);
-    a.out = out;
-    a.n_blocks = nblk;
-    a.offset = offset;
-    a.len = len;
-    a.err = ctx->c.err_word;
-    if (reinterpret_cast<uintptr_t>(out) & 15)
-        return set_error(VXG_ERR_INVALID_ARGUMENT, "output buffer must be 16-byte aligned");
     if (W > 0 && (reinterpret_cast<uintptr_t>(packed) & 15))
         return set_error(VXG_ERR_INVALID_ARGUMENT, "packed buffer must be 16-byte aligned");
-    return launch_fl_unpack(T, int(W), epi, vw, a, S(stream));
+    const int ow = epi == Epi::Dict ? vw : (epi == Epi::AlpF32 ? 4 : (epi == Epi::AlpF64 ? 8 : T / 8));
+    if (reinterpret_cast<uintptr_t>(out) % uint64_t(ow))
+        return set_error(VXG_ERR_INVALID_ARGUMENT, "output buffer must be aligned to the value width");
+    if (epi == Epi::Dict && W > unsigned(kDictFusedMaxW)) return VXG_ERR_NOT_IMPLEMENTED;
+    j.T = T;
+    j.W = int(W);
+    j.epi = epi;
+    j.vw = epi == Epi::Dict ? vw : 0;
+    j.d = ChunkDev{};
+    j.d.packed = static_cast<const uint8_t*>(packed);
+    j.d.out = out;
+    j.d.n_blocks = len ? nblk : 0;
+    j.d.len = len;
+    j.d.reference = a.reference;
+    j.d.alp_a = a.alp_a;
+    j.d.alp_b = a.alp_b;
+    j.d.dict = a.dict;
+    j.d.dict_len = a.dict_len;
+    j.d.offset = offset;
+    j.d.shift = a.shift;
+    return VXG_OK;
+}
+
+vxg_status bitunpack_common(vxg_ctx* ctx, int T, unsigned W, unsigned offset, uint64_t len,
+                            const void* packed, uint64_t packed_bytes, Epi epi, int vw,
+                            UnpackArgs a, void* out, void* stream) {
+    std::vector<K1Job> jobs(1);
+    VXG_TRY(make_k1_job(T, W, offset, len, packed, packed_bytes, epi, vw, a, out, jobs[0]));
+    return launch_k1_jobs(jobs, ctx->c.err_word, S(stream));
 }
 
 // ===================================================================================
@@ -174,6 +206,20 @@ class Planner {
     vxg_ctx* ctx_;
     hipStream_t s_;
     std::vector<void*> temps_;
+    // Deferred K1 decodes of the chunks of a ChunkedArray (grouped into shared launches) and
+    // the patch scatters that must follow them; null = launch immediately.
+    struct PatchJob {
+        const vxg_array* sp;
+        int T;
+        Epi epi;
+        int vw;
+        UnpackArgs a;
+        void* dst;
+        uint64_t out_len;
+    };
+    std::vector<K1Job>* k1_batch_ = nullptr;
+    std::vector<PatchJob>* patch_batch_ = nullptr;
+    bool k1_fusable(const vxg_array& c) const;
 
     vxg_status temp(uint64_t bytes, void** p) {
         if (bytes == 0) bytes = 16;
@@ -287,13 +333,22 @@ vxg_status Planner::decode_bitpacked(const vxg_array& bp, Epi epi, int vw, Unpac
     const vxg_buffer* packed = buf(bp, 0);
     const unsigned W = bp.meta.bitpacked.bit_width;
     a.err = ctx_->c.err_word;
-    VXG_TRY(bitunpack_common(ctx_, T, W, bp.meta.bitpacked.offset, bp.len, packed ? packed->ptr : nullptr,
-                             packed ? packed->len : 0, epi, vw, a, dst, s_));
+    K1Job j;
+    VXG_TRY(make_k1_job(T, W, bp.meta.bitpacked.offset, bp.len, packed ? packed->ptr : nullptr,
+                        packed ? packed->len : 0, epi, vw, a, dst, j));
+    const vxg_array* p = nullptr;
     if (bp.meta.bitpacked.has_patches) {
-        const vxg_array* p = child(bp, 0);
+        p = child(bp, 0);
         if (!p) return set_error(VXG_ERR_INVALID_ARGUMENT, "BitPackedArray: patches child missing");
-        VXG_TRY(apply_sparse_patches(*p, T, epi, vw, a, dst, bp.len));
     }
+    if (k1_batch_) {  // a chunk of a ChunkedArray: launched with the other chunks
+        k1_batch_->push_back(j);
+        if (p) patch_batch_->push_back(PatchJob{p, T, epi, vw, a, dst, bp.len});
+        return VXG_OK;
+    }
+    std::vector<K1Job> one{j};
+    VXG_TRY(launch_k1_jobs(one, ctx_->c.err_word, s_));
+    if (p) VXG_TRY(apply_sparse_patches(*p, T, epi, vw, a, dst, bp.len));
     return VXG_OK;
 }
 
@@ -331,6 +386,10 @@ vxg_status Planner::decode_alp(const vxg_array& a, void* dst) {
         if (!p) return set_error(VXG_ERR_INVALID_ARGUMENT, "ALPArray: patches child missing");
         UnpackArgs plain{};
         plain.err = ctx_->c.err_word;
+        if (patch_batch_) {  // after the chunk's K1 decode and its inner patches
+            patch_batch_->push_back(PatchJob{p, f32 ? 32 : 64, Epi::Plain, 0, plain, dst, a.len});
+            return VXG_OK;
+        }
         VXG_TRY(apply_sparse_patches(*p, f32 ? 32 : 64, Epi::Plain, 0, plain, dst, a.len));
     }
     return VXG_OK;
@@ -357,52 +416,58 @@ vxg_status Planner::decode_dict_primitive(const vxg_array& a, void* dst) {
     return launch_take(vw, pv, values->len, width(*codes), pc, a.len, dst, ctx_->c.err_word, s_);
 }
 
+// Chunks whose whole decode is one K1 launch (+ patch scatters): BitPacked, FoR/ZigZag/ALP over
+// BitPacked of the same width, Dict(Primitive values, BitPacked codes).  Their decodes are
+// deferred and grouped across chunks; nothing in them reads another deferred output.
+bool Planner::k1_fusable(const vxg_array& c) const {
+    auto bp_of_width = [&](const vxg_array* x, int w) {
+        return x && x->encoding == VXG_ENC_FL_BITPACKED && width(*x) == w && ptype_is_int(x->ptype);
+    };
+    const int w = width(c);
+    switch (c.encoding) {
+    case VXG_ENC_FL_BITPACKED: return ptype_is_int(c.ptype);
+    case VXG_ENC_FL_FOR: return ptype_is_int(c.ptype) && bp_of_width(child(c, 0), w);
+    case VXG_ENC_ZIGZAG: return ptype_is_signed(c.ptype) && bp_of_width(child(c, 0), w);
+    case VXG_ENC_ALP: {
+        if (c.ptype != VXG_F32 && c.ptype != VXG_F64) return false;
+        const vxg_array* e = child(c, 0);
+        if (e && e->encoding == VXG_ENC_FL_FOR) e = child(*e, 0);
+        return bp_of_width(e, w);
+    }
+    case VXG_ENC_DICT: {
+        const vxg_array* v = child(c, 0);
+        const vxg_array* k = child(c, 1);
+        return v && k && v->encoding == VXG_ENC_PRIMITIVE && k->encoding == VXG_ENC_FL_BITPACKED &&
+               ptype_is_unsigned(k->ptype) && !k->nullable && k->meta.bitpacked.bit_width <= kDictFusedMaxW;
+    }
+    default: return false;
+    }
+}
+
 vxg_status Planner::decode_chunked_primitive(const vxg_array& a, void* dst) {
-    // chunked/canonical.rs:27-122 / pack_primitives :170-187 -- each chunk decodes straight
-    // into its slice of the output (no per-chunk materialisation + memcpy).
+    // chunked/canonical.rs:27-122 / pack_primitives :170-187 -- every chunk decodes straight
+    // into its slice of the output (no per-chunk materialisation + memcpy).  Chunks that are
+    // one K1 decode share launches (chunk tables of up to kArgChunks per kernel); the others
+    // decode one by one.
     const uint64_t n = a.meta.chunked.nchunks;
     if (a.n_children != n + 1) return set_error(VXG_ERR_INVALID_ARGUMENT, "Chunked child count != nchunks + 1");
     const int w = width(a);
-    // Fast path: every chunk is Dict(codes = BitPacked, no patches, offset 0, same T/W/VW) ->
-    // one grouped launch over all chunks.
-    bool grouped = n > 1;
-    int T = 0, W = -1, vw = 0;
-    for (uint64_t i = 0; i < n && grouped; i++) {
-        const vxg_array& c = a.children[i + 1];
-        const vxg_array* codes = child(c, 1);
-        const vxg_array* values = child(c, 0);
-        if (c.encoding != VXG_ENC_DICT || !codes || !values || codes->encoding != VXG_ENC_FL_BITPACKED ||
-            codes->meta.bitpacked.has_patches || codes->meta.bitpacked.offset != 0 ||
-            codes->meta.bitpacked.bit_width > kDictFusedMaxW || values->encoding != VXG_ENC_PRIMITIVE) {
-            grouped = false;
-            break;
-        }
-        const int t = 8 * width(*codes), ww = codes->meta.bitpacked.bit_width, v = width(*values);
-        if (i == 0) { T = t; W = ww; vw = v; }
-        else if (t != T || ww != W || v != vw) grouped = false;
-    }
+    std::vector<K1Job> jobs;
+    std::vector<PatchJob> patches;
     uint64_t off = 0;
-    if (grouped) {
-        std::vector<DictChunkDev> h(n);
-        for (uint64_t i = 0; i < n && grouped; i++) {
-            const vxg_array& c = a.children[i + 1];
-            const vxg_array& codes = *child(c, 1);
-            const vxg_array& values = *child(c, 0);
-            const uint64_t nblk = (c.len + 1023) / 1024;
-            if (W > 0 && codes.buffers[0].len != nblk * 128ull * W)
-                return set_error(VXG_ERR_INVALID_ARGUMENT, "Chunk packed length mismatch");
-            if (((off * w) & 15) != 0) grouped = false;  // 16-B vector stores need aligned slices
-            h[i] = DictChunkDev{static_cast<const uint8_t*>(codes.buffers[0].ptr), values.buffers[0].ptr,
-                                static_cast<uint8_t*>(dst) + off * w, nblk, c.len, values.len, 0};
-            off += c.len;
-        }
-        if (grouped) return launch_chunk_batches(T, W, vw, h, ctx_->c.err_word, s_);
-        off = 0;
-    }
     for (uint64_t i = 0; i < n; i++) {
         const vxg_array& c = a.children[i + 1];
+        if (c.ptype != a.ptype || c.dtype != a.dtype)
+            return set_error(VXG_ERR_MISMATCHED_TYPES, "Chunks must have the ChunkedArray's dtype");
         uint8_t* slice = static_cast<uint8_t*>(dst) + off * w;
-        if ((reinterpret_cast<uintptr_t>(slice) & 15) == 0) {
+        if (k1_fusable(c)) {
+            k1_batch_ = &jobs;
+            patch_batch_ = &patches;
+            const vxg_status st = decode_into(c, slice);
+            k1_batch_ = nullptr;
+            patch_batch_ = nullptr;
+            VXG_TRY(st);
+        } else if ((reinterpret_cast<uintptr_t>(slice) & 15) == 0) {
             VXG_TRY(decode_into(c, slice));
         } else {
             const void* p;
@@ -412,6 +477,8 @@ vxg_status Planner::decode_chunked_primitive(const vxg_array& a, void* dst) {
         off += c.len;
     }
     if (off != a.len) return set_error(VXG_ERR_INVALID_ARGUMENT, "Chunked len != sum of chunk lens");
+    VXG_TRY(launch_k1_jobs(jobs, ctx_->c.err_word, s_));
+    for (const PatchJob& p : patches) VXG_TRY(apply_sparse_patches(*p.sp, p.T, p.epi, p.vw, p.a, p.dst, p.out_len));
     return VXG_OK;
 }
 
@@ -930,18 +997,18 @@ vxg_status vxg_bitunpack_dict_chunks(vxg_ctx* ctx, int codes_ptype, unsigned bit
     if (!ptype_is_unsigned(codes_ptype)) return set_error(VXG_ERR_MISMATCHED_TYPES, "Dict codes must be unsigned");
     if (bit_width > unsigned(kDictFusedMaxW))
         return set_error(VXG_ERR_NOT_IMPLEMENTED, "fused dict decode supports code widths <= 16");
-    std::vector<DictChunkDev> h(n_chunks);
+    std::vector<K1Job> jobs(n_chunks);
     for (uint32_t i = 0; i < n_chunks; i++) {
         const vxg_dict_chunk& c = chunks_host[i];
         if (c.n_blocks != (c.len + 1023) / 1024)
             return set_error(VXG_ERR_INVALID_ARGUMENT, "chunk n_blocks != ceil(len/1024)");
-        if ((reinterpret_cast<uintptr_t>(c.out) | reinterpret_cast<uintptr_t>(c.packed)) & 15)
-            return set_error(VXG_ERR_INVALID_ARGUMENT, "chunk buffers must be 16-byte aligned");
-        h[i] = DictChunkDev{static_cast<const uint8_t*>(c.packed), c.dict_values, c.out, c.n_blocks, c.len,
-                            c.dict_len, 0};
+        UnpackArgs a{};
+        a.dict = c.dict_values;
+        a.dict_len = c.dict_len;
+        VXG_TRY(make_k1_job(unsigned_T(codes_ptype), bit_width, 0, c.len, c.packed, c.n_blocks * 128ull * bit_width,
+                            Epi::Dict, int(value_width), a, c.out, jobs[i]));
     }
-    return launch_chunk_batches(unsigned_T(codes_ptype), int(bit_width), int(value_width), h, ctx->c.err_word,
-                                S(stream));
+    return launch_k1_jobs(jobs, ctx->c.err_word, S(stream));
 }
 
 vxg_status vxg_patch(vxg_ctx* ctx, int ptype, void* out, uint64_t out_len, int indices_ptype, const void* indices,

@@ -127,6 +127,18 @@ struct EpiParams {
     uint32_t* err;
 };
 
+inline EpiParams to_epi(const UnpackArgs& a) {
+    EpiParams ep;
+    ep.reference = a.reference;
+    ep.shift = a.shift;
+    ep.alp_a = a.alp_a;
+    ep.alp_b = a.alp_b;
+    ep.dict = a.dict;
+    ep.dict_len = a.dict_len;
+    ep.err = a.err;
+    return ep;
+}
+
 template <int T, Epi EPI, int VW> struct EpiOut {
     using type = typename Fl<T>::E;
 };
@@ -287,129 +299,78 @@ __device__ __forceinline__ void stage_dict(uint8_t* s_dict, const void* dict, ui
     __syncthreads();
 }
 
+// One launch decodes up to kArgChunks independent arrays ("chunks": a single array, or the
+// chunks of a ChunkedArray written straight into their output slices -- chunked/canonical.rs:
+// 170-187 without the pack copy).  The chunk table travels as the kernel argument (no upload,
+// no host synchronisation); each workgroup of 256 threads covers 32 FastLanes blocks of exactly
+// one chunk, found by a workgroup-uniform binary search on first_group (no search for n = 1).
 template <int T, int W, Epi EPI, int VW, bool LDSD = false>
-__global__ __launch_bounds__(256) void fl_unpack_kernel(const uint8_t* __restrict__ packed,
-                                                        void* __restrict__ out_v, uint64_t n_blocks,
-                                                        uint32_t offset, uint64_t len,
-                                                        EpiParams ep) {
+__global__ __launch_bounds__(256) void fl_unpack_kernel(ChunkTable tab) {
     using O = typename EpiOut<T, EPI, VW>::type;
-    const uint64_t gid = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    const uint64_t blk = gid >> 3;
-    const int t = int(gid & 7);
-    if constexpr (LDSD) {
-        __shared__ __attribute__((aligned(16))) uint8_t s_dict[kDictLdsBytes];
-        stage_dict<VW>(s_dict, ep.dict, ep.dict_len);
-        ep.dict = s_dict;
-    }
-    if (blk >= n_blocks) return;
-    const int64_t out_base = int64_t(blk * 1024) - int64_t(offset);
-    const bool full = offset == 0 && (blk + 1) * 1024 <= len;
-    // Decoded output is written once and never re-read by this launch: non-temporal 16-byte
-    // stores (measured on C1: 51.1 us vs 63.0 us with plain stores = 80% vs 65% of 8 TB/s,
-    // profiles/r01_ubench_k1.txt; a perfectly coalesced copy of the same bytes: 49.2 us).
-    unpack_block<T, W, EPI, VW, kOutNT>(packed + blk * (128 * W), t, static_cast<O*>(out_v), out_base,
-                                full, len, ep);
-}
-
-// Many independent chunks (e.g. Chunked[Dict(BitPacked)]) in one launch; each workgroup of
-// 256 threads covers 32 blocks of exactly one chunk.
-template <int T, int W, Epi EPI, int VW, bool LDSD = false>
-__global__ __launch_bounds__(256) void fl_unpack_chunks_kernel(DictChunkTable tab, EpiParams ep0) {
-    using O = typename EpiOut<T, EPI, VW>::type;
-    // the chunk table is a kernel argument (no upload, no host sync); workgroup-uniform
-    // binary search on first_group
     uint32_t lo = 0, hi = tab.n;
     const uint64_t g = blockIdx.x;
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
         if (tab.c[mid].first_group <= g) lo = mid; else hi = mid;
     }
-    const DictChunkDev c = tab.c[lo];
+    const ChunkDev& c = tab.c[lo];
     const uint64_t blk = (g - c.first_group) * 32 + (threadIdx.x >> 3);
     const int t = int(threadIdx.x & 7);
-    EpiParams ep = ep0;
+    EpiParams ep;
+    ep.reference = c.reference;
+    ep.shift = c.shift;
+    ep.alp_a = c.alp_a;
+    ep.alp_b = c.alp_b;
     ep.dict = c.dict;
     ep.dict_len = c.dict_len;
+    ep.err = tab.err;
     if constexpr (LDSD) {  // the whole workgroup is in chunk `lo`
         __shared__ __attribute__((aligned(16))) uint8_t s_dict[kDictLdsBytes];
         stage_dict<VW>(s_dict, c.dict, c.dict_len);
         ep.dict = s_dict;
     }
     if (blk >= c.n_blocks) return;
-    const bool full = (blk + 1) * 1024 <= c.len;
-    unpack_block<T, W, EPI, VW, kOutNT>(c.packed + blk * (128 * W), t, static_cast<O*>(c.out),
-                                        int64_t(blk * 1024), full, c.len, ep);
-}
-
-inline EpiParams to_epi(const UnpackArgs& a) {
-    EpiParams ep;
-    ep.reference = a.reference;
-    ep.shift = a.shift;
-    ep.alp_a = a.alp_a;
-    ep.alp_b = a.alp_b;
-    ep.dict = a.dict;
-    ep.dict_len = a.dict_len;
-    ep.err = a.err;
-    return ep;
+    const int64_t out_base = int64_t(blk * 1024) - int64_t(c.offset);
+    // full: straight-line 16-byte stores (block inside [0, len), 16-byte aligned slice)
+    const bool full =
+        c.offset == 0 && (blk + 1) * 1024 <= c.len && (reinterpret_cast<uintptr_t>(c.out) & 15) == 0;
+    // Decoded output is written once and never re-read by this launch: non-temporal 16-byte
+    // stores (measured on C1: 51.1 us vs 63.0 us with plain stores = 80% vs 65% of 8 TB/s,
+    // profiles/r01_ubench_k1.txt; a perfectly coalesced copy of the same bytes: 49.2 us).
+    unpack_block<T, W, EPI, VW, kOutNT>(c.packed + blk * (128 * W), t, static_cast<O*>(c.out), out_base, full,
+                                        c.len, ep);
 }
 
 template <int T, int W, Epi EPI, int VW>
-vxg_status launch_one(const UnpackArgs& a, hipStream_t s) {
-    if (a.n_blocks == 0) return VXG_OK;
-    const uint64_t threads = a.n_blocks * 8;
-    const uint64_t grid = (threads + 255) / 256;
+vxg_status launch_one(const ChunkTable& tab, uint64_t groups, hipStream_t s) {
+    if (groups == 0) return VXG_OK;
     if constexpr (EPI == Epi::Dict) {
-        if (a.dict_len * VW <= uint64_t(kDictLdsBytes) && (reinterpret_cast<uintptr_t>(a.dict) & 15) == 0) {
-            hipLaunchKernelGGL((fl_unpack_kernel<T, W, EPI, VW, true>), dim3(unsigned(grid)), dim3(256), 0, s,
-                               a.packed, a.out, a.n_blocks, a.offset, a.len, to_epi(a));
+        bool lds = true;
+        for (uint32_t k = 0; k < tab.n; k++)
+            lds = lds && tab.c[k].dict_len * VW <= uint64_t(kDictLdsBytes) &&
+                  (reinterpret_cast<uintptr_t>(tab.c[k].dict) & 15) == 0;
+        if (lds) {
+            hipLaunchKernelGGL((fl_unpack_kernel<T, W, EPI, VW, true>), dim3(unsigned(groups)), dim3(256), 0, s, tab);
             return hip_check(hipGetLastError(), "fl_unpack_kernel launch");
         }
     }
-    hipLaunchKernelGGL((fl_unpack_kernel<T, W, EPI, VW>), dim3(unsigned(grid)), dim3(256), 0, s,
-                       a.packed, a.out, a.n_blocks, a.offset, a.len, to_epi(a));
+    hipLaunchKernelGGL((fl_unpack_kernel<T, W, EPI, VW>), dim3(unsigned(groups)), dim3(256), 0, s, tab);
     return hip_check(hipGetLastError(), "fl_unpack_kernel launch");
-}
-
-template <int T, int W, Epi EPI, int VW>
-vxg_status launch_chunks_one(const DictChunkTable& tab, uint64_t total_groups, uint32_t* err, hipStream_t s) {
-    if (total_groups == 0) return VXG_OK;
-    EpiParams ep{};
-    ep.err = err;
-    bool lds = true;
-    for (uint32_t k = 0; k < tab.n; k++)
-        lds = lds && tab.c[k].dict_len * VW <= uint64_t(kDictLdsBytes) &&
-              (reinterpret_cast<uintptr_t>(tab.c[k].dict) & 15) == 0;
-    if (lds)
-        hipLaunchKernelGGL((fl_unpack_chunks_kernel<T, W, EPI, VW, true>), dim3(unsigned(total_groups)),
-                           dim3(256), 0, s, tab, ep);
-    else
-        hipLaunchKernelGGL((fl_unpack_chunks_kernel<T, W, EPI, VW>), dim3(unsigned(total_groups)),
-                           dim3(256), 0, s, tab, ep);
-    return hip_check(hipGetLastError(), "fl_unpack_chunks_kernel launch");
 }
 
 // Function-pointer table over W = 0..WMAX.
 template <int T, Epi EPI, int VW, int... Ws>
-vxg_status dispatch_w_impl(int W, const UnpackArgs& a, hipStream_t s,
+vxg_status dispatch_w_impl(int W, const ChunkTable& tab, uint64_t groups, hipStream_t s,
                            std::integer_sequence<int, Ws...>) {
-    using Fn = vxg_status (*)(const UnpackArgs&, hipStream_t);
+    using Fn = vxg_status (*)(const ChunkTable&, uint64_t, hipStream_t);
     static constexpr Fn table[] = {&launch_one<T, Ws, EPI, VW>...};
     if (W < 0 || W >= int(sizeof...(Ws))) return VXG_ERR_NOT_IMPLEMENTED;
-    return table[W](a, s);
+    return table[W](tab, groups, s);
 }
 
 template <int T, Epi EPI, int VW, int WMAX>
-vxg_status dispatch_w(int W, const UnpackArgs& a, hipStream_t s) {
-    return dispatch_w_impl<T, EPI, VW>(W, a, s, std::make_integer_sequence<int, WMAX + 1>{});
-}
-
-template <int T, Epi EPI, int VW, int... Ws>
-vxg_status dispatch_chunks_w_impl(int W, const DictChunkTable& tab, uint64_t g, uint32_t* err,
-                                  hipStream_t s, std::integer_sequence<int, Ws...>) {
-    using Fn = vxg_status (*)(const DictChunkTable&, uint64_t, uint32_t*, hipStream_t);
-    static constexpr Fn table[] = {&launch_chunks_one<T, Ws, EPI, VW>...};
-    if (W < 0 || W >= int(sizeof...(Ws))) return VXG_ERR_NOT_IMPLEMENTED;
-    return table[W](tab, g, err, s);
+vxg_status dispatch_w(int W, const ChunkTable& tab, uint64_t groups, hipStream_t s) {
+    return dispatch_w_impl<T, EPI, VW>(W, tab, groups, s, std::make_integer_sequence<int, WMAX + 1>{});
 }
 
 }  // namespace vxg

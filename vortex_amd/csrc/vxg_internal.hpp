@@ -82,27 +82,33 @@ struct UnpackArgs {
     uint32_t* err;
 };
 
-// T in {8,16,32,64} bits; value_width only used for Epi::Dict.
-vxg_status launch_fl_unpack(int T, int W, Epi epi, int value_width, const UnpackArgs& a,
-                            hipStream_t s);
-
-struct DictChunkDev {
+// One K1 "chunk": an independent BitPacked array (a whole array, or one chunk of a
+// ChunkedArray decoded straight into its output slice) with its fused epilogue parameters.
+struct ChunkDev {
     const uint8_t* packed;
-    const void* dict;
-    void* out;
-    uint64_t n_blocks;
-    uint64_t len;
+    void* out;              // output of packed position `offset` (values [0, len))
+    uint64_t n_blocks;      // FastLanes blocks covered (ceil((len + offset) / 1024))
+    uint64_t len;           // values to write
+    uint64_t first_group;   // first 32-block workgroup of this chunk in the launch
+    uint64_t reference;     // FoR reference bits
+    double alp_a, alp_b;    // ALP F10[f], IF10[e] (f32 tables converted exactly)
+    const void* dict;       // Dict values
     uint64_t dict_len;
-    uint64_t first_group;  // first 32-block workgroup index of this chunk
+    uint32_t offset;        // values to skip in block 0 (< 1024)
+    uint32_t shift;         // FoR shift
 };
-// Up to kArgChunks chunk descriptors travel as a kernel argument (1.8 KB kernarg).
+// Up to kArgChunks descriptors travel as the kernel argument (~2.8 KB kernarg).
 constexpr int kArgChunks = 32;
-struct DictChunkTable {
-    DictChunkDev c[kArgChunks];
+struct ChunkTable {
+    ChunkDev c[kArgChunks];
     uint32_t n;
+    uint32_t* err;
 };
-vxg_status launch_fl_unpack_dict_chunks(int T, int W, int value_width, const DictChunkTable& tab,
-                                        uint64_t total_groups, uint32_t* err, hipStream_t s);
+
+// T in {8,16,32,64} bits; value_width only used for Epi::Dict.  `groups` = total 32-block
+// workgroups of the table (first_group filled in).
+vxg_status launch_fl_unpack(int T, int W, Epi epi, int value_width, const ChunkTable& tab, uint64_t groups,
+                            hipStream_t s);
 
 // An integer column a consumer kernel (FSST, patch scatter) reads in place: a plain array of `width`-byte integers,
 // or a patch-free [FoR](BitPacked) column of T = 8*width bits (T = 32/64) whose elements are
@@ -139,15 +145,12 @@ vxg_status launch_set_bits_at(void* dst, const void* idx, int iw, bool isg, uint
                               uint64_t len, hipStream_t s);
 vxg_status launch_sum(const void* p, int w, bool sg, uint64_t n, void* out_u64, hipStream_t s);
 // K1 instantiation units (fl_inst.hip)
-vxg_status fl_plain_8(int W, Epi epi, const UnpackArgs& a, hipStream_t s);
-vxg_status fl_plain_16(int W, Epi epi, const UnpackArgs& a, hipStream_t s);
-vxg_status fl_plain_32(int W, Epi epi, const UnpackArgs& a, hipStream_t s);
-vxg_status fl_plain_64(int W, Epi epi, const UnpackArgs& a, hipStream_t s);
-vxg_status fl_alp(int T, int W, Epi epi, const UnpackArgs& a, hipStream_t s);
-#define VXG_DECL_DICT(VW)                                                                          \
-    vxg_status fl_dict_##VW(int T, int W, const UnpackArgs& a, hipStream_t s);                     \
-    vxg_status fl_dict_chunks_##VW(int T, int W, const DictChunkTable& d, uint64_t g,              \
-                                   uint32_t* err, hipStream_t s);
+vxg_status fl_plain_8(int W, Epi epi, const ChunkTable& t, uint64_t g, hipStream_t s);
+vxg_status fl_plain_16(int W, Epi epi, const ChunkTable& t, uint64_t g, hipStream_t s);
+vxg_status fl_plain_32(int W, Epi epi, const ChunkTable& t, uint64_t g, hipStream_t s);
+vxg_status fl_plain_64(int W, Epi epi, const ChunkTable& t, uint64_t g, hipStream_t s);
+vxg_status fl_alp(int T, int W, Epi epi, const ChunkTable& t, uint64_t g, hipStream_t s);
+#define VXG_DECL_DICT(VW) vxg_status fl_dict_##VW(int T, int W, const ChunkTable& t, uint64_t g, hipStream_t s);
 VXG_DECL_DICT(1)
 VXG_DECL_DICT(2)
 VXG_DECL_DICT(4)
