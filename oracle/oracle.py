@@ -40,6 +40,7 @@ _SIG = {
     "vxo_fsst_decompress": (SZ, [VP, VP, VP, SZ, VP]),
     "vxo_fsst_canonicalize": (INT, [VP, VP, VP, INT, VP, INT, VP, SZ, VP, VP, C.POINTER(SZ), VP]),
     "vxo_make_views": (None, [VP, VP, SZ, VP, C.c_uint32, VP]),
+    "vxo_rebase_views": (None, [VP, SZ, C.c_uint32]),
 }
 
 _lib = None

@@ -460,3 +460,17 @@ int vxo_fsst_canonicalize(const uint64_t* symbols, const uint8_t* sym_lens,
     *heap_len = hl;
     return 0;
 }
+
+void vxo_rebase_views(uint8_t* views, size_t n, uint32_t buffers_offset) {
+    /* chunked/canonical.rs:214-231: view.is_inlined() (len <= 12) -> copied as is, else
+     * BinaryView::new_view(len, prefix, buffers_offset + buffer_index, offset) */
+    for (size_t i = 0; i < n; i++) {
+        uint8_t* v = views + 16 * i;
+        uint32_t len, bi;
+        memcpy(&len, v, 4);
+        if (len <= 12) continue;
+        memcpy(&bi, v + 8, 4);
+        bi += buffers_offset;
+        memcpy(v + 8, &bi, 4);
+    }
+}

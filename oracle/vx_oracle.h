@@ -120,6 +120,10 @@ int vxo_fsst_canonicalize(const uint64_t* symbols, const uint8_t* sym_lens,
 void vxo_make_views(const uint8_t* heap, const int64_t* offsets, size_t n,
                     const uint8_t* validity, uint32_t buffer_index, uint8_t* views);
 
+/* pack_views (array/chunked/canonical.rs:214-231): add `buffers_offset` to the buffer_index
+ * of every non-inlined view (len > 12); inlined views are left unchanged. */
+void vxo_rebase_views(uint8_t* views, size_t n, uint32_t buffers_offset);
+
 #ifdef __cplusplus
 }
 #endif

@@ -47,6 +47,8 @@ def _validity(a: Array):
         return from_meta(1 if a.meta["has_patches"] else 0)
     if e in (ENC["FL_DELTA"], ENC["RUN_END"], ENC["VARBIN"]):
         return from_meta(2)
+    if e == ENC["VARBINVIEW"]:
+        return from_meta(1 + a.meta["n_buffers"])
     if e in (ENC["FL_FOR"], ENC["ZIGZAG"], ENC["ALP"], ENC["ALP_RD"]):
         return _validity(a.children[0])
     if e == ENC["FSST"]:
@@ -217,18 +219,38 @@ def _canon_string(a: Array):
         if rc:
             raise ValueError("fsst canonicalize: decoded length mismatch")
         return views, heap[: hl.value]
+    if e == ENC["VARBINVIEW"]:
+        # already canonical: views + data buffers (varbinview/mod.rs:217-262)
+        views = np.ascontiguousarray(canon(a.children[0])[0]).astype(np.uint8).reshape(-1, 16).copy()
+        bufs = [np.ascontiguousarray(canon(c)[0]).astype(np.uint8) for c in a.children[1: 1 + a.meta["n_buffers"]]]
+        return views, bufs
     if e == ENC["DICT"]:
         (vviews, vheap), _ = canon(a.children[0])
         codes = canon(a.children[1])[0].astype(np.int64)
         return vviews[codes], vheap
+    if e == ENC["CHUNKED"]:
+        # pack_views (chunked/canonical.rs:194-236): buffers concatenated in chunk order, each
+        # chunk's non-inlined views rebased by the number of buffers before it
+        all_views, bufs = [], []
+        for c in a.children[1:]:
+            (v, b), _ = canon(c)
+            b = b if isinstance(b, list) else [b]
+            v = np.ascontiguousarray(v).copy()
+            L.vxo_rebase_views(O.p(v), v.shape[0], len(bufs))
+            all_views.append(v)
+            bufs.extend(b)
+        return (np.concatenate(all_views) if all_views else np.zeros((0, 16), np.uint8)), bufs
     raise NotImplementedError(f"oracle string canonicalize for encoding {e}")
 
 
-def view_bytes(views: np.ndarray, heap: np.ndarray, i: int):
-    """Logical string of view i (None-safe caller) — Appendix C decoding."""
+def view_bytes(views: np.ndarray, heap, i: int):
+    """Logical string of view i (None-safe caller) — Appendix C decoding.  `heap` is the data
+    buffer, or the list of data buffers indexed by the view's buffer_index."""
     v = views[i]
     n = int(np.frombuffer(v[:4].tobytes(), dtype=np.uint32)[0])
     if n <= 12:
         return v[4: 4 + n].tobytes()
+    bi = int(np.frombuffer(v[8:12].tobytes(), dtype=np.uint32)[0])
     off = int(np.frombuffer(v[12:16].tobytes(), dtype=np.uint32)[0])
-    return heap[off: off + n].tobytes()
+    buf = heap[bi] if isinstance(heap, list) else heap
+    return buf[off: off + n].tobytes()

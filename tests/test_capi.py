@@ -30,7 +30,7 @@ def test_gpu_lib_exports_match_header():
     lib = L.gpu_lib()  # loads (HIP runtime present in the image; no device needed)
     for name in decl:
         assert hasattr(lib, name)
-    assert lib.vxg_abi_version() == 1
+    assert lib.vxg_abi_version() == L.ABI_VERSION
 
 
 def test_enc_lib_exports_match_header():
@@ -45,7 +45,9 @@ def test_struct_layouts_match_c(tmp_path):
     fields = {"vxg_array": (L.VxgArray, ["encoding", "len", "meta", "n_buffers", "n_children", "buffers",
                                          "children"]),
               "vxg_canonical": (L.VxgCanonical, ["kind", "len", "values", "views", "data", "data_bytes",
-                                                 "validity"]),
+                                                 "validity", "n_data_buffers", "data_buffers_cap",
+                                                 "data_buffers"]),
+              "vxg_data_buffer": (L.VxgDataBuffer, ["offset", "len"]),
               "vxg_dict_chunk": (L.VxgDictChunk, ["packed", "out", "n_blocks", "dict_len"])}
     src = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{ROOT}/include/vortex_gpu.h"', "int main(){",
            'printf("vxg_meta %zu\\n", sizeof(vxg_meta));']

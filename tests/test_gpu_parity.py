@@ -44,9 +44,13 @@ def assert_primitive_parity(arr, ctx, expect=None):
 
 def assert_string_parity(arr, ctx, strings=None):
     res = gpu(arr, ctx)
-    views, heap = res.numpy()
+    views, _ = res.numpy()
+    heap = res.buffers()
     (rviews, rheap), rvalid = canon(arr)
-    assert heap.tobytes() == rheap.tobytes()
+    rheap = rheap if isinstance(rheap, list) else [rheap]
+    assert len(heap) == len(rheap)
+    for g, r in zip(heap, rheap):
+        assert g.tobytes() == r.tobytes()
     assert views.tobytes() == rviews.tobytes()
     gvalid = res.validity_mask()
     if rvalid is None:
@@ -360,6 +364,51 @@ def _fsst_handmade(strings, symbols):
                        utf8=False, validity=None if valid.all() else valid)
     return A.fsst(A.primitive(sym_u64), A.primitive(np.array([len(y) for y in syms], np.uint8)), code_vb,
                   A.primitive(np.array(lens, np.int32)))
+
+
+def _comment_strings(rng, n, vocab=40):
+    words = [bytes(rng.integers(97, 123, rng.integers(2, 10)).astype(np.uint8)) for _ in range(vocab)]
+    out = []
+    for _ in range(n):
+        k = int(rng.integers(1, 8))
+        out.append(b" ".join(words[j] for j in rng.integers(0, vocab, k))[: int(rng.integers(1, 44))])
+    return out
+
+
+@pytest.mark.parametrize("kind", ["fsst", "varbin", "dict", "varbinview", "mixed"])
+def test_chunked_strings_pack_views(ctx, kind):
+    """ChunkedArray of strings -> one VarBinView whose data buffers are the chunks' buffers in
+    order and whose non-inlined views carry the rebased buffer_index (pack_views,
+    chunked/canonical.rs:194-236); nulls in some chunks; FSST chunks have their own tables."""
+    rng = np.random.default_rng(len(kind))
+    chunks, strings = [], []
+    for c in range(9):
+        n = 3000 + 517 * c
+        ss = _comment_strings(rng, n, vocab=20 + c)
+        if c % 3 == 1:
+            for i in rng.choice(n, n // 10, replace=False):
+                ss[i] = None
+        k = kind if kind != "mixed" else ["fsst", "varbin", "dict", "varbinview"][c % 4]
+        if k == "fsst":
+            arr = E.encode_fsst(ss)
+        elif k == "varbin":
+            heap, offs, valid = E.strings_to_heap(ss)
+            arr = A.varbin(A.primitive(offs.astype(np.int64)), A.primitive(heap),
+                           validity=None if valid.all() else valid)
+        elif k == "dict":
+            ss = [s if s is not None else b"" for s in ss]  # dictionary values are non-null
+            uniq = sorted(set(ss))
+            pos = {s: i for i, s in enumerate(uniq)}
+            heap, offs, _ = E.strings_to_heap(uniq)
+            values = A.varbin(A.primitive(offs.astype(np.int32)), A.primitive(heap))
+            codes = np.array([pos[s] for s in ss], dtype=np.uint32)
+            arr = A.dict_array(values, E.encode_bitpacked(codes, allow_patches=False))
+        else:
+            arr = E.encode_varbinview(ss)
+        chunks.append(arr)
+        strings.extend(ss)
+    arr = A.chunked(chunks)
+    assert_string_parity(arr, ctx, strings)
 
 
 def test_fsst_escape_runs(ctx):

@@ -229,6 +229,24 @@ def test_kat_fsst_roundtrip():
     assert heap.tobytes() == b"".join(strings)
 
 
+def test_kat_pack_views_rebases_buffer_index():
+    """chunked/canonical.rs:254-273 (pack_sliced_varbin) with strings long enough to be
+    non-inlined: each chunk keeps its own buffer and its ref views' buffer_index is offset by
+    the number of buffers before it; inlined views are copied unchanged."""
+    words = [b"foo-foo-foo-foo", b"bar", b"baz-baz-baz-baz-baz", b"quak-quak-quak-quak"]
+    a1 = E.encode_varbinview(words)
+    a2 = E.encode_varbinview(list(reversed(words)))
+    arr = A.chunked([a1, a2])
+    (views, bufs), valid = canon(arr)
+    assert valid is None and len(bufs) == 2
+    got = [view_bytes(views, bufs, i) for i in range(8)]
+    assert got == words + list(reversed(words))
+    bidx = views[:, 8:12].copy().view(np.uint32).reshape(-1)
+    lens = views[:, :4].copy().view(np.uint32).reshape(-1)
+    assert bidx[lens > 12][:3].tolist() == [0, 0, 0] and bidx[lens > 12][3:].tolist() == [1, 1, 1]
+    assert not views[1, 8:].any() and not views[6, 8:].any()  # "bar" stays inlined
+
+
 def test_kat_views_inline_boundary():
     k = KATS["varbin_to_views_inline_boundary"]
     strings = [None if s is None else s.encode() for s in k["strings"]]

@@ -21,6 +21,7 @@ PTYPES = ["u8", "u16", "u32", "u64", "i8", "i16", "i32", "i64", "f16", "f32", "f
 PTYPE = {n: i for i, n in enumerate(PTYPES)}
 DTYPE = dict(NULL=0, BOOL=1, PRIMITIVE=2, UTF8=3, BINARY=4)
 VALIDITY = dict(NON_NULLABLE=0, ALL_VALID=1, ALL_INVALID=2, ARRAY=3)
+ABI_VERSION = 2  # VXG_ABI_VERSION
 STATUS = {0: "OK", 1: "OutOfBounds", 2: "ComputeError", 3: "InvalidArgument", 4: "InvalidSerde",
           5: "NotImplemented", 6: "MismatchedTypes", 7: "AssertionFailed", 8: "HipError",
           9: "OutOfMemory"}
@@ -95,11 +96,16 @@ class _MBool(C.Structure):
     _fields_ = [("first_byte_bit_offset", C.c_uint8)]
 
 
+class _MVarBinView(C.Structure):
+    _fields_ = [("n_buffers", C.c_uint32)]
+
+
 class VxgMeta(C.Union):
     _fields_ = [("bitpacked", _MBitPacked), ("for_", _MFoR), ("delta", _MDelta), ("alp", _MAlp),
                 ("alprd", _MAlpRd), ("dict", _MDict), ("fsst", _MFsst), ("runend", _MRunEnd),
                 ("sparse", _MSparse), ("constant", _MConstant), ("chunked", _MChunked),
-                ("varbin", _MVarBin), ("boolean", _MBool), ("raw", C.c_uint64 * 5)]
+                ("varbin", _MVarBin), ("boolean", _MBool), ("varbinview", _MVarBinView),
+                ("raw", C.c_uint64 * 5)]
 
 
 class VxgArray(C.Structure):
@@ -113,11 +119,17 @@ VxgArray._fields_ = [("encoding", C.c_uint16), ("dtype", C.c_uint8), ("ptype", C
                      ("children", C.POINTER(VxgArray))]
 
 
+class VxgDataBuffer(C.Structure):
+    _fields_ = [("offset", C.c_uint64), ("len", C.c_uint64)]
+
+
 class VxgCanonical(C.Structure):
     _fields_ = [("kind", C.c_uint16), ("ptype", C.c_uint8), ("dtype", C.c_uint8),
                 ("reserved", C.c_uint32), ("len", C.c_uint64), ("values", C.c_void_p),
                 ("values_bytes", C.c_uint64), ("views", C.c_void_p), ("data", C.c_void_p),
-                ("data_bytes", C.c_uint64), ("validity", C.c_void_p)]
+                ("data_bytes", C.c_uint64), ("validity", C.c_void_p),
+                ("n_data_buffers", C.c_uint32), ("data_buffers_cap", C.c_uint32),
+                ("data_buffers", C.POINTER(VxgDataBuffer))]
 
 
 class VxgDictChunk(C.Structure):
@@ -144,6 +156,8 @@ GPU_SIGNATURES = {
     "vxg_stream_sync": (ST, [VP, VP]),
     "vxg_canonical_size": (ST, [VP, C.POINTER(VxgArray), C.POINTER(U64), C.POINTER(U64)]),
     "vxg_canonicalize": (ST, [VP, C.POINTER(VxgArray), C.POINTER(VxgCanonical), VP]),
+    "vxg_canonical_layout": (ST, [VP, C.POINTER(VxgArray), C.POINTER(U64), C.POINTER(U64),
+                                  C.POINTER(VxgDataBuffer), U32, C.POINTER(U32)]),
     "vxg_bitunpack": (ST, [VP, INT, UINT, UINT, U64, VP, U64, VP, VP]),
     "vxg_bitunpack_for": (ST, [VP, INT, UINT, UINT, U64, VP, U64, U64, UINT, INT, VP, VP]),
     "vxg_bitunpack_alp": (ST, [VP, INT, UINT, UINT, U64, VP, U64, U64, UINT, UINT, UINT, VP, VP]),
@@ -205,7 +219,7 @@ def gpu_lib() -> C.CDLL:
     global _gpu
     if _gpu is None:
         _gpu = _load(GPU_LIB_PATH, GPU_SIGNATURES)
-        if _gpu.vxg_abi_version() != 1:
+        if _gpu.vxg_abi_version() != ABI_VERSION:
             raise ImportError("libvortex_gpu.so ABI version mismatch")
     return _gpu
 

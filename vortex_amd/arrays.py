@@ -276,6 +276,23 @@ def varbin(offsets: Array, data: Array, utf8: bool = True, validity=None) -> Arr
                  [offsets, data] + ([vchild] if vchild is not None else []))
 
 
+def varbinview(views, buffers: Sequence, utf8: bool = True, validity=None) -> Array:
+    """VarBinViewArray::try_new (array/varbinview/mod.rs:217-262): children views (u8, 16 B per
+    row), the data buffers (u8), validity.  `views` is a (n, 16) / flat u8 array of arrow
+    BinaryViews; buffer_lens must fit u32."""
+    v = np.ascontiguousarray(views, dtype=np.uint8).reshape(-1)
+    if v.size % 16:
+        _bail("InvalidArgument", "views must be a multiple of 16 bytes")
+    bufs = [np.ascontiguousarray(b, dtype=np.uint8).reshape(-1) for b in buffers]
+    if any(b.size >= 2 ** 32 for b in bufs):
+        _bail("InvalidArgument", "buffer must be within 32-bit range")
+    nullable = validity is not None
+    vk, vchild = _validity_kind(nullable, validity)
+    return Array(ENC["VARBINVIEW"], v.size // 16, DTYPE["UTF8" if utf8 else "BINARY"], "u8", nullable, vk,
+                 {"n_buffers": len(bufs)}, [],
+                 [primitive(v)] + [primitive(b) for b in bufs] + ([vchild] if vchild is not None else []))
+
+
 def fsst(symbols: Array, symbol_lengths: Array, codes: Array, uncompressed_lengths: Array,
          utf8: bool = True) -> Array:
     """FSSTArray::try_new (fsst/array.rs:43-105)."""
@@ -339,6 +356,8 @@ def _fill_meta(m: _lib.VxgMeta, a: Array) -> None:
         m.varbin.offsets_ptype, m.varbin.bytes_len = md["offsets_ptype"], md["bytes_len"]
     elif e == ENC["BOOL"]:
         m.boolean.first_byte_bit_offset = md.get("first_byte_bit_offset", 0)
+    elif e == ENC["VARBINVIEW"]:
+        m.varbinview.n_buffers = md["n_buffers"]
 
 
 def _buf_ptr(b) -> tuple[int, int]:
@@ -412,14 +431,20 @@ class Canonical:
     ptype: str
     values: Any = None       # torch.uint8 tensor (len * width bytes) for Primitive
     views: Any = None        # torch.uint8 tensor (16 * len) for VarBinView
-    data: Any = None         # torch.uint8 tensor: buffer 0 of the view array
+    data: Any = None         # torch.uint8 tensor holding every data buffer of the view array
     validity: Any = None     # torch.uint8 LSB bitmap or None (no nulls)
+    data_buffers: Any = None  # [(offset, len)] of each data buffer inside `data`
 
     def numpy(self):
         """Host copy: values as the ptype's numpy dtype, or (views u8[n,16], data u8[])."""
         if self.kind == "primitive":
             return self.values.cpu().numpy().view(NP_OF_PTYPE[self.ptype])
         return self.views.cpu().numpy().reshape(-1, 16), self.data.cpu().numpy()
+
+    def buffers(self):
+        """The VarBinView's data buffers (buffer_index order) as host u8 arrays."""
+        d = self.data.cpu().numpy()
+        return [d[o: o + n] for o, n in self.data_buffers]
 
     def validity_mask(self):
         if self.validity is None:
@@ -435,8 +460,17 @@ def canonicalize(a: Array, ctx: Context, out_values=None, sync: bool = True) -> 
     keep: list = []
     node = flatten(a, keep)
     dev = torch.device("cuda", ctx.device)
-    vb, db = C.c_uint64(), C.c_uint64()
-    _lib.check(ctx.lib.vxg_canonical_size(ctx.handle, C.byref(node), C.byref(vb), C.byref(db)))
+    vb, db, nb = C.c_uint64(), C.c_uint64(), C.c_uint32()
+    cap = 256
+    while True:  # the layout (FSST heap sizes are device sums) in one call unless > cap buffers
+        table = (_lib.VxgDataBuffer * cap)()
+        st = ctx.lib.vxg_canonical_layout(ctx.handle, C.byref(node), C.byref(vb), C.byref(db), table, cap,
+                                          C.byref(nb))
+        if st == 3 and cap < (1 << 24):
+            cap *= 16
+            continue
+        _lib.check(st)
+        break
     out = _lib.VxgCanonical()
     res = Canonical("primitive" if a.dtype == DTYPE["PRIMITIVE"] else "varbinview", a.len, a.ptype)
     nbits = ((a.len + 31) // 32) * 4
@@ -450,7 +484,9 @@ def canonicalize(a: Array, ctx: Context, out_values=None, sync: bool = True) -> 
         data = torch.empty(db.value + 16, dtype=torch.uint8, device=dev)
         out.views, out.data = views.data_ptr(), data.data_ptr()
         out.data_bytes = db.value
+        out.data_buffers, out.n_data_buffers, out.data_buffers_cap = table, nb.value, nb.value
         res.views, res.data = views[: vb.value], data[: db.value]
+        res.data_buffers = [(int(table[i].offset), int(table[i].len)) for i in range(nb.value)]
     if valid_t is not None:
         out.validity = valid_t.data_ptr()
     _lib.check(ctx.lib.vxg_canonicalize(ctx.handle, C.byref(node), C.byref(out), ctx.stream_ptr()))

@@ -201,6 +201,9 @@ class Planner {
 
     vxg_status canonical(const vxg_array& a, vxg_canonical& out);
     vxg_status canonical_size(const vxg_array& a, uint64_t& vb, uint64_t& db);
+    // Data buffers of a string canonical, placed 16-byte aligned in one allocation.
+    vxg_status string_layout(const vxg_array& a, std::vector<vxg_data_buffer>& bufs, uint64_t& extent);
+    static vxg_status string_buffer_count(const vxg_array& a, uint32_t& n);
 
   private:
     vxg_ctx* ctx_;
@@ -256,6 +259,10 @@ class Planner {
     vxg_status validity_into(const vxg_array& a, void** bitmap);
     vxg_status validity_source(const vxg_array& a, const vxg_array** node, int* kind);
     vxg_status string_canonical(const vxg_array& a, vxg_canonical& out);
+    vxg_status string_lens(const vxg_array& a, std::vector<uint64_t>& lens,
+                           std::vector<std::pair<size_t, const vxg_array*>>& fsst) const;
+    vxg_status strings_into(const vxg_array& a, uint8_t* views, uint8_t* data, const vxg_data_buffer* bufs,
+                            uint32_t bidx, const uint8_t* validity);
 };
 
 vxg_status Planner::view_primitive(const vxg_array& a, const void** p) {
@@ -636,6 +643,7 @@ vxg_status Planner::validity_source(const vxg_array& a, const vxg_array** node, 
     case VXG_ENC_FL_DELTA: return from_meta(2);
     case VXG_ENC_RUN_END: return from_meta(2);
     case VXG_ENC_VARBIN: return from_meta(2);
+    case VXG_ENC_VARBINVIEW: return from_meta(1 + a.meta.varbinview.n_buffers);
     case VXG_ENC_FL_FOR:
     case VXG_ENC_ZIGZAG:
     case VXG_ENC_ALP: return child(a, 0) ? validity_source(*child(a, 0), node, kind) : VXG_OK;
@@ -713,33 +721,128 @@ vxg_status Planner::validity_into(const vxg_array& a, void** bitmap) {
     return VXG_OK;
 }
 
-vxg_status Planner::string_canonical(const vxg_array& a, vxg_canonical& out) {
-    out.kind = VXG_ENC_VARBINVIEW;
-    out.len = a.len;
-    out.dtype = a.dtype;
-    // Sizes are only needed to allocate; a caller that passes both buffers (sized with
-    // vxg_canonical_size) pays no device sum + sync on the decode path.
-    if (!out.views || !out.data) {
-        uint64_t vb, db;
-        VXG_TRY(canonical_size(a, vb, db));
-        if (!out.views) VXG_TRY(hip_check(hipMalloc(&out.views, vb ? vb : 16), "views alloc"));
-        if (!out.data) VXG_TRY(hip_check(hipMalloc(&out.data, db + 16), "data alloc"));
-        out.data_bytes = db;
+// ---- strings: VarBin, VarBinView, FSST, Dict(strings), Chunked (pack_views) -------------
+// Every string canonical is a VarBinView (canonical.rs:56-63).  Its data buffers: one per
+// VarBin / FSST leaf (the bytes buffer / the decoded heap), a Dict's are its values', a
+// VarBinView input keeps its own, and a ChunkedArray concatenates its chunks' lists with each
+// chunk's buffer_index rebased by the buffers before it (chunked/canonical.rs:194-236).
+vxg_status Planner::string_buffer_count(const vxg_array& a, uint32_t& n) {
+    switch (a.encoding) {
+    case VXG_ENC_VARBIN:
+    case VXG_ENC_FSST: n = 1; return VXG_OK;
+    case VXG_ENC_VARBINVIEW: n = a.meta.varbinview.n_buffers; return VXG_OK;
+    case VXG_ENC_DICT:
+        if (a.n_children < 1) return set_error(VXG_ERR_INVALID_ARGUMENT, "DictArray needs values and codes");
+        return string_buffer_count(a.children[0], n);
+    case VXG_ENC_CHUNKED: {
+        uint32_t t = 0;
+        for (uint32_t i = 1; i < a.n_children; i++) {
+            uint32_t k;
+            VXG_TRY(string_buffer_count(a.children[i], k));
+            t += k;
+        }
+        n = t;
+        return VXG_OK;
     }
-    const uint64_t db = out.data_bytes;
-    VXG_TRY(validity_into(a, &out.validity));
-    if (a.encoding == VXG_ENC_VARBIN) {
-        // varbin/flatten.rs:10-17: views over the whole bytes buffer (block 0)
+    default:
+        return set_error(VXG_ERR_NOT_IMPLEMENTED, "string canonicalize for encoding id " + std::to_string(a.encoding));
+    }
+}
+
+// Buffer lengths in order; FSST heap sizes (sum of uncompressed lengths) are device sums
+// recorded in `fsst` as (slot, node) and resolved by string_layout with one readback.
+vxg_status Planner::string_lens(const vxg_array& a, std::vector<uint64_t>& lens,
+                                std::vector<std::pair<size_t, const vxg_array*>>& fsst) const {
+    switch (a.encoding) {
+    case VXG_ENC_VARBIN: {
+        const vxg_array* bytes = child(a, 1);
+        if (!bytes) return set_error(VXG_ERR_INVALID_ARGUMENT, "VarBinArray needs offsets and bytes");
+        lens.push_back(bytes->len);
+        return VXG_OK;
+    }
+    case VXG_ENC_VARBINVIEW:
+        if (a.n_children < 1 + a.meta.varbinview.n_buffers)
+            return set_error(VXG_ERR_INVALID_ARGUMENT, "VarBinViewArray: missing views/data buffers");
+        for (uint32_t b = 0; b < a.meta.varbinview.n_buffers; b++) lens.push_back(a.children[1 + b].len);
+        return VXG_OK;
+    case VXG_ENC_FSST:
+        if (!child(a, 3)) return set_error(VXG_ERR_INVALID_ARGUMENT, "FSST lengths child missing");
+        fsst.emplace_back(lens.size(), &a);
+        lens.push_back(0);
+        return VXG_OK;
+    case VXG_ENC_DICT:
+        if (!child(a, 0)) return set_error(VXG_ERR_INVALID_ARGUMENT, "DictArray needs values and codes");
+        return string_lens(a.children[0], lens, fsst);
+    case VXG_ENC_CHUNKED:
+        for (uint32_t i = 1; i < a.n_children; i++) VXG_TRY(string_lens(a.children[i], lens, fsst));
+        return VXG_OK;
+    default:
+        return set_error(VXG_ERR_NOT_IMPLEMENTED, "string canonicalize for encoding id " + std::to_string(a.encoding));
+    }
+}
+
+vxg_status Planner::string_layout(const vxg_array& a, std::vector<vxg_data_buffer>& bufs, uint64_t& extent) {
+    std::vector<uint64_t> lens;
+    std::vector<std::pair<size_t, const vxg_array*>> fsst;
+    VXG_TRY(string_lens(a, lens, fsst));
+    if (!fsst.empty()) {  // fsst/canonical.rs:29-42: heap size = sum of uncompressed lengths
+        void* d;
+        VXG_TRY(temp(8 * fsst.size(), &d));
+        for (size_t k = 0; k < fsst.size(); k++) {
+            const vxg_array& ul = *child(*fsst[k].second, 3);
+            const void* pul;
+            VXG_TRY(view_primitive(ul, &pul));
+            VXG_TRY(launch_sum(pul, width(ul), ptype_is_signed(ul.ptype), ul.len, static_cast<uint64_t*>(d) + k, s_));
+        }
+        std::vector<uint64_t> h(fsst.size());
+        VXG_TRY(hip_check(hipMemcpyAsync(h.data(), d, 8 * h.size(), hipMemcpyDeviceToHost, s_), "sum readback"));
+        VXG_TRY(hip_check(hipStreamSynchronize(s_), "sum sync"));
+        for (size_t k = 0; k < fsst.size(); k++) lens[fsst[k].first] = h[k];
+    }
+    bufs.resize(lens.size());
+    uint64_t off = 0;
+    for (size_t b = 0; b < lens.size(); b++) {
+        bufs[b] = vxg_data_buffer{off, lens[b]};
+        off = (off + lens[b] + 15) & ~15ull;
+    }
+    extent = lens.empty() ? 0 : bufs.back().offset + bufs.back().len;
+    return VXG_OK;
+}
+
+// Canonical views of `a` into `views`, its data buffers into `data` at bufs[0..k), non-inlined
+// views carrying buffer_index bidx + (buffer within a).  `validity`: a's LSB bitmap or NULL.
+vxg_status Planner::strings_into(const vxg_array& a, uint8_t* views, uint8_t* data, const vxg_data_buffer* bufs,
+                                 uint32_t bidx, const uint8_t* validity) {
+    switch (a.encoding) {
+    case VXG_ENC_VARBIN: {
+        // varbin/flatten.rs:10-17: views over the whole bytes buffer (arrow-cast Utf8 -> Utf8View)
         const vxg_array* offs = child(a, 0);
         const vxg_array* bytes = child(a, 1);
         const void *po, *pb;
         VXG_TRY(view_primitive(*offs, &po));
         VXG_TRY(view_primitive(*bytes, &pb));
-        if (db) VXG_TRY(hip_check(hipMemcpyAsync(out.data, pb, db, hipMemcpyDeviceToDevice, s_), "heap copy"));
-        return launch_varbin_views(static_cast<const uint8_t*>(out.data), width(*offs), po, a.len,
-                                   static_cast<const uint8_t*>(out.validity), static_cast<uint8_t*>(out.views), s_);
+        uint8_t* heap = data + bufs[0].offset;
+        if (bufs[0].len)
+            VXG_TRY(hip_check(hipMemcpyAsync(heap, pb, bufs[0].len, hipMemcpyDeviceToDevice, s_), "heap copy"));
+        return launch_varbin_views(heap, width(*offs), po, a.len, validity, bidx, views, s_);
     }
-    if (a.encoding == VXG_ENC_FSST) {
+    case VXG_ENC_VARBINVIEW: {
+        // already canonical: views (rebased) and buffers copied into the output layout
+        const vxg_array* vw = child(a, 0);
+        const void* pv;
+        VXG_TRY(view_primitive(*vw, &pv));
+        if (vw->len < 16 * a.len) return set_error(VXG_ERR_INVALID_ARGUMENT, "VarBinView views shorter than 16 * len");
+        VXG_TRY(launch_views_rebase(static_cast<const uint8_t*>(pv), a.len, bidx, views, s_));
+        for (uint32_t b = 0; b < a.meta.varbinview.n_buffers; b++) {
+            const void* pb;
+            VXG_TRY(view_primitive(a.children[1 + b], &pb));
+            if (bufs[b].len)
+                VXG_TRY(hip_check(hipMemcpyAsync(data + bufs[b].offset, pb, bufs[b].len, hipMemcpyDeviceToDevice, s_),
+                                  "view buffer copy"));
+        }
+        return VXG_OK;
+    }
+    case VXG_ENC_FSST: {
         // fsst/canonical.rs:7-57
         const vxg_array* sym = child(a, 0);
         const vxg_array* slen = child(a, 1);
@@ -757,32 +860,97 @@ vxg_status Planner::string_canonical(const vxg_array& a, vxg_canonical& out) {
         void* scratch;
         VXG_TRY(temp(fsst_scratch_bytes(a.len), &scratch));
         return launch_fsst(static_cast<const uint64_t*>(psym), static_cast<const uint8_t*>(pslen),
-                           unsigned(sym->len), static_cast<const uint8_t*>(pcb), offs, lens, a.len,
-                           static_cast<const uint8_t*>(out.validity), scratch, static_cast<uint8_t*>(out.data),
-                           static_cast<uint8_t*>(out.views), ctx_->c.err_word, s_);
+                           unsigned(sym->len), static_cast<const uint8_t*>(pcb), offs, lens, a.len, validity, scratch,
+                           data + bufs[0].offset, views, bidx, ctx_->c.err_word, s_);
     }
-    if (a.encoding == VXG_ENC_DICT) {
-        // Dict over string values: take on the 16-B views, buffers kept (varbinview/compute.rs:68-76)
+    case VXG_ENC_DICT: {
+        // Dict over string values: take on the values' views (varbinview/compute.rs:68-76); the
+        // values' buffers are the result's buffers, so they decode straight into the output
         const vxg_array* values = child(a, 0);
         const vxg_array* codes = child(a, 1);
-        vxg_canonical vc{};
-        VXG_TRY(canonical(*values, vc));
-        temps_.push_back(vc.views);
-        temps_.push_back(vc.data);
-        if (vc.validity) temps_.push_back(vc.validity);
-        if (vc.data_bytes)
-            VXG_TRY(hip_check(hipMemcpyAsync(out.data, vc.data, vc.data_bytes, hipMemcpyDeviceToDevice, s_), "dict heap"));
+        if (!values || !codes) return set_error(VXG_ERR_INVALID_ARGUMENT, "DictArray needs values and codes");
+        const vxg_array* vn;
+        int vk;
+        VXG_TRY(validity_source(*values, &vn, &vk));
+        if (vk != 0) return set_error(VXG_ERR_NOT_IMPLEMENTED, "nullable dictionary values");
+        void* vviews;
+        VXG_TRY(temp(16 * values->len, &vviews));
+        VXG_TRY(strings_into(*values, static_cast<uint8_t*>(vviews), data, bufs, bidx, nullptr));
         if (codes->encoding == VXG_ENC_FL_BITPACKED && codes->meta.bitpacked.bit_width <= kDictFusedMaxW) {
             UnpackArgs ua{};
-            ua.dict = vc.views;
+            ua.dict = vviews;
             ua.dict_len = values->len;
-            return decode_bitpacked(*codes, Epi::Dict, 16, ua, out.views);
+            return decode_bitpacked(*codes, Epi::Dict, 16, ua, views);
         }
         const void* pc;
         VXG_TRY(view_primitive(*codes, &pc));
-        return launch_take(16, vc.views, values->len, width(*codes), pc, a.len, out.views, ctx_->c.err_word, s_);
+        return launch_take(16, vviews, values->len, width(*codes), pc, a.len, views, ctx_->c.err_word, s_);
     }
-    return set_error(VXG_ERR_NOT_IMPLEMENTED, "string canonicalize for encoding id " + std::to_string(a.encoding));
+    case VXG_ENC_CHUNKED: {
+        // pack_views (chunked/canonical.rs:194-236): each chunk's views go to its slice of the
+        // output, its buffers after the preceding chunks', buffer_index rebased accordingly
+        const uint64_t n = a.meta.chunked.nchunks;
+        if (a.n_children != n + 1) return set_error(VXG_ERR_INVALID_ARGUMENT, "Chunked child count != nchunks + 1");
+        uint64_t row = 0;
+        uint32_t b = 0;
+        for (uint64_t i = 0; i < n; i++) {
+            const vxg_array& c = a.children[i + 1];
+            if (c.dtype != a.dtype) return set_error(VXG_ERR_MISMATCHED_TYPES, "Chunks must have the ChunkedArray's dtype");
+            uint32_t k;
+            VXG_TRY(string_buffer_count(c, k));
+            void* cv = nullptr;  // the chunk's own validity (null views are all-zero)
+            const vxg_array* vn;
+            int vk;
+            VXG_TRY(validity_source(c, &vn, &vk));
+            if (vk != 0) {
+                VXG_TRY(temp(((c.len + 31) / 32) * 4, &cv));
+                VXG_TRY(validity_into(c, &cv));
+            }
+            VXG_TRY(strings_into(c, views + 16 * row, data, bufs + b, bidx + b, static_cast<const uint8_t*>(cv)));
+            row += c.len;
+            b += k;
+        }
+        if (row != a.len) return set_error(VXG_ERR_INVALID_ARGUMENT, "Chunked len != sum of chunk lens");
+        return VXG_OK;
+    }
+    default:
+        return set_error(VXG_ERR_NOT_IMPLEMENTED, "string canonicalize for encoding id " + std::to_string(a.encoding));
+    }
+}
+
+vxg_status Planner::string_canonical(const vxg_array& a, vxg_canonical& out) {
+    out.kind = VXG_ENC_VARBINVIEW;
+    out.len = a.len;
+    out.dtype = a.dtype;
+    uint32_t nb;
+    VXG_TRY(string_buffer_count(a, nb));
+    std::vector<vxg_data_buffer> bufs;
+    if (out.views && out.data) {
+        // caller-allocated (sized with vxg_canonical_layout / _size): no device sum + sync on
+        // the decode path
+        if (nb == 1) {
+            bufs.push_back(vxg_data_buffer{0, out.data_bytes});
+        } else {
+            if (!out.data_buffers || out.n_data_buffers != nb)
+                return set_error(VXG_ERR_INVALID_ARGUMENT, "caller-provided data needs the vxg_canonical_layout buffer table (" +
+                                                               std::to_string(nb) + " buffers)");
+            bufs.assign(out.data_buffers, out.data_buffers + nb);
+        }
+    } else {
+        uint64_t extent;
+        VXG_TRY(string_layout(a, bufs, extent));
+        if (nb > 1 && (!out.data_buffers || out.data_buffers_cap < nb))
+            return set_error(VXG_ERR_INVALID_ARGUMENT, "data_buffers must have room for " + std::to_string(nb) + " buffers");
+        if (!out.views) VXG_TRY(hip_check(hipMalloc(&out.views, a.len ? 16 * a.len : 16), "views alloc"));
+        if (!out.data) VXG_TRY(hip_check(hipMalloc(&out.data, extent + 16), "data alloc"));
+        out.data_bytes = extent;
+    }
+    out.n_data_buffers = nb;
+    if (out.data_buffers && out.data_buffers_cap >= nb && out.data_buffers != bufs.data())
+        std::copy(bufs.begin(), bufs.end(), out.data_buffers);
+    VXG_TRY(validity_into(a, &out.validity));
+    return strings_into(a, static_cast<uint8_t*>(out.views), static_cast<uint8_t*>(out.data), bufs.data(), 0,
+                        static_cast<const uint8_t*>(out.validity));
 }
 
 vxg_status Planner::canonical_size(const vxg_array& a, uint64_t& vb, uint64_t& db) {
@@ -794,32 +962,8 @@ vxg_status Planner::canonical_size(const vxg_array& a, uint64_t& vb, uint64_t& d
     if (a.dtype != VXG_DTYPE_UTF8 && a.dtype != VXG_DTYPE_BINARY)
         return set_error(VXG_ERR_NOT_IMPLEMENTED, "canonical size for this dtype");
     vb = a.len * 16;
-    if (a.encoding == VXG_ENC_VARBIN) {
-        const vxg_array* bytes = child(a, 1);
-        db = bytes ? bytes->len : 0;
-        return VXG_OK;
-    }
-    if (a.encoding == VXG_ENC_FSST) {
-        const vxg_array* ulen = child(a, 3);
-        if (!ulen) return set_error(VXG_ERR_INVALID_ARGUMENT, "FSST lengths child missing");
-        const void* pul;
-        VXG_TRY(view_primitive(*ulen, &pul));
-        void* d;
-        VXG_TRY(temp(8, &d));
-        VXG_TRY(launch_sum(pul, width(*ulen), ptype_is_signed(ulen->ptype), ulen->len, d, s_));
-        uint64_t h = 0;
-        VXG_TRY(hip_check(hipMemcpyAsync(&h, d, 8, hipMemcpyDeviceToHost, s_), "sum readback"));
-        VXG_TRY(hip_check(hipStreamSynchronize(s_), "sum sync"));
-        db = h;
-        return VXG_OK;
-    }
-    if (a.encoding == VXG_ENC_DICT) {
-        uint64_t v2, d2;
-        VXG_TRY(canonical_size(*child(a, 0), v2, d2));
-        db = d2;
-        return VXG_OK;
-    }
-    return set_error(VXG_ERR_NOT_IMPLEMENTED, "canonical size for encoding id " + std::to_string(a.encoding));
+    std::vector<vxg_data_buffer> bufs;
+    return string_layout(a, bufs, db);
 }
 
 vxg_status Planner::canonical(const vxg_array& a, vxg_canonical& out) {
@@ -928,6 +1072,28 @@ vxg_status vxg_canonical_size(vxg_ctx* ctx, const vxg_array* a, uint64_t* values
     VXG_TRY(p.canonical_size(*a, vb, db));
     if (values_bytes) *values_bytes = vb;
     if (data_bytes) *data_bytes = db;
+    return VXG_OK;
+}
+
+vxg_status vxg_canonical_layout(vxg_ctx* ctx, const vxg_array* a, uint64_t* values_bytes, uint64_t* data_bytes,
+                                vxg_data_buffer* bufs, uint32_t cap, uint32_t* n_bufs) {
+    VXG_TRY(use_device(ctx));
+    if (!a) return set_error(VXG_ERR_INVALID_ARGUMENT, "null array");
+    Planner p(ctx, nullptr);
+    uint64_t vb = 0, db = 0;
+    VXG_TRY(p.canonical_size(*a, vb, db));
+    uint32_t n = 0;
+    if (a->dtype == VXG_DTYPE_UTF8 || a->dtype == VXG_DTYPE_BINARY) {
+        std::vector<vxg_data_buffer> v;
+        uint64_t ext;
+        VXG_TRY(p.string_layout(*a, v, ext));
+        n = uint32_t(v.size());
+        if (bufs && cap < n) return set_error(VXG_ERR_INVALID_ARGUMENT, "buffer table too small");
+        if (bufs) std::copy(v.begin(), v.end(), bufs);
+    }
+    if (values_bytes) *values_bytes = vb;
+    if (data_bytes) *data_bytes = db;
+    if (n_bufs) *n_bufs = n;
     return VXG_OK;
 }
 
@@ -1103,7 +1269,7 @@ vxg_status vxg_fsst_decode(vxg_ctx* ctx, const uint64_t* symbols, const uint8_t*
     ls.p = lens;
     ls.width = ptype_width(lens_ptype);
     ls.sgn = ptype_is_signed(lens_ptype);
-    return launch_fsst(symbols, sym_lens, n_symbols, code_bytes, offs, ls, n, validity, scratch, heap, views,
+    return launch_fsst(symbols, sym_lens, n_symbols, code_bytes, offs, ls, n, validity, scratch, heap, views, 0,
                        ctx->c.err_word, S(stream));
 }
 

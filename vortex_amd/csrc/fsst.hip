@@ -70,10 +70,10 @@ __device__ __forceinline__ int64_t block_exclusive_scan(int64_t v, int64_t* wave
 }
 
 // arrow-array 53.2 make_view: len <= 12 -> [len][bytes, zero padded]; else
-// [len][first 4 bytes][buffer_index = 0][offset].  `get(j)` returns byte j of the string (only
+// [len][first 4 bytes][buffer_index][offset].  `get(j)` returns byte j of the string (only
 // called for j < 12 inline / j < 4 prefix, and masked by j < len).
 template <typename Get>
-__device__ __forceinline__ uint4 build_view(uint32_t len, uint32_t offset, Get get) {
+__device__ __forceinline__ uint4 build_view(uint32_t len, uint32_t offset, uint32_t bidx, Get get) {
     uint32_t w1 = 0, w2 = 0, w3 = 0;
     if (len <= 12) {
 #pragma unroll
@@ -86,18 +86,19 @@ __device__ __forceinline__ uint4 build_view(uint32_t len, uint32_t offset, Get g
     } else {
 #pragma unroll
         for (int j = 0; j < 4; j++) w1 |= uint32_t(get(j)) << (8 * j);
+        w2 = bidx;
         w3 = offset;
     }
     return make_uint4(len, w1, w2, w3);
 }
 
 // The same view from an LDS byte image: four aligned dword reads and byte funnel shifts.
-__device__ __forceinline__ uint4 lds_view(const uint32_t* h32, int a, uint32_t len, uint32_t offset) {
+__device__ __forceinline__ uint4 lds_view(const uint32_t* h32, int a, uint32_t len, uint32_t offset, uint32_t bidx) {
     const int w = a >> 2;
     const uint32_t sh = uint32_t(a & 3);
     const uint32_t d0 = h32[w], d1 = h32[w + 1], d2 = h32[w + 2], d3 = h32[w + 3];
     uint32_t w1 = __builtin_amdgcn_alignbyte(d1, d0, sh);
-    if (len > 12) return make_uint4(len, w1, 0u, offset);
+    if (len > 12) return make_uint4(len, w1, bidx, offset);
     uint32_t w2 = __builtin_amdgcn_alignbyte(d2, d1, sh);
     uint32_t w3 = __builtin_amdgcn_alignbyte(d3, d2, sh);
     auto keep = [&](int base) -> uint32_t {
@@ -253,7 +254,7 @@ __global__ __launch_bounds__(kTile) void fsst_decode(const uint64_t* __restrict_
                                                      const int64_t* __restrict__ tile_prefix,
                                                      const int64_t* __restrict__ block_totals,
                                                      uint8_t* __restrict__ heap, uint4* __restrict__ views,
-                                                     uint32_t* __restrict__ err) {
+                                                     uint32_t bidx, uint32_t* __restrict__ err) {
     __shared__ uint64_t s_sym[256];
     __shared__ uint8_t s_len[256];
     __shared__ int ws_a[kTile / 64], ws_b[kTile / 64];
@@ -440,7 +441,7 @@ __global__ __launch_bounds__(kTile) void fsst_decode(const uint64_t* __restrict_
             }
         }
         if (live)
-            views[i] = valid ? lds_view(s_heap32, hshift + int(my_rel), vlen, uint32_t(tile_out0 + my_rel))
+            views[i] = valid ? lds_view(s_heap32, hshift + int(my_rel), vlen, uint32_t(tile_out0 + my_rel), bidx)
                              : make_uint4(0, 0, 0, 0);
     } else {
         // direct path: per-string decode straight into HBM (codes of string i are
@@ -467,7 +468,7 @@ __global__ __launch_bounds__(kTile) void fsst_decode(const uint64_t* __restrict_
         if (o != o_end) __hip_atomic_fetch_or(err, kErrFsst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (live) {
             const uint8_t* hp = heap + o_start;
-            views[i] = valid ? build_view(vlen, uint32_t(o_start),
+            views[i] = valid ? build_view(vlen, uint32_t(o_start), bidx,
                                           [&](int j) { return uint32_t(j) < vlen ? hp[j] : uint8_t(0); })
                              : make_uint4(0, 0, 0, 0);
         }
@@ -491,7 +492,7 @@ static void launch_tile_scan_fl32(int W, dim3 grid, hipStream_t s, const IntCol&
 vxg_status launch_fsst(const uint64_t* symbols, const uint8_t* sym_lens, unsigned n_symbols,
                        const uint8_t* code_bytes, const IntCol& offs, const IntCol& lens, uint64_t n,
                        const uint8_t* validity, void* scratch, uint8_t* heap, uint8_t* views,
-                       uint32_t* err, hipStream_t s) {
+                       uint32_t bidx, uint32_t* err, hipStream_t s) {
     if (n == 0) return VXG_OK;
     if (n_symbols > 255) return set_error(VXG_ERR_INVALID_ARGUMENT, "FSST symbol table > 255 entries");
     const uint64_t n_tiles = (n + kTile - 1) / kTile;
@@ -511,7 +512,7 @@ vxg_status launch_fsst(const uint64_t* symbols, const uint8_t* sym_lens, unsigne
                                tiles, blocks);
         hipLaunchKernelGGL((fsst_decode<OA, LA>), dim3(unsigned(n_tiles)), dim3(kTile), 0, s, symbols, sym_lens,
                            n_symbols, code_bytes, off_acc, len_acc, n, validity, tiles, blocks, heap,
-                           reinterpret_cast<uint4*>(views), err);
+                           reinterpret_cast<uint4*>(views), bidx, err);
     };
     // accessor = plain width 1/2/4/8 or packed T = 32/64
     auto with = [](const IntCol& c, auto&& f) -> bool {

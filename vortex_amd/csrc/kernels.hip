@@ -568,7 +568,8 @@ vxg_status launch_fill(int value_width, const uint8_t* scalar16, uint64_t n, voi
 // null rows -> all-zero view (GenericByteViewBuilder::append_null).
 // Byte positions are compile-time (unrolled j) so nothing is a runtime-indexed register array
 // (which hipcc places in scratch); reads are guarded by j < len.
-__device__ __forceinline__ uint4 make_view(const uint8_t* __restrict__ heap, uint64_t start, uint32_t len) {
+__device__ __forceinline__ uint4 make_view(const uint8_t* __restrict__ heap, uint64_t start, uint32_t len,
+                                          uint32_t bidx) {
     const uint8_t* p = heap + start;
     uint32_t w1 = 0, w2 = 0, w3 = 0;
     if (len <= 12) {
@@ -582,6 +583,7 @@ __device__ __forceinline__ uint4 make_view(const uint8_t* __restrict__ heap, uin
     } else {
 #pragma unroll
         for (int j = 0; j < 4; j++) w1 |= uint32_t(p[j]) << (8 * j);
+        w2 = bidx;
         w3 = uint32_t(start);
     }
     return make_uint4(len, w1, w2, w3);
@@ -590,7 +592,7 @@ __device__ __forceinline__ uint4 make_view(const uint8_t* __restrict__ heap, uin
 __global__ __launch_bounds__(kBlock) void varbin_views_kernel(const uint8_t* __restrict__ heap, const void* offs,
                                                               int offs_width, uint64_t n,
                                                               const uint8_t* __restrict__ validity,
-                                                              uint4* __restrict__ views) {
+                                                              uint32_t bidx, uint4* __restrict__ views) {
     const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
     for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
         if (validity && !((validity[i >> 3] >> (i & 7)) & 1)) {
@@ -599,16 +601,35 @@ __global__ __launch_bounds__(kBlock) void varbin_views_kernel(const uint8_t* __r
         }
         const uint64_t a = load_uint(offs, offs_width, offs_width < 8, i);
         const uint64_t b = load_uint(offs, offs_width, offs_width < 8, i + 1);
-        views[i] = make_view(heap, a, uint32_t(b - a));
+        views[i] = make_view(heap, a, uint32_t(b - a), bidx);
     }
 }
 
 vxg_status launch_varbin_views(const uint8_t* heap, int offs_width, const void* offsets, uint64_t n,
-                               const uint8_t* validity, uint8_t* views, hipStream_t s) {
+                               const uint8_t* validity, uint32_t bidx, uint8_t* views, hipStream_t s) {
     if (n == 0) return VXG_OK;
     hipLaunchKernelGGL(varbin_views_kernel, dim3(grid_for(n)), dim3(kBlock), 0, s, heap, offsets,
-                       offs_width, n, validity, reinterpret_cast<uint4*>(views));
+                       offs_width, n, validity, bidx, reinterpret_cast<uint4*>(views));
     return hip_check(hipGetLastError(), "varbin_views_kernel");
+}
+
+// pack_views (chunked/canonical.rs:214-231): copy views, adding `add` to the buffer_index of
+// every non-inlined view (len > 12); inlined views are copied unchanged.
+__global__ __launch_bounds__(kBlock) void views_rebase_kernel(const uint4* __restrict__ src, uint64_t n, uint32_t add,
+                                                              uint4* __restrict__ dst) {
+    const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+        uint4 v = src[i];
+        if (v.x > 12) v.z += add;
+        dst[i] = v;
+    }
+}
+
+vxg_status launch_views_rebase(const uint8_t* src, uint64_t n, uint32_t add, uint8_t* dst, hipStream_t s) {
+    if (n == 0) return VXG_OK;
+    hipLaunchKernelGGL(views_rebase_kernel, dim3(grid_for(n)), dim3(kBlock), 0, s,
+                       reinterpret_cast<const uint4*>(src), n, add, reinterpret_cast<uint4*>(dst));
+    return hip_check(hipGetLastError(), "views_rebase_kernel");
 }
 
 }  // namespace vxg

@@ -169,8 +169,10 @@ uint64_t fsst_scratch_bytes(uint64_t n);
 vxg_status launch_fsst(const uint64_t* symbols, const uint8_t* sym_lens, unsigned n_symbols,
                        const uint8_t* code_bytes, const IntCol& offs, const IntCol& lens, uint64_t n,
                        const uint8_t* validity, void* scratch, uint8_t* heap, uint8_t* views,
-                       uint32_t* err, hipStream_t s);
+                       uint32_t bidx, uint32_t* err, hipStream_t s);
+// Views carry `bidx` as the buffer_index of non-inlined rows.
 vxg_status launch_varbin_views(const uint8_t* heap, int offs_width, const void* offsets, uint64_t n,
-                               const uint8_t* validity, uint8_t* views, hipStream_t s);
+                               const uint8_t* validity, uint32_t bidx, uint8_t* views, hipStream_t s);
+vxg_status launch_views_rebase(const uint8_t* src, uint64_t n, uint32_t add, uint8_t* dst, hipStream_t s);
 
 }  // namespace vxg

@@ -261,3 +261,27 @@ def encode_fsst_from_heap(heap: np.ndarray, offsets: np.ndarray, valid: Optional
 def encode_fsst(strings: Sequence[Optional[bytes]], compress_children: bool = True) -> Array:
     heap, offs, valid = strings_to_heap(strings)
     return encode_fsst_from_heap(heap, offs, valid if not valid.all() else None, compress_children)
+
+
+def encode_varbinview(strings: Sequence[Optional[bytes]], utf8: bool = True) -> Array:
+    """VarBinViewArray::from_iter (varbinview/mod.rs:318-337 via arrow's GenericByteViewBuilder):
+    one data buffer holding the non-inlined strings; views per arrow make_view (len <= 12
+    inline, else [len][prefix][buffer 0][offset]); nulls are all-zero views."""
+    n = len(strings)
+    views = np.zeros((n, 16), dtype=np.uint8)
+    parts, off = [], 0
+    for i, st in enumerate(strings):
+        if st is None:
+            continue
+        ln = len(st)
+        views[i, :4] = np.frombuffer(np.uint32(ln).tobytes(), np.uint8)
+        if ln <= 12:
+            views[i, 4: 4 + ln] = np.frombuffer(st, np.uint8)
+        else:
+            views[i, 4:8] = np.frombuffer(st[:4], np.uint8)
+            views[i, 12:16] = np.frombuffer(np.uint32(off).tobytes(), np.uint8)
+            parts.append(st)
+            off += ln
+    data = np.frombuffer(b"".join(parts), dtype=np.uint8).copy()
+    valid = [s is not None for s in strings]
+    return A.varbinview(views, [data], utf8=utf8, validity=None if all(valid) else valid)
