@@ -14,8 +14,9 @@ Contract:
     time from HIP events on the decode stream, against 8.0 TB/s;
   * `cpu_baseline` = the oracle (C restatement of the reference's single-threaded
     canonicalize) on a bounded sample, rank 0 only;
-  * the other single-GPU configs (C2 ALP f64, C3 Dict->BitPacked u64 chunk shard, C4 FSST)
-    are measured the same way and reported under "encodings".
+  * the other configs (C2 ALP f64, C3 Dict->BitPacked u64 chunk shard, C4 FSST, C5 the TPC-H
+    lineitem scan: 16 chunked columns, this rank's chunk range) are measured the same way and
+    reported under "encodings".
 Inputs are rotated across several HBM copies so every step reads from HBM, not from the
 256 MiB Infinity Cache.
 """
@@ -124,35 +125,72 @@ def make_c4(rng):
                      read_bytes=arr.nbytes(), write_bytes=total + 16 * n, dtype="u8")
 
 
+def make_c5_shard(rng, world: int, rank: int):
+    """C5: bench-vortex's TPC-H lineitem scan -> canonicalize (tools/lineitem.py): SF1's 6 001 215
+    rows, 16 columns, each a ChunkedArray of 64 Ki-row chunks compressed with the sampling
+    compressor's cascades.  The table is fixed (strong scaling): the 92 chunks are split into
+    contiguous ranges, one per rank, and a step canonicalizes every column of this rank's range
+    (struct_to_arrow, canonical.rs:169-187: one canonicalize per field).  The reference reads
+    the table from a Vortex file (vortex-serde); the file reader is out of this round's scope,
+    so the columns start in HBM like the other configs."""
+    from tools import lineitem as L
+    from vortex_amd.shard import plan_shards
+    nch = L.n_chunks()
+    mine = plan_shards([1] * nch, world)[rank]
+    cols, plain = L.lineitem_columns(mine)
+    rows = sum(len(v) for v in plain["l_orderkey"])
+    write = sum(L.canonical_bytes(v) for vs in plain.values() for v in vs)
+    read = sum(a.nbytes() for a in cols.values())
+    return [cols[name] for name, _ in L.COLUMNS], dict(
+        name="C5", encoding="lineitem scan: 16 x vortex.chunked[<per-column cascades>] -> canonical",
+        values=rows, read_bytes=read, write_bytes=write, dtype="mixed", chunks_per_gpu=len(mine),
+        chunk_range=[mine.start, mine.stop], global_chunks=nch, strong_scaling=True)
+
+
 # ------------------------------------------------------------------------------ timing
 class Workload:
-    def __init__(self, arr, info, ctx, copies: int):
+    """One or more arrays (C5: the 16 lineitem columns) with preallocated canonical outputs; a
+    step canonicalizes each of them once through the C ABI, on one stream."""
+
+    def __init__(self, arrs, info, ctx, copies: int):
         import torch
         import vortex_amd.arrays as A
         self.info, self.ctx = info, ctx
+        arrs = arrs if isinstance(arrs, list) else [arrs]
         dev = torch.device("cuda", ctx.device)
-        self.trees = [arr.to(dev) for _ in range(copies)]
         self.keep = []
-        self.nodes = [A.flatten(t, self.keep) for t in self.trees]
-        vb, db = C.c_uint64(), C.c_uint64()
-        V = ctx.lib
-        chk(V.vxg_canonical_size(ctx.handle, C.byref(self.nodes[0]), C.byref(vb), C.byref(db)))
-        self.out = A._lib.VxgCanonical()
-        if arr.dtype == A.DTYPE["PRIMITIVE"]:
-            self.values = torch.empty(vb.value, dtype=torch.uint8, device=dev)
-            self.out.values = self.values.data_ptr()
-        else:
-            self.views = torch.empty(vb.value, dtype=torch.uint8, device=dev)
-            self.data = torch.empty(db.value + 16, dtype=torch.uint8, device=dev)
-            self.out.views, self.out.data = self.views.data_ptr(), self.data.data_ptr()
-            self.out.data_bytes = db.value
+        self.cols = []
+        for arr in arrs:
+            trees = [arr.to(dev) for _ in range(copies)]
+            nodes = [A.flatten(t, self.keep) for t in trees]
+            vb, db, nb = C.c_uint64(), C.c_uint64(), C.c_uint32()
+            table = (A._lib.VxgDataBuffer * 4096)()
+            chk(ctx.lib.vxg_canonical_layout(ctx.handle, C.byref(nodes[0]), C.byref(vb), C.byref(db), table, 4096,
+                                             C.byref(nb)))
+            out = A._lib.VxgCanonical()
+            if arr.dtype == A.DTYPE["PRIMITIVE"]:
+                vals = torch.empty(max(vb.value, 16), dtype=torch.uint8, device=dev)
+                out.values = vals.data_ptr()
+                self.keep.append(vals)
+            else:
+                views = torch.empty(max(vb.value, 16), dtype=torch.uint8, device=dev)
+                data = torch.empty(db.value + 16, dtype=torch.uint8, device=dev)
+                out.views, out.data, out.data_bytes = views.data_ptr(), data.data_ptr(), db.value
+                out.data_buffers, out.n_data_buffers, out.data_buffers_cap = table, nb.value, 4096
+                self.keep += [views, data, table]
+            if arr.nullable:
+                vt = torch.empty(((arr.len + 31) // 32) * 4 + 4, dtype=torch.uint8, device=dev)
+                out.validity = vt.data_ptr()
+                self.keep.append(vt)
+            self.cols.append((trees, nodes, out))
         self.i = 0
 
     def step(self):
-        node = self.nodes[self.i % len(self.nodes)]
+        k = self.i
         self.i += 1
-        chk(self.ctx.lib.vxg_canonicalize(self.ctx.handle, C.byref(node), C.byref(self.out),
-                                          self.ctx.stream_ptr()))
+        for trees, nodes, out in self.cols:
+            chk(self.ctx.lib.vxg_canonicalize(self.ctx.handle, C.byref(nodes[k % len(nodes)]), C.byref(out),
+                                              self.ctx.stream_ptr()))
 
 
 def chk(st):
@@ -292,7 +330,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--workloads", default="c1,c2,c3,c4",
+    ap.add_argument("--workloads", default="c1,c2,c3,c4,c5",
                     help="comma list; c1 is the headline, others go under 'encodings'")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -315,13 +353,14 @@ def main():
     import vortex_amd as V
     ctx = V.Context(local)
     rng = np.random.default_rng(42 + rank)
-    makers = {"c1": make_c1, "c2": make_c2, "c3": lambda r: make_c3_shard(r, world, rank), "c4": make_c4}
-    copies = {"c1": 4, "c2": 1, "c3": 2, "c4": 1}
+    makers = {"c1": make_c1, "c2": make_c2, "c3": lambda r: make_c3_shard(r, world, rank), "c4": make_c4,
+              "c5": lambda r: make_c5_shard(r, world, rank)}
+    copies = {"c1": 4, "c2": 1, "c3": 2, "c4": 1, "c5": 1}
     results = {}
     for key in [w.strip() for w in args.workloads.split(",") if w.strip()]:
         t0 = time.perf_counter()
         arr, info = makers[key](rng)
-        e2e = run_e2e(arr, info, ctx) if args.e2e else None
+        e2e = run_e2e(arr, info, ctx) if args.e2e and not isinstance(arr, list) else None
         wl = Workload(arr, info, ctx, copies[key])
         del arr
         if rank == 0:
@@ -330,9 +369,14 @@ def main():
         elapsed, kmean, kmed = run_workload(wl, steps, args.warmup if key == "c1" else 2, dist, rank)
         per_step = elapsed / steps
         algo = info["read_bytes"] + info["write_bytes"]
+        total_write = world * info["write_bytes"]
+        if info.get("strong_scaling") and dist is not None:  # ranks hold different shares of one table
+            t = torch.tensor([float(info["write_bytes"])], dtype=torch.float64, device="cuda")
+            dist.all_reduce(t)
+            total_write = float(t.item())
         results[key] = dict(info=info, elapsed=elapsed, ms_per_step=per_step * 1e3, kernel_ms_mean=kmean,
                             kernel_ms_median=kmed, algo_bytes=algo,
-                            value=world * info["write_bytes"] * steps / elapsed / 1e9, e2e=e2e)
+                            value=total_write * steps / elapsed / 1e9, e2e=e2e)
         del wl
         torch.cuda.empty_cache()
 
@@ -359,7 +403,7 @@ def main():
                        "parallelism": f"chunk-per-GPU x{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": pmc_traffic("fl_unpack_u32_w7"),
+                         "traffic": pmc_traffic("fl_unpack_u32_w7") if head_key == "c1" else None,
                          "kernel_ms_mean": round(h["kernel_ms_mean"], 5),
                          "algorithmic_bytes_per_launch": h["algo_bytes"]},
             "encodings": {},

@@ -486,3 +486,23 @@ def test_full_size_c1_roundtrip(ctx):
     got = gpu(arr, ctx).numpy()
     assert got.tobytes() == vals.tobytes()
     assert int(got.astype(np.uint64).sum()) == int(vals.astype(np.uint64).sum())
+
+
+# ------------------------------------------------------------------ C5: TPC-H lineitem scan
+def test_lineitem_scan_every_column(ctx):
+    """BASELINE C5 at reduced size: all 16 lineitem columns (tools/lineitem.py cascades:
+    RunEnd, FoR/BitPacked, ALP, Dict(VarBin), FSST), 3 chunks of 8 Ki rows (one ragged), each
+    column canonicalized through the C ABI and compared with the oracle and the plain values."""
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+    from tools import lineitem as L
+    rows, cr = 2 * 8192 + 777, 8192
+    cols, plain = L.lineitem_columns(range(L.n_chunks(rows, cr)), rows=rows, chunk_rows=cr)
+    for name, kind in L.COLUMNS:
+        arr = cols[name]
+        if kind == "utf8":
+            strings = [s for part in plain[name] for s in part]
+            assert_string_parity(arr, ctx, strings)
+        else:
+            assert_primitive_parity(arr, ctx, np.concatenate(plain[name]))

@@ -370,3 +370,24 @@ def test_reference_validation_errors():
         A.dict_array(A.primitive(np.array([1], np.int32)), A.primitive(np.array([0], np.int32)))
     with pytest.raises(A.VortexError, match="bit width"):
         E.encode_bitpacked(np.array([1, 2], np.uint8), bit_width=8)
+
+
+def test_lineitem_generator_and_cascades():
+    """tools/lineitem.py: chunk c is a pure function of (seed, c); the cascades decode (oracle)
+    back to the plain values; l_orderkey is sorted across chunks."""
+    import sys
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+    from tools import lineitem as L
+    rows, cr = 8192 + 100, 8192
+    cols, plain = L.lineitem_columns(range(2), rows=rows, chunk_rows=cr)
+    again = L.chunk_values(1, rows, cr)
+    assert np.array_equal(again["l_partkey"], plain["l_partkey"][1])
+    ok = np.concatenate(plain["l_orderkey"])
+    assert ok.size == rows and np.all(np.diff(ok) >= 0)
+    for name, kind in L.COLUMNS:
+        if kind == "utf8":
+            (views, bufs), _ = canon(cols[name])
+            strings = [s for part in plain[name] for s in part]
+            assert [view_bytes(views, bufs, i) for i in range(0, rows, 97)] == strings[::97]
+        else:
+            assert np.array_equal(canon(cols[name])[0], np.concatenate(plain[name]))

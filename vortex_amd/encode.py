@@ -210,12 +210,25 @@ def runend_encode(values) -> tuple[np.ndarray, np.ndarray]:
     return ends[:r], rv[:r]
 
 
-def encode_runend(values, bitpack_ends: bool = True) -> Array:
-    """runend_encode (runend/compress.rs:15-93) + ends cascade (compressors/runend.rs)."""
+def encode_runend(values, bitpack_ends: bool = True, compress_values: bool = False) -> Array:
+    """runend_encode (runend/compress.rs:15-93) + the compressor cascade (compressors/runend.rs:
+    45-70: ends -> BitPacked, values -> FoR/BitPacked when `compress_values`)."""
     v = np.ascontiguousarray(values)
     ends, rv = runend_encode(v)
     e = encode_bitpacked(ends, allow_patches=False) if bitpack_ends and ends.size else A.primitive(ends)
-    return A.run_end(e, A.primitive(rv), length=v.size)
+    vals = encode_for_bitpacked(rv) if compress_values and rv.size and rv.dtype.kind in "iu" else A.primitive(rv)
+    return A.run_end(e, vals, length=v.size)
+
+
+def encode_dict_strings(strings: Sequence[bytes], utf8: bool = True) -> Array:
+    """dict_encode_varbin (dict/compress.rs:88-143): values = VarBin of the distinct strings in
+    first-appearance order (i32 offsets), codes u64 -> BitPacked (compressors/dict.rs)."""
+    pos: dict = {}
+    codes = np.fromiter((pos.setdefault(s, len(pos)) for s in strings), dtype=np.uint64, count=len(strings))
+    uniq = list(pos.keys())
+    heap, offs, _ = strings_to_heap(uniq)
+    values = A.varbin(A.primitive(offs.astype(np.int32)), A.primitive(heap), utf8=utf8)
+    return A.dict_array(values, encode_bitpacked(codes, allow_patches=False))
 
 
 def strings_to_heap(strings: Sequence[Optional[bytes]]) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
