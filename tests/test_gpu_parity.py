@@ -506,3 +506,23 @@ def test_lineitem_scan_every_column(ctx):
             assert_string_parity(arr, ctx, strings)
         else:
             assert_primitive_parity(arr, ctx, np.concatenate(plain[name]))
+
+
+def test_chunked_runend_batched(ctx):
+    """Chunked[RunEnd]: ends/values decoded with the other chunks' K1 launches into one
+    temporary, expansions in shared launches; sliced chunks (offset) and primitive children."""
+    rng = np.random.default_rng(21)
+    chunks, expect = [], []
+    for c in range(60):
+        n = 5000 + 333 * c
+        v = np.repeat(rng.integers(-10 ** 6, 10 ** 6, n), rng.integers(1, 6, n))[:n].astype(np.int64)
+        arr = E.encode_runend(v, compress_values=c % 2 == 0, bitpack_ends=c % 3 != 0)
+        if c % 5 == 4:  # RunEndArray::slice (runend/compute.rs:98-110): runs from the one holding
+            ends, rv = E.runend_encode(v)  # `start`, offset = start, ends stay absolute
+            sb = int(np.searchsorted(ends, 7, side="right"))
+            arr = A.run_end(E.encode_bitpacked(ends[sb:], allow_patches=False), A.primitive(rv[sb:]),
+                            length=n - 20, offset=7)
+            v = v[7: 7 + n - 20]
+        chunks.append(arr)
+        expect.append(v)
+    assert_primitive_parity(A.chunked(chunks), ctx, np.concatenate(expect))

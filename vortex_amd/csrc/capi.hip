@@ -453,14 +453,56 @@ bool Planner::k1_fusable(const vxg_array& c) const {
 
 vxg_status Planner::decode_chunked_primitive(const vxg_array& a, void* dst) {
     // chunked/canonical.rs:27-122 / pack_primitives :170-187 -- every chunk decodes straight
-    // into its slice of the output (no per-chunk materialisation + memcpy).  Chunks that are
-    // one K1 decode share launches (chunk tables of up to kArgChunks per kernel); the others
-    // decode one by one.
+    // into its slice of the output (no per-chunk materialisation + memcpy).  Launches are
+    // shared across chunks, level by level:
+    //   level 0  K1 decodes: chunks that are one K1 decode, and the ends/values children of
+    //            RunEnd chunks (into one temporary)      -> grouped by kernel, 32 per launch
+    //   level 1  their patch scatters
+    //   level 2  RunEnd expansions                         -> 48 chunks per launch
+    // Other chunks decode one by one.
     const uint64_t n = a.meta.chunked.nchunks;
     if (a.n_children != n + 1) return set_error(VXG_ERR_INVALID_ARGUMENT, "Chunked child count != nchunks + 1");
     const int w = width(a);
     std::vector<K1Job> jobs;
     std::vector<PatchJob> patches;
+    std::vector<RunEndChunk> runs;
+    // RunEnd chunks whose ends/values are primitive or one K1 decode: their temporaries
+    auto child_ok = [&](const vxg_array* x) {
+        return x && ptype_is_int(x->ptype) && (x->encoding == VXG_ENC_PRIMITIVE || k1_fusable(*x));
+    };
+    auto batch_runend = [&](const vxg_array& c) {
+        const vxg_array* e = child(c, 0);
+        const vxg_array* v = child(c, 1);
+        return c.encoding == VXG_ENC_RUN_END && child_ok(e) && v && width(*v) == w && e->len == v->len &&
+               (v->encoding == VXG_ENC_PRIMITIVE || k1_fusable(*v)) && e->len > 0;
+    };
+    uint64_t tmp_bytes = 0;
+    for (uint64_t i = 0; i < n; i++) {
+        const vxg_array& c = a.children[i + 1];
+        if (!batch_runend(c)) continue;
+        const vxg_array* e = child(c, 0);
+        const vxg_array* v = child(c, 1);
+        if (e->encoding != VXG_ENC_PRIMITIVE) tmp_bytes += (e->len * width(*e) + 15) & ~15ull;
+        if (v->encoding != VXG_ENC_PRIMITIVE) tmp_bytes += (v->len * width(*v) + 15) & ~15ull;
+    }
+    uint8_t* tmp = nullptr;
+    if (tmp_bytes) {
+        void* t;
+        VXG_TRY(temp(tmp_bytes, &t));
+        tmp = static_cast<uint8_t*>(t);
+    }
+    // decode `x` (primitive or one K1 decode) for a RunEnd chunk: pointer into the temporary
+    auto level0 = [&](const vxg_array& x, const void** p) -> vxg_status {
+        if (x.encoding == VXG_ENC_PRIMITIVE) return view_primitive(x, p);
+        *p = tmp;
+        tmp += (x.len * width(x) + 15) & ~15ull;
+        k1_batch_ = &jobs;
+        patch_batch_ = &patches;
+        const vxg_status st = decode_into(x, const_cast<void*>(*p));
+        k1_batch_ = nullptr;
+        patch_batch_ = nullptr;
+        return st;
+    };
     uint64_t off = 0;
     for (uint64_t i = 0; i < n; i++) {
         const vxg_array& c = a.children[i + 1];
@@ -474,6 +516,19 @@ vxg_status Planner::decode_chunked_primitive(const vxg_array& a, void* dst) {
             k1_batch_ = nullptr;
             patch_batch_ = nullptr;
             VXG_TRY(st);
+        } else if (batch_runend(c)) {
+            // runend/compress.rs:115-148 (runend/array.rs:191-197)
+            const vxg_array& e = *child(c, 0);
+            const vxg_array& v = *child(c, 1);
+            RunEndChunk r{};
+            VXG_TRY(level0(e, &r.ends));
+            VXG_TRY(level0(v, &r.values));
+            r.out = slice;
+            r.n_runs = e.len;
+            r.offset = c.meta.runend.offset;
+            r.len = c.len;
+            r.ends_width = uint32_t(width(e));
+            runs.push_back(r);
         } else if ((reinterpret_cast<uintptr_t>(slice) & 15) == 0) {
             VXG_TRY(decode_into(c, slice));
         } else {
@@ -486,6 +541,19 @@ vxg_status Planner::decode_chunked_primitive(const vxg_array& a, void* dst) {
     if (off != a.len) return set_error(VXG_ERR_INVALID_ARGUMENT, "Chunked len != sum of chunk lens");
     VXG_TRY(launch_k1_jobs(jobs, ctx_->c.err_word, s_));
     for (const PatchJob& p : patches) VXG_TRY(apply_sparse_patches(*p.sp, p.T, p.epi, p.vw, p.a, p.dst, p.out_len));
+    for (size_t i = 0; i < runs.size(); i += kRunEndArgChunks) {
+        RunEndTable tab{};
+        tab.err = ctx_->c.err_word;
+        uint64_t groups = 0;
+        for (size_t k = i; k < runs.size() && k - i < size_t(kRunEndArgChunks); k++) {
+            if (runs[k].len == 0) continue;
+            RunEndChunk& r = tab.c[tab.n++];
+            r = runs[k];
+            r.first_group = groups;
+            groups += (r.len + 2047) / 2048;
+        }
+        VXG_TRY(launch_runend_chunks(w, tab, groups, s_));
+    }
     return VXG_OK;
 }
 
@@ -888,9 +956,33 @@ vxg_status Planner::strings_into(const vxg_array& a, uint8_t* views, uint8_t* da
     }
     case VXG_ENC_CHUNKED: {
         // pack_views (chunked/canonical.rs:194-236): each chunk's views go to its slice of the
-        // output, its buffers after the preceding chunks', buffer_index rebased accordingly
+        // output, its buffers after the preceding chunks', buffer_index rebased accordingly.
+        // Dict(VarBin values, BitPacked codes) chunks share launches: one batched
+        // views-and-bytes launch for all their dictionaries, one grouped K1 gather.
         const uint64_t n = a.meta.chunked.nchunks;
         if (a.n_children != n + 1) return set_error(VXG_ERR_INVALID_ARGUMENT, "Chunked child count != nchunks + 1");
+        auto dict_batchable = [&](const vxg_array& c) {
+            if (c.encoding != VXG_ENC_DICT || c.n_children < 2) return false;
+            const vxg_array& v = c.children[0];
+            const vxg_array& k = c.children[1];
+            return v.encoding == VXG_ENC_VARBIN && v.validity != VXG_VALIDITY_ARRAY &&
+                   v.validity != VXG_VALIDITY_ALL_INVALID && v.n_children >= 2 &&
+                   v.children[0].encoding == VXG_ENC_PRIMITIVE && v.children[1].encoding == VXG_ENC_PRIMITIVE &&
+                   k.encoding == VXG_ENC_FL_BITPACKED && ptype_is_unsigned(k.ptype) && !k.nullable &&
+                   k.meta.bitpacked.bit_width <= kDictFusedMaxW;
+        };
+        uint64_t dict_rows = 0;
+        for (uint64_t i = 0; i < n; i++)
+            if (dict_batchable(a.children[i + 1])) dict_rows += a.children[i + 1].children[0].len;
+        uint8_t* dviews = nullptr;
+        if (dict_rows) {
+            void* t;
+            VXG_TRY(temp(16 * dict_rows, &t));
+            dviews = static_cast<uint8_t*>(t);
+        }
+        std::vector<VarBinChunk> dicts;
+        std::vector<K1Job> jobs;
+        std::vector<PatchJob> patches;
         uint64_t row = 0;
         uint32_t b = 0;
         for (uint64_t i = 0; i < n; i++) {
@@ -898,19 +990,59 @@ vxg_status Planner::strings_into(const vxg_array& a, uint8_t* views, uint8_t* da
             if (c.dtype != a.dtype) return set_error(VXG_ERR_MISMATCHED_TYPES, "Chunks must have the ChunkedArray's dtype");
             uint32_t k;
             VXG_TRY(string_buffer_count(c, k));
-            void* cv = nullptr;  // the chunk's own validity (null views are all-zero)
-            const vxg_array* vn;
-            int vk;
-            VXG_TRY(validity_source(c, &vn, &vk));
-            if (vk != 0) {
-                VXG_TRY(temp(((c.len + 31) / 32) * 4, &cv));
-                VXG_TRY(validity_into(c, &cv));
+            if (dict_batchable(c)) {
+                const vxg_array& v = c.children[0];
+                const void *po, *pb;
+                VXG_TRY(view_primitive(v.children[0], &po));
+                VXG_TRY(view_primitive(v.children[1], &pb));
+                VarBinChunk d{};
+                d.src = static_cast<const uint8_t*>(pb);
+                d.dst = data + bufs[b].offset;
+                d.offsets = po;
+                d.views = dviews;
+                d.bytes = bufs[b].len;
+                d.n = v.len;
+                d.offs_width = uint32_t(width(v.children[0]));
+                d.bidx = bidx + b;
+                dicts.push_back(d);
+                UnpackArgs ua{};
+                ua.dict = dviews;
+                ua.dict_len = v.len;
+                dviews += 16 * v.len;
+                k1_batch_ = &jobs;
+                patch_batch_ = &patches;
+                const vxg_status st = decode_bitpacked(c.children[1], Epi::Dict, 16, ua, views + 16 * row);
+                k1_batch_ = nullptr;
+                patch_batch_ = nullptr;
+                VXG_TRY(st);
+            } else {
+                void* cv = nullptr;  // the chunk's own validity (null views are all-zero)
+                const vxg_array* vn;
+                int vk;
+                VXG_TRY(validity_source(c, &vn, &vk));
+                if (vk != 0) {
+                    VXG_TRY(temp(((c.len + 31) / 32) * 4, &cv));
+                    VXG_TRY(validity_into(c, &cv));
+                }
+                VXG_TRY(strings_into(c, views + 16 * row, data, bufs + b, bidx + b, static_cast<const uint8_t*>(cv)));
             }
-            VXG_TRY(strings_into(c, views + 16 * row, data, bufs + b, bidx + b, static_cast<const uint8_t*>(cv)));
             row += c.len;
             b += k;
         }
         if (row != a.len) return set_error(VXG_ERR_INVALID_ARGUMENT, "Chunked len != sum of chunk lens");
+        for (size_t i = 0; i < dicts.size(); i += kVarBinArgChunks) {
+            VarBinTable tab{};
+            uint64_t groups = 0;
+            for (size_t j = i; j < dicts.size() && j - i < size_t(kVarBinArgChunks); j++) {
+                VarBinChunk& d = tab.c[tab.n++];
+                d = dicts[j];
+                d.first_group = groups;
+                groups += d.n ? (d.n + 255) / 256 : 1;
+            }
+            VXG_TRY(launch_varbin_chunks(tab, groups, s_));
+        }
+        VXG_TRY(launch_k1_jobs(jobs, ctx_->c.err_word, s_));
+        for (const PatchJob& p : patches) VXG_TRY(apply_sparse_patches(*p.sp, p.T, p.epi, p.vw, p.a, p.dst, p.out_len));
         return VXG_OK;
     }
     default:

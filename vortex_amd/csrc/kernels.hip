@@ -538,6 +538,59 @@ vxg_status launch_runend(int value_width, const void* values, int ends_width, co
     return hip_check(hipGetLastError(), "runend_kernel");
 }
 
+// Chunk-table form: workgroup g expands outputs [2048 (g - first_group), +2048) of one chunk.
+template <typename V>
+__global__ __launch_bounds__(kBlock) void runend_chunks_kernel(RunEndTable tab) {
+    constexpr int ITEMS = 8;
+    uint32_t lo = 0, hi = tab.n;
+    const uint64_t g = blockIdx.x;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (tab.c[mid].first_group <= g) lo = mid; else hi = mid;
+    }
+    const RunEndChunk& c = tab.c[lo];
+    const V* __restrict__ values = static_cast<const V*>(c.values);
+    V* __restrict__ out = static_cast<V*>(c.out);
+    const int ew = int(c.ends_width);
+    const uint64_t j0 = ((g - c.first_group) * kBlock + threadIdx.x) * ITEMS;
+    if (j0 >= c.len) return;
+    uint64_t rlo = 0, rhi = c.n_runs;
+    while (rlo < rhi) {
+        const uint64_t mid = (rlo + rhi) >> 1;
+        if (load_uint(c.ends, ew, false, mid) - c.offset > j0) rhi = mid; else rlo = mid + 1;
+    }
+    uint64_t r = rlo;
+    if (r >= c.n_runs) {
+        __hip_atomic_fetch_or(tab.err, kErrRunEnd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    uint64_t end = load_uint(c.ends, ew, false, r) - c.offset;
+#pragma unroll
+    for (int k = 0; k < ITEMS; k++) {
+        const uint64_t j = j0 + k;
+        if (j >= c.len) break;
+        while (end <= j && r + 1 < c.n_runs) {
+            r++;
+            end = load_uint(c.ends, ew, false, r) - c.offset;
+        }
+        nt_store(out + j, values[r]);
+    }
+}
+
+vxg_status launch_runend_chunks(int value_width, const RunEndTable& t, uint64_t groups, hipStream_t s) {
+    if (groups == 0) return VXG_OK;
+    switch (value_width) {
+#define RE_CASE(W)                                                                                  \
+    case W:                                                                                         \
+        hipLaunchKernelGGL((runend_chunks_kernel<typename UInt<W>::t>), dim3(unsigned(groups)), dim3(kBlock), 0, s, t); \
+        break;
+        RE_CASE(1) RE_CASE(2) RE_CASE(4) RE_CASE(8) RE_CASE(16)
+#undef RE_CASE
+    default: return VXG_ERR_INVALID_ARGUMENT;
+    }
+    return hip_check(hipGetLastError(), "runend_chunks_kernel");
+}
+
 // ------------------------------------------------------------------ K10 fill
 template <typename V>
 __global__ __launch_bounds__(kBlock) void fill_kernel(V v, uint64_t n, V* __restrict__ out) {
@@ -611,6 +664,34 @@ vxg_status launch_varbin_views(const uint8_t* heap, int offs_width, const void* 
     hipLaunchKernelGGL(varbin_views_kernel, dim3(grid_for(n)), dim3(kBlock), 0, s, heap, offsets,
                        offs_width, n, validity, bidx, reinterpret_cast<uint4*>(views));
     return hip_check(hipGetLastError(), "varbin_views_kernel");
+}
+
+// Chunk-table VarBin -> views: workgroup g of a chunk copies its share of the bytes into the
+// output data buffer and builds the views of rows [256 (g - first_group), +256).
+__global__ __launch_bounds__(kBlock) void varbin_chunks_kernel(VarBinTable tab) {
+    uint32_t lo = 0, hi = tab.n;
+    const uint64_t g = blockIdx.x;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (tab.c[mid].first_group <= g) lo = mid; else hi = mid;
+    }
+    const VarBinChunk& c = tab.c[lo];
+    const uint64_t lg = g - c.first_group;
+    const uint64_t ng = (c.n + kBlock - 1) / kBlock > 0 ? (c.n + kBlock - 1) / kBlock : 1;
+    const uint64_t per = (c.bytes + ng - 1) / ng;
+    for (uint64_t b = lg * per + threadIdx.x; b < c.bytes && b < (lg + 1) * per; b += kBlock) c.dst[b] = c.src[b];
+    const uint64_t i = lg * kBlock + threadIdx.x;
+    if (i < c.n) {
+        const uint64_t a = load_uint(c.offsets, int(c.offs_width), c.offs_width < 8, i);
+        const uint64_t e = load_uint(c.offsets, int(c.offs_width), c.offs_width < 8, i + 1);
+        reinterpret_cast<uint4*>(c.views)[i] = make_view(c.src, a, uint32_t(e - a), c.bidx);
+    }
+}
+
+vxg_status launch_varbin_chunks(const VarBinTable& t, uint64_t groups, hipStream_t s) {
+    if (groups == 0) return VXG_OK;
+    hipLaunchKernelGGL(varbin_chunks_kernel, dim3(unsigned(groups)), dim3(kBlock), 0, s, t);
+    return hip_check(hipGetLastError(), "varbin_chunks_kernel");
 }
 
 // pack_views (chunked/canonical.rs:214-231): copy views, adding `add` to the buffer_index of

@@ -163,6 +163,45 @@ vxg_status launch_delta(int width, const void* bases, const void* deltas, uint64
 vxg_status launch_runend(int value_width, const void* values, int ends_width, const void* ends,
                          uint64_t n_runs, uint64_t offset, uint64_t len, void* out, uint32_t* err,
                          hipStream_t s);
+// Batched RunEnd expansion: many chunks' runs in one launch (chunk table as kernel argument).
+struct RunEndChunk {
+    const void* values;
+    const void* ends;
+    void* out;
+    uint64_t n_runs;
+    uint64_t offset;
+    uint64_t len;
+    uint64_t first_group;  // first workgroup of this chunk (2048 outputs per workgroup)
+    uint32_t ends_width;
+};
+constexpr int kRunEndArgChunks = 48;
+struct RunEndTable {
+    RunEndChunk c[kRunEndArgChunks];
+    uint32_t n;
+    uint32_t* err;
+};
+vxg_status launch_runend_chunks(int value_width, const RunEndTable& t, uint64_t groups, hipStream_t s);
+
+// Batched VarBin -> views (+ copy of the bytes into the output's data buffer), e.g. the
+// dictionaries of a chunked Dict(VarBin) string column.
+struct VarBinChunk {
+    const uint8_t* src;      // VarBin bytes
+    uint8_t* dst;            // data buffer in the canonical output
+    const void* offsets;
+    uint8_t* views;          // 16 B per row
+    uint64_t bytes;          // bytes to copy
+    uint64_t n;              // rows
+    uint64_t first_group;
+    uint32_t offs_width;
+    uint32_t bidx;
+};
+constexpr int kVarBinArgChunks = 48;
+struct VarBinTable {
+    VarBinChunk c[kVarBinArgChunks];
+    uint32_t n;
+};
+vxg_status launch_varbin_chunks(const VarBinTable& t, uint64_t groups, hipStream_t s);
+
 vxg_status launch_fill(int value_width, const uint8_t* scalar16, uint64_t n, void* out,
                        hipStream_t s);
 uint64_t fsst_scratch_bytes(uint64_t n);
