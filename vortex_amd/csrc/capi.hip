@@ -222,6 +222,7 @@ class Planner {
     };
     std::vector<K1Job>* k1_batch_ = nullptr;
     std::vector<PatchJob>* patch_batch_ = nullptr;
+    std::vector<FsstChunk>* fsst_batch_ = nullptr;  // FSST chunks of a chunked string array
     bool k1_fusable(const vxg_array& c) const;
 
     vxg_status temp(uint64_t bytes, void** p) {
@@ -922,14 +923,26 @@ vxg_status Planner::strings_into(const vxg_array& a, uint8_t* views, uint8_t* da
         VXG_TRY(view_primitive(*sym, &psym));
         VXG_TRY(view_primitive(*slen, &pslen));
         VXG_TRY(view_primitive(*child(*codes, 1), &pcb));
-        IntCol offs, lens;  // read in place by the FSST kernels (packed columns stay packed)
-        VXG_TRY(int_column(*child(*codes, 0), offs));
-        VXG_TRY(int_column(*ulen, lens));
+        FsstChunk f{};
+        f.symbols = static_cast<const uint64_t*>(psym);
+        f.sym_lens = static_cast<const uint8_t*>(pslen);
+        f.n_symbols = unsigned(sym->len);
+        f.codes = static_cast<const uint8_t*>(pcb);
+        VXG_TRY(int_column(*child(*codes, 0), f.offs));  // read in place by the FSST kernels
+        VXG_TRY(int_column(*ulen, f.lens));              // (packed columns stay packed)
+        f.n = a.len;
+        f.validity = validity;
+        f.heap = data + bufs[0].offset;
+        f.views = views;
+        f.bidx = bidx;
+        if (fsst_batch_) {  // a chunk: decoded with the other FSST chunks
+            fsst_batch_->push_back(f);
+            return VXG_OK;
+        }
+        std::vector<FsstChunk> one{f};
         void* scratch;
-        VXG_TRY(temp(fsst_scratch_bytes(a.len), &scratch));
-        return launch_fsst(static_cast<const uint64_t*>(psym), static_cast<const uint8_t*>(pslen),
-                           unsigned(sym->len), static_cast<const uint8_t*>(pcb), offs, lens, a.len, validity, scratch,
-                           data + bufs[0].offset, views, bidx, ctx_->c.err_word, s_);
+        VXG_TRY(temp(fsst_batch_scratch_bytes(one.data(), 1), &scratch));
+        return launch_fsst_batch(one, scratch, ctx_->c.err_word, s_);
     }
     case VXG_ENC_DICT: {
         // Dict over string values: take on the values' views (varbinview/compute.rs:68-76); the
@@ -983,6 +996,7 @@ vxg_status Planner::strings_into(const vxg_array& a, uint8_t* views, uint8_t* da
         std::vector<VarBinChunk> dicts;
         std::vector<K1Job> jobs;
         std::vector<PatchJob> patches;
+        std::vector<FsstChunk> fssts;
         uint64_t row = 0;
         uint32_t b = 0;
         for (uint64_t i = 0; i < n; i++) {
@@ -1024,12 +1038,21 @@ vxg_status Planner::strings_into(const vxg_array& a, uint8_t* views, uint8_t* da
                     VXG_TRY(temp(((c.len + 31) / 32) * 4, &cv));
                     VXG_TRY(validity_into(c, &cv));
                 }
-                VXG_TRY(strings_into(c, views + 16 * row, data, bufs + b, bidx + b, static_cast<const uint8_t*>(cv)));
+                if (c.encoding == VXG_ENC_FSST) fsst_batch_ = &fssts;
+                const vxg_status st =
+                    strings_into(c, views + 16 * row, data, bufs + b, bidx + b, static_cast<const uint8_t*>(cv));
+                fsst_batch_ = nullptr;
+                VXG_TRY(st);
             }
             row += c.len;
             b += k;
         }
         if (row != a.len) return set_error(VXG_ERR_INVALID_ARGUMENT, "Chunked len != sum of chunk lens");
+        if (!fssts.empty()) {
+            void* scratch;
+            VXG_TRY(temp(fsst_batch_scratch_bytes(fssts.data(), fssts.size()), &scratch));
+            VXG_TRY(launch_fsst_batch(fssts, scratch, ctx_->c.err_word, s_));
+        }
         for (size_t i = 0; i < dicts.size(); i += kVarBinArgChunks) {
             VarBinTable tab{};
             uint64_t groups = 0;
@@ -1394,15 +1417,23 @@ vxg_status vxg_fsst_decode(vxg_ctx* ctx, const uint64_t* symbols, const uint8_t*
     VXG_TRY(use_device(ctx));
     if (!ptype_is_int(offs_ptype) || !ptype_is_int(lens_ptype))
         return set_error(VXG_ERR_MISMATCHED_TYPES, "FSST offsets/lengths must be integers");
-    IntCol offs{}, ls{};
-    offs.p = code_offsets;
-    offs.width = ptype_width(offs_ptype);
-    offs.sgn = ptype_is_signed(offs_ptype);
-    ls.p = lens;
-    ls.width = ptype_width(lens_ptype);
-    ls.sgn = ptype_is_signed(lens_ptype);
-    return launch_fsst(symbols, sym_lens, n_symbols, code_bytes, offs, ls, n, validity, scratch, heap, views, 0,
-                       ctx->c.err_word, S(stream));
+    FsstChunk f{};
+    f.symbols = symbols;
+    f.sym_lens = sym_lens;
+    f.n_symbols = n_symbols;
+    f.codes = code_bytes;
+    f.offs.p = code_offsets;
+    f.offs.width = ptype_width(offs_ptype);
+    f.offs.sgn = ptype_is_signed(offs_ptype);
+    f.lens.p = lens;
+    f.lens.width = ptype_width(lens_ptype);
+    f.lens.sgn = ptype_is_signed(lens_ptype);
+    f.n = n;
+    f.validity = validity;
+    f.heap = heap;
+    f.views = views;
+    std::vector<FsstChunk> one{f};
+    return launch_fsst_batch(one, scratch, ctx->c.err_word, S(stream));
 }
 
 vxg_status vxg_fill(vxg_ctx* ctx, unsigned value_width, const void* scalar_host, uint64_t n, void* out,

@@ -24,6 +24,9 @@
 //   A tile whose codes do not decode to exactly the sum of its lengths raises an error (the
 //   reference would slice a shifted stream); tiles too large for the LDS images take a
 //   per-string direct-to-HBM path that checks every string.
+#include <algorithm>
+#include <tuple>
+
 #include "fl_unpack_impl.hpp"
 #include "intcol.hpp"
 
@@ -148,26 +151,41 @@ __device__ __forceinline__ int block_excl_scan32(int v, int* ws, int& total) {
 // Pre-pass: per workgroup of 128 tiles, the tile length sums, their exclusive scan
 // (tile_prefix) and the workgroup total (block_totals).  The decode adds the totals of the
 // preceding workgroups (<= a few hundred) itself.
-template <class LenAcc>
-__device__ __forceinline__ void scan_tile_sums(const int64_t* s_ts, int64_t* ws, uint64_t n_tiles,
+__device__ __forceinline__ void scan_tile_sums(const int64_t* s_ts, int64_t* ws, uint64_t n_tiles, uint64_t sb,
                                                int64_t* __restrict__ tile_prefix, int64_t* __restrict__ block_totals) {
+    // sb = scan block within the chunk; tile_prefix / block_totals point at the chunk's slices
     const int tid = threadIdx.x;
     int64_t tot;
     const int64_t ex = block_exclusive_scan<kTile / 64>(tid < kScanTiles ? s_ts[tid] : 0, ws, tot);
-    const uint64_t tt = uint64_t(blockIdx.x) * kScanTiles + tid;
+    const uint64_t tt = sb * kScanTiles + tid;
     if (tid < kScanTiles && tt < n_tiles) tile_prefix[tt] = ex;
-    if (tid == 0) block_totals[blockIdx.x] = tot;
+    if (tid == 0) block_totals[sb] = tot;
+}
+
+// Chunk of workgroup g in a launch (workgroup-uniform binary search on the table's first_*).
+template <bool SCAN>
+__device__ __forceinline__ const FsstChunk& fsst_chunk_of(const FsstTable& tab, uint64_t g) {
+    uint32_t lo = 0, hi = tab.n;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if ((SCAN ? tab.c[mid].first_scan : tab.c[mid].first_tile) <= g) lo = mid; else hi = mid;
+    }
+    return tab.c[lo];
 }
 
 // Any length column: wave w sums tile 4r + w in round r (4 consecutive lengths per lane).
 template <class LenAcc>
-__global__ __launch_bounds__(kTile) void fsst_tile_scan(LenAcc lens, uint64_t n, uint64_t n_tiles,
-                                                        int64_t* __restrict__ tile_prefix,
-                                                        int64_t* __restrict__ block_totals) {
+__global__ __launch_bounds__(kTile) void fsst_tile_scan(FsstTable tab, int64_t* __restrict__ tile_prefix_all,
+                                                        int64_t* __restrict__ block_totals_all) {
     __shared__ int64_t s_ts[kScanTiles];
     __shared__ int64_t ws[kTile / 64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t t0 = uint64_t(blockIdx.x) * kScanTiles;
+    const FsstChunk& c = fsst_chunk_of<true>(tab, blockIdx.x);
+    const LenAcc lens(c.lens);
+    const uint64_t n = c.n, n_tiles = (n + kTile - 1) / kTile, sb = blockIdx.x - c.first_scan;
+    int64_t* const tile_prefix = tile_prefix_all + c.first_tile;
+    int64_t* const block_totals = block_totals_all + c.first_scan;
+    const uint64_t t0 = sb * kScanTiles;
     for (int r0 = 0; r0 < kScanTiles / 4; r0 += 8) {
         int64_t v[8];
 #pragma unroll
@@ -189,7 +207,7 @@ __global__ __launch_bounds__(kTile) void fsst_tile_scan(LenAcc lens, uint64_t n,
         }
     }
     __syncthreads();
-    scan_tile_sums<LenAcc>(s_ts, ws, n_tiles, tile_prefix, block_totals);
+    scan_tile_sums(s_ts, ws, n_tiles, sb, tile_prefix, block_totals);
 }
 
 // Patch-free FoR(BitPacked u32/i32) lengths with offset 0 (the reference cascade): decode
@@ -215,14 +233,19 @@ __device__ __forceinline__ void fl32_tile_rows(const Vec16<32>* p, int t, uint64
 }
 
 template <int W>
-__global__ __launch_bounds__(kTile) void fsst_tile_scan_fl32(const uint8_t* __restrict__ packed, uint32_t shift,
-                                                             uint32_t reference, bool sgn, uint64_t n,
-                                                             uint64_t n_tiles, int64_t* __restrict__ tile_prefix,
-                                                             int64_t* __restrict__ block_totals) {
+__global__ __launch_bounds__(kTile) void fsst_tile_scan_fl32(FsstTable tab, int64_t* __restrict__ tile_prefix_all,
+                                                             int64_t* __restrict__ block_totals_all) {
     __shared__ int64_t s_ts[kScanTiles];
     __shared__ int64_t ws[kTile / 64];
     const int tid = threadIdx.x, t = tid & 7;
-    const uint64_t blk = uint64_t(blockIdx.x) * (kScanTiles / 4) + (tid >> 3);
+    const FsstChunk& c = fsst_chunk_of<true>(tab, blockIdx.x);
+    const uint8_t* __restrict__ packed = static_cast<const uint8_t*>(c.lens.p);
+    const uint32_t shift = c.lens.shift, reference = uint32_t(c.lens.reference);
+    const bool sgn = c.lens.sgn;
+    const uint64_t n = c.n, n_tiles = (n + kTile - 1) / kTile, sb = blockIdx.x - c.first_scan;
+    int64_t* const tile_prefix = tile_prefix_all + c.first_tile;
+    int64_t* const block_totals = block_totals_all + c.first_scan;
+    const uint64_t blk = sb * (kScanTiles / 4) + (tid >> 3);
     int64_t acc[4] = {0, 0, 0, 0};
     if (blk * 1024 < n) {
         Vec16<32> p[W > 0 ? W : 1];
@@ -242,19 +265,27 @@ __global__ __launch_bounds__(kTile) void fsst_tile_scan_fl32(const uint8_t* __re
         for (int k = 0; k < 4; k++) s_ts[(tid >> 3) * 4 + k] = acc[k];
     }
     __syncthreads();
-    scan_tile_sums<void>(s_ts, ws, n_tiles, tile_prefix, block_totals);
+    scan_tile_sums(s_ts, ws, n_tiles, sb, tile_prefix, block_totals);
 }
 
 template <class OffAcc, class LenAcc>
-__global__ __launch_bounds__(kTile) void fsst_decode(const uint64_t* __restrict__ symbols,
-                                                     const uint8_t* __restrict__ sym_lens, unsigned n_symbols,
-                                                     const uint8_t* __restrict__ codes, OffAcc code_offs,
-                                                     LenAcc lens, uint64_t n,
-                                                     const uint8_t* __restrict__ validity,
-                                                     const int64_t* __restrict__ tile_prefix,
-                                                     const int64_t* __restrict__ block_totals,
-                                                     uint8_t* __restrict__ heap, uint4* __restrict__ views,
-                                                     uint32_t bidx, uint32_t* __restrict__ err) {
+__global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, const int64_t* __restrict__ tile_prefix_all,
+                                                     const int64_t* __restrict__ block_totals_all,
+                                                     uint32_t* __restrict__ err) {
+    const FsstChunk& ch = fsst_chunk_of<false>(tab, blockIdx.x);
+    const uint64_t* __restrict__ symbols = ch.symbols;
+    const uint8_t* __restrict__ sym_lens = ch.sym_lens;
+    const unsigned n_symbols = ch.n_symbols;
+    const uint8_t* __restrict__ codes = ch.codes;
+    const OffAcc code_offs(ch.offs);
+    const LenAcc lens(ch.lens);
+    const uint64_t n = ch.n;
+    const uint8_t* __restrict__ validity = ch.validity;
+    const int64_t* __restrict__ tile_prefix = tile_prefix_all + ch.first_tile;
+    const int64_t* __restrict__ block_totals = block_totals_all + ch.first_scan;
+    uint8_t* __restrict__ heap = ch.heap;
+    uint4* __restrict__ views = reinterpret_cast<uint4*>(ch.views);
+    const uint32_t bidx = ch.bidx;
     __shared__ uint64_t s_sym[256];
     __shared__ uint8_t s_len[256];
     __shared__ int ws_a[kTile / 64], ws_b[kTile / 64];
@@ -267,7 +298,7 @@ __global__ __launch_bounds__(kTile) void fsst_decode(const uint64_t* __restrict_
     uint8_t* const s_heap = reinterpret_cast<uint8_t*>(s_heap32);
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const uint32_t tile = blockIdx.x;
+    const uint32_t tile = uint32_t(blockIdx.x - ch.first_tile);
     {
         const uint32_t sk = uint32_t(tid) < n_symbols ? uint32_t(tid) : 0;
         const uint64_t sym_v = symbols[sk];
@@ -480,61 +511,99 @@ uint64_t fsst_scratch_bytes(uint64_t n) {
     return (n_tiles + (n_tiles + kScanTiles - 1) / kScanTiles + 2) * sizeof(int64_t);
 }
 
-template <int... Ws>
-static void launch_tile_scan_fl32(int W, dim3 grid, hipStream_t s, const IntCol& c, uint64_t n, uint64_t n_tiles,
-                                  int64_t* tiles, int64_t* blocks, std::integer_sequence<int, Ws...>) {
-    using Fn = void (*)(const uint8_t*, uint32_t, uint32_t, bool, uint64_t, uint64_t, int64_t*, int64_t*);
-    static constexpr Fn table[] = {&fsst_tile_scan_fl32<Ws>...};
-    hipLaunchKernelGGL(table[W], grid, dim3(kTile), 0, s, static_cast<const uint8_t*>(c.p), c.shift,
-                       uint32_t(c.reference), c.sgn, n, n_tiles, tiles, blocks);
+uint64_t fsst_batch_scratch_bytes(const FsstChunk* chunks, size_t n_chunks) {
+    uint64_t b = 16;
+    for (size_t i = 0; i < n_chunks; i++) b += fsst_scratch_bytes(chunks[i].n);
+    return b;
 }
 
-vxg_status launch_fsst(const uint64_t* symbols, const uint8_t* sym_lens, unsigned n_symbols,
-                       const uint8_t* code_bytes, const IntCol& offs, const IntCol& lens, uint64_t n,
-                       const uint8_t* validity, void* scratch, uint8_t* heap, uint8_t* views,
-                       uint32_t bidx, uint32_t* err, hipStream_t s) {
-    if (n == 0) return VXG_OK;
-    if (n_symbols > 255) return set_error(VXG_ERR_INVALID_ARGUMENT, "FSST symbol table > 255 entries");
-    const uint64_t n_tiles = (n + kTile - 1) / kTile;
-    if (n_tiles > 0xFFFFFFFFull) return set_error(VXG_ERR_INVALID_ARGUMENT, "FSST array too long");
-    const uint64_t n_scan = (n_tiles + kScanTiles - 1) / kScanTiles;
-    int64_t* tiles = static_cast<int64_t*>(scratch);
-    int64_t* blocks = tiles + n_tiles;
-    const bool fl32 = lens.packed && lens.width == 4 && lens.offset == 0 && lens.W <= 32;
-    if (fl32)
-        launch_tile_scan_fl32(int(lens.W), dim3(unsigned(n_scan)), s, lens, n, n_tiles, tiles, blocks,
-                              std::make_integer_sequence<int, 33>{});
-    auto run = [&](auto off_acc, auto len_acc) {
-        using OA = decltype(off_acc);
-        using LA = decltype(len_acc);
-        if (!fl32)
-            hipLaunchKernelGGL((fsst_tile_scan<LA>), dim3(unsigned(n_scan)), dim3(kTile), 0, s, len_acc, n, n_tiles,
-                               tiles, blocks);
-        hipLaunchKernelGGL((fsst_decode<OA, LA>), dim3(unsigned(n_tiles)), dim3(kTile), 0, s, symbols, sym_lens,
-                           n_symbols, code_bytes, off_acc, len_acc, n, validity, tiles, blocks, heap,
-                           reinterpret_cast<uint4*>(views), bidx, err);
-    };
-    // accessor = plain width 1/2/4/8 or packed T = 32/64
-    auto with = [](const IntCol& c, auto&& f) -> bool {
-        if (c.packed) {
-            if (c.width == 4) return f(PackedCol<32>(c)), true;
-            if (c.width == 8) return f(PackedCol<64>(c)), true;
-            return false;
+namespace {
+
+// Kernel key of a chunk: accessor kind of offsets and lengths (plain width 1/2/4/8 or packed
+// T = 32/64) and, for the FastLanes lengths pre-pass, the lengths' bit width.
+int acc_kind(const IntCol& c) { return c.packed ? (c.width == 4 ? 32 : 64) : c.width; }
+bool fl32_lens(const IntCol& c) { return c.packed && c.width == 4 && c.offset == 0 && c.W <= 32; }
+std::tuple<int, int, int> fsst_key(const FsstChunk& c) {
+    return {acc_kind(c.offs), acc_kind(c.lens), fl32_lens(c.lens) ? int(c.lens.W) : -1};
+}
+
+template <int... Ws>
+void launch_tile_scan_fl32(int W, dim3 grid, hipStream_t s, const FsstTable& t, int64_t* tiles, int64_t* blocks,
+                           std::integer_sequence<int, Ws...>) {
+    using Fn = void (*)(FsstTable, int64_t*, int64_t*);
+    static constexpr Fn table[] = {&fsst_tile_scan_fl32<Ws>...};
+    hipLaunchKernelGGL(table[W], grid, dim3(kTile), 0, s, t, tiles, blocks);
+}
+
+// accessor = plain width 1/2/4/8 or packed T = 32/64
+template <class F>
+bool with_acc(int kind, F&& f) {
+    switch (kind) {
+    case 1: f(static_cast<PlainCol<1>*>(nullptr)); return true;
+    case 2: f(static_cast<PlainCol<2>*>(nullptr)); return true;
+    case 4: f(static_cast<PlainCol<4>*>(nullptr)); return true;
+    case 8: f(static_cast<PlainCol<8>*>(nullptr)); return true;
+    case 32: f(static_cast<PackedCol<32>*>(nullptr)); return true;
+    case 64: f(static_cast<PackedCol<64>*>(nullptr)); return true;
+    default: return false;
+    }
+}
+
+}  // namespace
+
+vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint32_t* err, hipStream_t s) {
+    for (const FsstChunk& c : chunks) {
+        if (c.n_symbols > 255) return set_error(VXG_ERR_INVALID_ARGUMENT, "FSST symbol table > 255 entries");
+        if ((c.n + kTile - 1) / kTile > 0xFFFFFFFFull) return set_error(VXG_ERR_INVALID_ARGUMENT, "FSST array too long");
+        if (acc_kind(c.offs) == 0 || acc_kind(c.lens) == 0 || (c.offs.packed && c.offs.width != 4 && c.offs.width != 8) ||
+            (c.lens.packed && c.lens.width != 4 && c.lens.width != 8))
+            return set_error(VXG_ERR_MISMATCHED_TYPES, "FSST offsets/lengths must be 1/2/4/8-byte integers "
+                                                        "(packed: 32/64-bit)");
+    }
+    std::stable_sort(chunks.begin(), chunks.end(),
+                     [](const FsstChunk& a, const FsstChunk& b) { return fsst_key(a) < fsst_key(b); });
+    int64_t* tiles_all = static_cast<int64_t*>(scratch);
+    size_t i = 0;
+    while (i < chunks.size()) {
+        FsstTable tab{};
+        uint64_t tiles = 0, scans = 0;
+        size_t j = i;
+        for (; j < chunks.size() && j - i < size_t(kFsstArgChunks) && fsst_key(chunks[j]) == fsst_key(chunks[i]); j++) {
+            if (chunks[j].n == 0) continue;
+            FsstChunk& c = tab.c[tab.n++];
+            c = chunks[j];
+            const uint64_t nt = (c.n + kTile - 1) / kTile;
+            c.first_tile = tiles;
+            c.first_scan = scans;
+            tiles += nt;
+            scans += (nt + kScanTiles - 1) / kScanTiles;
         }
-        switch (c.width) {
-        case 1: return f(PlainCol<1>(c)), true;
-        case 2: return f(PlainCol<2>(c)), true;
-        case 4: return f(PlainCol<4>(c)), true;
-        case 8: return f(PlainCol<8>(c)), true;
-        default: return false;
+        if (tab.n) {
+            int64_t* tp = tiles_all;
+            int64_t* bt = tiles_all + tiles;
+            tiles_all += tiles + scans;
+            const auto key = fsst_key(tab.c[0]);
+            if (std::get<2>(key) >= 0)
+                launch_tile_scan_fl32(std::get<2>(key), dim3(unsigned(scans)), s, tab, tp, bt,
+                                      std::make_integer_sequence<int, 33>{});
+            bool ok = true;
+            with_acc(std::get<0>(key), [&](auto* oa) {
+                ok = with_acc(std::get<1>(key), [&](auto* la) {
+                    using OA = std::remove_pointer_t<decltype(oa)>;
+                    using LA = std::remove_pointer_t<decltype(la)>;
+                    if (std::get<2>(key) < 0)
+                        hipLaunchKernelGGL((fsst_tile_scan<LA>), dim3(unsigned(scans)), dim3(kTile), 0, s, tab, tp, bt);
+                    hipLaunchKernelGGL((fsst_decode<OA, LA>), dim3(unsigned(tiles)), dim3(kTile), 0, s, tab, tp, bt,
+                                       err);
+                });
+            });
+            if (!ok) return set_error(VXG_ERR_MISMATCHED_TYPES, "FSST accessor");
+            const vxg_status st = hip_check(hipGetLastError(), "fsst kernels");
+            if (st != VXG_OK) return st;
         }
-    };
-    bool ok = true;
-    const bool ok_off = with(offs, [&](auto oa) { ok = with(lens, [&](auto la) { run(oa, la); }); });
-    if (!ok_off || !ok)
-        return set_error(VXG_ERR_MISMATCHED_TYPES, "FSST offsets/lengths must be 1/2/4/8-byte integers "
-                                                    "(packed: 32/64-bit)");
-    return hip_check(hipGetLastError(), "fsst kernels");
+        i = j;
+    }
+    return VXG_OK;
 }
 
 }  // namespace vxg

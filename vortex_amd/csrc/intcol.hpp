@@ -51,7 +51,7 @@ __device__ __forceinline__ int64_t fl_get(const void* packed, uint32_t W, uint32
 template <int WIDTH> struct PlainCol {
     const void* p;
     bool sgn;
-    explicit PlainCol(const IntCol& c) : p(c.p), sgn(c.sgn) {}
+    __host__ __device__ explicit PlainCol(const IntCol& c) : p(c.p), sgn(c.sgn) {}
     __device__ __forceinline__ int64_t operator()(uint64_t i) const {
         const int64_t u = ld<WIDTH, false>(p, i);
         if constexpr (WIDTH == 8) return u;
@@ -63,7 +63,7 @@ template <int T> struct PackedCol {
     uint32_t W, shift, offset;
     uint64_t reference;
     bool sgn;
-    explicit PackedCol(const IntCol& c)
+    __host__ __device__ explicit PackedCol(const IntCol& c)
         : p(c.p), W(c.W), shift(c.shift), offset(c.offset), reference(c.reference), sgn(c.sgn) {}
     __device__ __forceinline__ int64_t operator()(uint64_t i) const {
         return fl_get<T>(p, W, shift, offset, reference, sgn, i);

@@ -5,6 +5,7 @@
 
 #include <cstdint>
 #include <string>
+#include <vector>
 
 #include "../../include/vortex_gpu.h"
 
@@ -204,11 +205,33 @@ vxg_status launch_varbin_chunks(const VarBinTable& t, uint64_t groups, hipStream
 
 vxg_status launch_fill(int value_width, const uint8_t* scalar16, uint64_t n, void* out,
                        hipStream_t s);
+// One FSST -> VarBinView decode (a whole array or one chunk of a ChunkedArray).
+struct FsstChunk {
+    const uint64_t* symbols;
+    const uint8_t* sym_lens;
+    const uint8_t* codes;
+    const uint8_t* validity;  // LSB bitmap or NULL
+    uint8_t* heap;            // the chunk's data buffer
+    uint8_t* views;           // 16 B per row
+    IntCol offs;              // codes VarBin offsets (n + 1)
+    IntCol lens;              // uncompressed lengths (n)
+    uint64_t n;
+    uint64_t first_tile;      // launch-local: first 256-string tile / first 128-tile scan block
+    uint64_t first_scan;
+    uint32_t n_symbols;
+    uint32_t bidx;            // buffer_index of non-inlined views
+};
+constexpr int kFsstArgChunks = 16;
+struct FsstTable {
+    FsstChunk c[kFsstArgChunks];
+    uint32_t n;
+};
+// Scratch for a set of chunks (tile prefixes + scan-block totals).
 uint64_t fsst_scratch_bytes(uint64_t n);
-vxg_status launch_fsst(const uint64_t* symbols, const uint8_t* sym_lens, unsigned n_symbols,
-                       const uint8_t* code_bytes, const IntCol& offs, const IntCol& lens, uint64_t n,
-                       const uint8_t* validity, void* scratch, uint8_t* heap, uint8_t* views,
-                       uint32_t bidx, uint32_t* err, hipStream_t s);
+uint64_t fsst_batch_scratch_bytes(const FsstChunk* chunks, size_t n_chunks);
+// Decode every chunk: grouped by accessor kinds, kFsstArgChunks per launch pair (pre-pass +
+// decode).  `scratch` >= fsst_batch_scratch_bytes.
+vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint32_t* err, hipStream_t s);
 // Views carry `bidx` as the buffer_index of non-inlined rows.
 vxg_status launch_varbin_views(const uint8_t* heap, int offs_width, const void* offsets, uint64_t n,
                                const uint8_t* validity, uint32_t bidx, uint8_t* views, hipStream_t s);
