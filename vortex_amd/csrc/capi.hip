@@ -22,6 +22,12 @@ struct vxg_ctx {
     vxg::Ctx c;
 };
 
+// Chunk tables travel as kernel arguments: they must fit the 4 KiB kernarg segment.
+static_assert(sizeof(vxg::ChunkTable) <= 4096, "ChunkTable exceeds the kernarg limit");
+static_assert(sizeof(vxg::FsstTable) <= 4096, "FsstTable exceeds the kernarg limit");
+static_assert(sizeof(vxg::RunEndTable) <= 4096, "RunEndTable exceeds the kernarg limit");
+static_assert(sizeof(vxg::VarBinTable) <= 4096, "VarBinTable exceeds the kernarg limit");
+
 namespace vxg {
 
 const float kF10f[11] = {1.0f, 10.0f, 100.0f, 1000.0f, 10000.0f, 100000.0f, 1000000.0f,
@@ -1236,15 +1242,16 @@ vxg_status vxg_canonical_layout(vxg_ctx* ctx, const vxg_array* a, uint64_t* valu
     if (!a) return set_error(VXG_ERR_INVALID_ARGUMENT, "null array");
     Planner p(ctx, nullptr);
     uint64_t vb = 0, db = 0;
-    VXG_TRY(p.canonical_size(*a, vb, db));
     uint32_t n = 0;
     if (a->dtype == VXG_DTYPE_UTF8 || a->dtype == VXG_DTYPE_BINARY) {
         std::vector<vxg_data_buffer> v;
-        uint64_t ext;
-        VXG_TRY(p.string_layout(*a, v, ext));
+        VXG_TRY(p.string_layout(*a, v, db));
+        vb = 16 * a->len;
         n = uint32_t(v.size());
         if (bufs && cap < n) return set_error(VXG_ERR_INVALID_ARGUMENT, "buffer table too small");
         if (bufs) std::copy(v.begin(), v.end(), bufs);
+    } else {
+        VXG_TRY(p.canonical_size(*a, vb, db));
     }
     if (values_bytes) *values_bytes = vb;
     if (data_bytes) *data_bytes = db;

@@ -285,6 +285,43 @@ __device__ __forceinline__ void unpack_block(const uint8_t* __restrict__ blk_pac
         if (oob) __hip_atomic_fetch_or(ep.err, kErrTakeOOB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Rows [Q*T/S, (Q+1)*T/S) of a block (row split S, quarter Q): only the word rows those rows
+// read are loaded.  Used by small launches (few blocks) to put 4x more threads on the array.
+template <int T, int W, Epi EPI, int VW, int NT, int S, int Q, bool FULL, int... Rs>
+__device__ __forceinline__ void process_rows_part(const Vec16<T>* p, int lane0,
+                                                  typename EpiOut<T, EPI, VW>::type* __restrict__ out,
+                                                  int64_t out_base, uint64_t len, const EpiParams& ep, bool& oob,
+                                                  std::integer_sequence<int, Rs...>) {
+    (process_row<T, W, EPI, VW, NT, Q * (T / S) + Rs, FULL>(p, lane0, out, out_base, len, ep, oob), ...);
+}
+
+template <int T, int W, Epi EPI, int VW, int NT, int S, int Q>
+__device__ __forceinline__ void unpack_block_part(const uint8_t* __restrict__ blk_packed, int t,
+                                                  typename EpiOut<T, EPI, VW>::type* __restrict__ out,
+                                                  int64_t out_base, bool full, uint64_t len,
+                                                  const EpiParams& ep) {
+    using E = typename Fl<T>::E;
+    constexpr int EPV = 16 / int(sizeof(E));
+    constexpr int NW = W > 0 ? W : 1;
+    constexpr int R0 = Q * (T / S), R1 = (Q + 1) * (T / S);
+    constexpr int WLO = W > 0 ? (R0 * W) / T : 0;
+    constexpr int WHI = W > 0 ? (R1 * W - 1) / T : 0;  // inclusive
+    Vec16<T> p[NW];
+    if constexpr (W > 0) {
+#pragma unroll
+        for (int w = WLO; w <= WHI && w < W; w++) p[w] = load16<T>(blk_packed + 128 * w + 16 * t);
+    }
+    bool oob = false;
+    if (full)
+        process_rows_part<T, W, EPI, VW, NT, S, Q, true>(p, t * EPV, out, out_base, len, ep, oob,
+                                                         std::make_integer_sequence<int, T / S>{});
+    else
+        process_rows_part<T, W, EPI, VW, NT, S, Q, false>(p, t * EPV, out, out_base, len, ep, oob,
+                                                          std::make_integer_sequence<int, T / S>{});
+    if constexpr (EPI == Epi::Dict)
+        if (oob) __hip_atomic_fetch_or(ep.err, kErrTakeOOB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Dictionaries up to this size are staged into LDS by every workgroup of a Dict launch: a
 // gather of 64 random 8-byte entries from global memory touches up to 64 cache lines (one
 // TA cycle each), from LDS it is one ds_read_b64 with bank conflicts.
@@ -304,9 +341,13 @@ __device__ __forceinline__ void stage_dict(uint8_t* s_dict, const void* dict, ui
 // 170-187 without the pack copy).  The chunk table travels as the kernel argument (no upload,
 // no host synchronisation); each workgroup of 256 threads covers 32 FastLanes blocks of exactly
 // one chunk, found by a workgroup-uniform binary search on first_group (no search for n = 1).
-template <int T, int W, Epi EPI, int VW, bool LDSD = false>
+// S = 1: 8 threads per block, 32 blocks per workgroup (large launches).  S = 4 (T = 32/64):
+// each wave takes one quarter of the rows of 8 blocks -> 8 blocks per workgroup and 4x the
+// threads, for launches too small to fill 256 CUs (the quarter is wave-uniform, no divergence).
+template <int T, int W, Epi EPI, int VW, bool LDSD = false, int S = 1>
 __global__ __launch_bounds__(256) void fl_unpack_kernel(ChunkTable tab) {
     using O = typename EpiOut<T, EPI, VW>::type;
+    constexpr int BPG = 32 / S;  // blocks per workgroup
     uint32_t lo = 0, hi = tab.n;
     const uint64_t g = blockIdx.x;
     while (hi - lo > 1) {
@@ -314,7 +355,7 @@ __global__ __launch_bounds__(256) void fl_unpack_kernel(ChunkTable tab) {
         if (tab.c[mid].first_group <= g) lo = mid; else hi = mid;
     }
     const ChunkDev& c = tab.c[lo];
-    const uint64_t blk = (g - c.first_group) * 32 + (threadIdx.x >> 3);
+    const uint64_t blk = (g - c.first_group) * BPG + ((threadIdx.x >> 3) % BPG);
     const int t = int(threadIdx.x & 7);
     EpiParams ep;
     ep.reference = c.reference;
@@ -337,25 +378,56 @@ __global__ __launch_bounds__(256) void fl_unpack_kernel(ChunkTable tab) {
     // Decoded output is written once and never re-read by this launch: non-temporal 16-byte
     // stores (measured on C1: 51.1 us vs 63.0 us with plain stores = 80% vs 65% of 8 TB/s,
     // profiles/r01_ubench_k1.txt; a perfectly coalesced copy of the same bytes: 49.2 us).
-    unpack_block<T, W, EPI, VW, kOutNT>(c.packed + blk * (128 * W), t, static_cast<O*>(c.out), out_base, full,
-                                        c.len, ep);
+    const uint8_t* bp = c.packed + blk * (128 * W);
+    if constexpr (S == 1) {
+        unpack_block<T, W, EPI, VW, kOutNT>(bp, t, static_cast<O*>(c.out), out_base, full, c.len, ep);
+    } else {
+        static_assert(S == 4, "row split 1 or 4");
+        switch (threadIdx.x >> 6) {  // wave-uniform quarter
+        case 0: unpack_block_part<T, W, EPI, VW, kOutNT, 4, 0>(bp, t, static_cast<O*>(c.out), out_base, full, c.len, ep); break;
+        case 1: unpack_block_part<T, W, EPI, VW, kOutNT, 4, 1>(bp, t, static_cast<O*>(c.out), out_base, full, c.len, ep); break;
+        case 2: unpack_block_part<T, W, EPI, VW, kOutNT, 4, 2>(bp, t, static_cast<O*>(c.out), out_base, full, c.len, ep); break;
+        default: unpack_block_part<T, W, EPI, VW, kOutNT, 4, 3>(bp, t, static_cast<O*>(c.out), out_base, full, c.len, ep); break;
+        }
+    }
 }
 
-template <int T, int W, Epi EPI, int VW>
-vxg_status launch_one(const ChunkTable& tab, uint64_t groups, hipStream_t s) {
+// A launch with fewer 32-block workgroups than this uses the row split (S = 4).
+constexpr uint64_t kSplitBelowGroups = 512;
+
+template <int T, int W, Epi EPI, int VW, bool LDSD, int S>
+vxg_status launch_s(ChunkTable tab, hipStream_t s) {
+    uint64_t groups = 0;
+    for (uint32_t k = 0; k < tab.n; k++) {
+        tab.c[k].first_group = groups;
+        groups += (tab.c[k].n_blocks + (32 / S) - 1) / (32 / S);
+    }
     if (groups == 0) return VXG_OK;
+    if (groups > 0xFFFFFFFFull) return set_error(VXG_ERR_INVALID_ARGUMENT, "array too long for one launch");
+    hipLaunchKernelGGL((fl_unpack_kernel<T, W, EPI, VW, LDSD, S>), dim3(unsigned(groups)), dim3(256), 0, s, tab);
+    return hip_check(hipGetLastError(), "fl_unpack_kernel launch");
+}
+
+// `groups32` = the table's workgroups at 32 blocks per workgroup (decides the row split).
+template <int T, int W, Epi EPI, int VW>
+vxg_status launch_one(const ChunkTable& tab, uint64_t groups32, hipStream_t s) {
+    if (groups32 == 0) return VXG_OK;
+    constexpr bool kSplit = (T == 32 || T == 64) && W > 0;
+    const bool split = kSplit && groups32 < kSplitBelowGroups;
+    bool lds = false;
     if constexpr (EPI == Epi::Dict) {
-        bool lds = true;
+        lds = true;
         for (uint32_t k = 0; k < tab.n; k++)
             lds = lds && tab.c[k].dict_len * VW <= uint64_t(kDictLdsBytes) &&
                   (reinterpret_cast<uintptr_t>(tab.c[k].dict) & 15) == 0;
-        if (lds) {
-            hipLaunchKernelGGL((fl_unpack_kernel<T, W, EPI, VW, true>), dim3(unsigned(groups)), dim3(256), 0, s, tab);
-            return hip_check(hipGetLastError(), "fl_unpack_kernel launch");
-        }
     }
-    hipLaunchKernelGGL((fl_unpack_kernel<T, W, EPI, VW>), dim3(unsigned(groups)), dim3(256), 0, s, tab);
-    return hip_check(hipGetLastError(), "fl_unpack_kernel launch");
+    if constexpr (kSplit) {
+        if (split) return lds ? launch_s<T, W, EPI, VW, true, 4>(tab, s) : launch_s<T, W, EPI, VW, false, 4>(tab, s);
+    }
+    if constexpr (EPI == Epi::Dict) {
+        if (lds) return launch_s<T, W, EPI, VW, true, 1>(tab, s);
+    }
+    return launch_s<T, W, EPI, VW, false, 1>(tab, s);
 }
 
 // Function-pointer table over W = 0..WMAX.

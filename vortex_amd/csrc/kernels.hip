@@ -538,10 +538,41 @@ vxg_status launch_runend(int value_width, const void* values, int ends_width, co
     return hip_check(hipGetLastError(), "runend_kernel");
 }
 
-// Chunk-table form: workgroup g expands outputs [2048 (g - first_group), +2048) of one chunk.
+// Chunk-table form.  A workgroup expands outputs [j0, j0 + 2048) of one chunk:
+//   * wave 0 finds the runs holding j0 and the range's last output with 64-ary searches over the
+//     ends (3-4 dependent loads, not a 14-step binary search per thread);
+//   * every run of the range writes its index at its first output position (a run head) into
+//     LDS, an inclusive max-scan fills the positions between heads;
+//   * outputs are written coalesced: out[j] = values[run(j)].
+// Ends are trimmed as the reference does: min(ends[r] - offset, len) (runend/compress.rs:140).
+__device__ __forceinline__ uint64_t runend_first_gt(const void* ends, int ew, uint64_t offset, uint64_t n_runs,
+                                                    uint64_t j) {
+    // first run r with ends[r] - offset > j (n_runs if none); wave-uniform result, one wave
+    const int lane = threadIdx.x & 63;
+    uint64_t lo = 0, hi = n_runs;
+    while (hi - lo > 64) {
+        const uint64_t step = (hi - lo + 63) / 64;
+        const uint64_t idx = lo + step * uint64_t(lane);
+        const bool gt = idx < hi ? load_uint(ends, ew, false, idx) - offset > j : true;
+        const unsigned long long bm = __ballot(gt);
+        const int k = bm ? __ffsll(bm) - 1 : 64;
+        const uint64_t nlo = k == 0 ? lo : lo + step * uint64_t(k - 1) + 1;
+        const uint64_t nhi = k == 64 ? hi : (lo + step * uint64_t(k) < hi ? lo + step * uint64_t(k) : hi);
+        lo = nlo;
+        hi = nhi;
+    }
+    const uint64_t idx = lo + uint64_t(lane);
+    const bool gt = idx < hi ? load_uint(ends, ew, false, idx) - offset > j : false;
+    const unsigned long long bm = __ballot(gt);
+    return bm ? lo + uint64_t(__ffsll(bm) - 1) : hi;
+}
+
 template <typename V>
 __global__ __launch_bounds__(kBlock) void runend_chunks_kernel(RunEndTable tab) {
-    constexpr int ITEMS = 8;
+    constexpr int SPAN = 2048, PER = SPAN / kBlock;
+    __shared__ uint32_t s_head[SPAN];
+    __shared__ uint32_t s_wmax[kBlock / 64];
+    __shared__ uint64_t s_r[2];
     uint32_t lo = 0, hi = tab.n;
     const uint64_t g = blockIdx.x;
     while (hi - lo > 1) {
@@ -551,30 +582,56 @@ __global__ __launch_bounds__(kBlock) void runend_chunks_kernel(RunEndTable tab) 
     const RunEndChunk& c = tab.c[lo];
     const V* __restrict__ values = static_cast<const V*>(c.values);
     V* __restrict__ out = static_cast<V*>(c.out);
-    const int ew = int(c.ends_width);
-    const uint64_t j0 = ((g - c.first_group) * kBlock + threadIdx.x) * ITEMS;
-    if (j0 >= c.len) return;
-    uint64_t rlo = 0, rhi = c.n_runs;
-    while (rlo < rhi) {
-        const uint64_t mid = (rlo + rhi) >> 1;
-        if (load_uint(c.ends, ew, false, mid) - c.offset > j0) rhi = mid; else rlo = mid + 1;
+    const int ew = int(c.ends_width), tid = threadIdx.x;
+    const uint64_t j0 = (g - c.first_group) * SPAN;
+    const int jn = int(c.len - j0 < uint64_t(SPAN) ? c.len - j0 : uint64_t(SPAN));
+    if (tid < 64) {
+        const uint64_t r0 = runend_first_gt(c.ends, ew, c.offset, c.n_runs, j0);
+        const uint64_t r1 = runend_first_gt(c.ends, ew, c.offset, c.n_runs, j0 + uint64_t(jn) - 1);
+        if (tid == 0) {
+            s_r[0] = r0;
+            s_r[1] = r1;
+        }
     }
-    uint64_t r = rlo;
-    if (r >= c.n_runs) {
-        __hip_atomic_fetch_or(tab.err, kErrRunEnd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int k = 0; k < PER; k++) s_head[tid + k * kBlock] = 0;
+    __syncthreads();
+    const uint64_t r0 = s_r[0], r1 = s_r[1];
+    if (r1 >= c.n_runs) {  // the ends do not reach the last output of this range
+        if (tid == 0) __hip_atomic_fetch_or(tab.err, kErrRunEnd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
     }
-    uint64_t end = load_uint(c.ends, ew, false, r) - c.offset;
-#pragma unroll
-    for (int k = 0; k < ITEMS; k++) {
-        const uint64_t j = j0 + k;
-        if (j >= c.len) break;
-        while (end <= j && r + 1 < c.n_runs) {
-            r++;
-            end = load_uint(c.ends, ew, false, r) - c.offset;
-        }
-        nt_store(out + j, values[r]);
+    // run heads: run r0 + k starts at max(trimmed end of r0 + k - 1, j0)
+    for (uint64_t k = 1 + uint64_t(tid); k <= r1 - r0; k += kBlock) {
+        const uint64_t st = load_uint(c.ends, ew, false, r0 + k - 1) - c.offset;  // > j0 by construction
+        s_head[st - j0] = uint32_t(k);
     }
+    __syncthreads();
+    // inclusive max-scan of s_head: thread t owns entries [PER t, PER t + PER)
+    uint32_t v[PER];
+    uint32_t m = 0;
+#pragma unroll
+    for (int k = 0; k < PER; k++) {
+        m = max(m, s_head[tid * PER + k]);
+        v[k] = m;
+    }
+    uint32_t x = m;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if ((tid & 63) >= d) x = max(x, y);
+    }
+    if ((tid & 63) == 63) s_wmax[tid >> 6] = x;
+    __syncthreads();
+    uint32_t before = __shfl_up(x, 1, 64);
+    if ((tid & 63) == 0) before = 0;
+#pragma unroll
+    for (int w = 0; w < kBlock / 64; w++)
+        if (w < (tid >> 6)) before = max(before, s_wmax[w]);
+#pragma unroll
+    for (int k = 0; k < PER; k++) s_head[tid * PER + k] = max(v[k], before);
+    __syncthreads();
+    for (int i = tid; i < jn; i += kBlock) nt_store(out + j0 + i, values[r0 + s_head[i]]);
 }
 
 vxg_status launch_runend_chunks(int value_width, const RunEndTable& t, uint64_t groups, hipStream_t s) {

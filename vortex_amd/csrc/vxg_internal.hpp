@@ -221,7 +221,7 @@ struct FsstChunk {
     uint32_t n_symbols;
     uint32_t bidx;            // buffer_index of non-inlined views
 };
-constexpr int kFsstArgChunks = 16;
+constexpr int kFsstArgChunks = 24;
 struct FsstTable {
     FsstChunk c[kFsstArgChunks];
     uint32_t n;
