@@ -334,6 +334,8 @@ def main():
                     help="comma list; c1 is the headline, others go under 'encodings'")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--simulate-world", type=int, default=0,
+                    help="diagnostic: with one process, build rank 0's shard of an N-GPU run of C3/C5")
     ap.add_argument("--e2e", action="store_true",
                     help="also measure host->host (H2D + decode + D2H over PCIe); never the headline value")
     args = ap.parse_args()
@@ -353,8 +355,11 @@ def main():
     import vortex_amd as V
     ctx = V.Context(local)
     rng = np.random.default_rng(42 + rank)
-    makers = {"c1": make_c1, "c2": make_c2, "c3": lambda r: make_c3_shard(r, world, rank), "c4": make_c4,
-              "c5": lambda r: make_c5_shard(r, world, rank)}
+    # --simulate-world N (diagnostic, single process): rank 0's shard of an N-GPU run of the
+    # sharded configs, to read one GPU's share of the N-GPU work before an N-GPU node is used
+    shard_world = args.simulate_world if args.simulate_world and world == 1 else world
+    makers = {"c1": make_c1, "c2": make_c2, "c3": lambda r: make_c3_shard(r, shard_world, rank), "c4": make_c4,
+              "c5": lambda r: make_c5_shard(r, shard_world, rank)}
     copies = {"c1": 4, "c2": 1, "c3": 2, "c4": 1, "c5": 1}
     results = {}
     for key in [w.strip() for w in args.workloads.split(",") if w.strip()]:

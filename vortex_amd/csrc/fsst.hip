@@ -41,6 +41,8 @@ constexpr int kTile = 256;            // strings per tile = threads per workgrou
 constexpr int kCodeLds = 6 * 1024;    // staged code bytes per tile
 constexpr int kHeapLds = 10 * 1024;   // staged output bytes per tile
 constexpr int kScanTiles = 128;       // tiles per pre-pass workgroup (= 32 FastLanes blocks)
+constexpr int kMaxDw = (kCodeLds / kTile + 3) / 4;  // code dwords per thread in the decode
+static_assert(kMaxDw * 4 * kTile >= kCodeLds, "segments must cover the staged codes");
 
 __device__ __forceinline__ int64_t wave_sum(int64_t x) {
 #pragma unroll
@@ -111,6 +113,19 @@ __device__ __forceinline__ uint4 lds_view(const uint32_t* h32, int a, uint32_t l
     return make_uint4(len, w1 & keep(0), w2 & keep(4), w3 & keep(8));
 }
 
+// Bytes [sh, sh + 16) of the 32-byte concatenation x:y (little endian), sh in [0, 16).
+__device__ __forceinline__ uint4 funnel16(const uint4 x, const uint4 y, int sh) {
+    const uint32_t z[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
+    const uint32_t b = uint32_t(sh & 3);
+    auto ab = [b](uint32_t hi, uint32_t lo) { return __builtin_amdgcn_alignbyte(hi, lo, b); };
+    switch (sh >> 2) {  // uniform per tile
+    case 0: return make_uint4(ab(z[1], z[0]), ab(z[2], z[1]), ab(z[3], z[2]), ab(z[4], z[3]));
+    case 1: return make_uint4(ab(z[2], z[1]), ab(z[3], z[2]), ab(z[4], z[3]), ab(z[5], z[4]));
+    case 2: return make_uint4(ab(z[3], z[2]), ab(z[4], z[3]), ab(z[5], z[4]), ab(z[6], z[5]));
+    default: return make_uint4(ab(z[4], z[3]), ab(z[5], z[4]), ab(z[6], z[5]), ab(z[7], z[6]));
+    }
+}
+
 __device__ __forceinline__ uint32_t byte_of(const uint4& v, int j) {
     const uint32_t w = j < 4 ? v.x : j < 8 ? v.y : j < 12 ? v.z : v.w;
     return (w >> (8 * (j & 3))) & 0xFFu;
@@ -164,13 +179,17 @@ __device__ __forceinline__ void scan_tile_sums(const int64_t* s_ts, int64_t* ws,
 
 // Chunk of workgroup g in a launch (workgroup-uniform binary search on the table's first_*).
 template <bool SCAN>
-__device__ __forceinline__ const FsstChunk& fsst_chunk_of(const FsstTable& tab, uint64_t g) {
+__device__ __forceinline__ uint32_t fsst_chunk_index(const FsstTable& tab, uint64_t g) {
     uint32_t lo = 0, hi = tab.n;
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
         if ((SCAN ? tab.c[mid].first_scan : tab.c[mid].first_tile) <= g) lo = mid; else hi = mid;
     }
-    return tab.c[lo];
+    return lo;
+}
+template <bool SCAN>
+__device__ __forceinline__ const FsstChunk& fsst_chunk_of(const FsstTable& tab, uint64_t g) {
+    return tab.c[fsst_chunk_index<SCAN>(tab, g)];
 }
 
 // Any length column: wave w sums tile 4r + w in round r (4 consecutive lengths per lane).
@@ -269,9 +288,23 @@ __global__ __launch_bounds__(kTile) void fsst_tile_scan_fl32(FsstTable tab, int6
 }
 
 template <class OffAcc, class LenAcc>
-__global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, const int64_t* __restrict__ tile_prefix_all,
+__global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t total_tiles,
+                                                     const int64_t* __restrict__ tile_prefix_all,
                                                      const int64_t* __restrict__ block_totals_all,
                                                      uint32_t* __restrict__ err) {
+    __shared__ uint64_t s_sym[256];
+    __shared__ uint8_t s_len[256];
+    __shared__ int ws_a[kTile / 64], ws_b[kTile / 64];
+    __shared__ unsigned ws_bad[kTile / 64];
+    __shared__ int64_t ws64[kTile / 64];
+    __shared__ int64_t s_block_prefix;
+    __shared__ int64_t s_coff[3];  // code_offs[0], code_offs[first], code_offs[last]
+    __shared__ __attribute__((aligned(16))) uint8_t s_codes[kCodeLds + 48];
+    // + slack: view reads past a string, and ORs of the (<= 3) code bytes past the tile
+    __shared__ __attribute__((aligned(16))) uint32_t s_heap32[(kHeapLds + 96) / 4];
+    uint8_t* const s_heap = reinterpret_cast<uint8_t*>(s_heap32);
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+
     const FsstChunk& ch = fsst_chunk_of<false>(tab, blockIdx.x);
     const uint64_t* __restrict__ symbols = ch.symbols;
     const uint8_t* __restrict__ sym_lens = ch.sym_lens;
@@ -286,18 +319,6 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, const int64_
     uint8_t* __restrict__ heap = ch.heap;
     uint4* __restrict__ views = reinterpret_cast<uint4*>(ch.views);
     const uint32_t bidx = ch.bidx;
-    __shared__ uint64_t s_sym[256];
-    __shared__ uint8_t s_len[256];
-    __shared__ int ws_a[kTile / 64], ws_b[kTile / 64];
-    __shared__ unsigned ws_bad[kTile / 64];
-    __shared__ int64_t ws64[kTile / 64];
-    __shared__ int64_t s_block_prefix;
-    __shared__ int64_t s_coff[3];  // code_offs[0], code_offs[first], code_offs[last]
-    __shared__ __attribute__((aligned(16))) uint8_t s_codes[kCodeLds + 48];
-    __shared__ __attribute__((aligned(16))) uint32_t s_heap32[(kHeapLds + 48) / 4];
-    uint8_t* const s_heap = reinterpret_cast<uint8_t*>(s_heap32);
-
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint32_t tile = uint32_t(blockIdx.x - ch.first_tile);
     {
         const uint32_t sk = uint32_t(tid) < n_symbols ? uint32_t(tid) : 0;
@@ -351,105 +372,149 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, const int64_
     const bool stage = !any_bad && (c1 - c0) <= kCodeLds && c1 >= c0 && tile_total <= kHeapLds;
 
     if (stage) {
-        // (b) stage the tile's codes at the same offset mod 16 as in `codes` (an aligned 16-byte
-        // chunk holding a tile byte never crosses a page, so it is read whole; bytes outside
-        // the tile are ignored), and zero the output image (+16 slack for view reads)
+        // (b) stage the tile's code bytes into LDS shifted so that the tile's first code is
+        // s_codes[0] (two aligned 16-byte loads + a byte funnel per chunk; an aligned chunk that
+        // holds a tile byte never crosses a page, so it is read whole), and zero the image
         const int64_t cabs0 = c_base + c0;
-        const int cshift = int((reinterpret_cast<uintptr_t>(codes) + cabs0) & 15);
+        const uintptr_t ga = reinterpret_cast<uintptr_t>(codes) + uintptr_t(cabs0);
+        const int cshift = int(ga & 15);
         const int hshift = int((reinterpret_cast<uintptr_t>(heap) + tile_out0) & 15);  // image byte hshift = heap[tile_out0]
-        const int span = cshift + int(c1 - c0);  // tile codes at s_codes[cshift, span)
+        const int span = int(c1 - c0);  // tile codes at s_codes[0, span)
         const int ttot = int(tile_total);
         {
-            const uint8_t* a0 = codes + (cabs0 - cshift);
+            const uint4* a0 = reinterpret_cast<const uint4*>(ga - uintptr_t(cshift));
             const int nchunk = (span + 15) >> 4;
-            for (int q = tid; q < nchunk; q += kTile)
-                *reinterpret_cast<uint4*>(s_codes + 16 * q) = *reinterpret_cast<const uint4*>(a0 + 16 * q);
+            for (int q = tid; q < nchunk; q += kTile) {
+                const uint4 x = a0[q];
+                uint4 y = make_uint4(0, 0, 0, 0);
+                if (cshift != 0 && 16 * (q + 1) - cshift < span) y = a0[q + 1];
+                *reinterpret_cast<uint4*>(s_codes + 16 * q) = funnel16(x, y, cshift);
+            }
             const int nz = (hshift + ttot + 16 + 15) >> 4;
             for (int q = tid; q < nz; q += kTile) reinterpret_cast<uint4*>(s_heap32)[q] = make_uint4(0, 0, 0, 0);
         }
         __syncthreads();
 
-        // (c) code-parallel decode.  Segment = `seg` bytes (multiple of 16, at most two 16-byte
-        // chunks) of s_codes per thread.
-        static_assert(((kCodeLds + 15 + kTile - 1) / kTile + 15) / 16 <= 2, "segment > 2 chunks");
-        const int seg = (((span + kTile - 1) / kTile) + 15) & ~15;
-        const int s0 = tid * seg;
-        const int nch = s0 < span ? (min(s0 + seg, span) - s0 + 15) >> 4 : 0;
+        // (c) code-parallel decode over segments of nd dwords (4 code bytes each) per thread,
+        // sized so that ~all 256 threads have work.  A wave whose bytes hold no escape (255)
+        // and does not start right after one takes the fast path (no escape logic, no
+        // predication); otherwise the general path.  Both pack each code's decoded length x 8
+        // into one byte of a per-dword word (sum = v_sad_u8).
+        const int nd = max(1, ((span + kTile - 1) / kTile + 3) >> 2);
+        const int s0 = tid * 4 * nd;
+        bool slow = false;
         bool skip0 = false;  // is s_codes[s0] the literal byte of an escape?
-        if (s0 > cshift && s0 < span) {
+        if (s0 > 0 && s0 < span && s_codes[s0 - 1] == 255) {
+            slow = true;
             int r = 0;
-            for (int p = s0 - 1; p >= cshift && s_codes[p] == 255; --p) ++r;
+            for (int p = s0 - 1; p >= 0 && s_codes[p] == 255; --p) ++r;
             skip0 = r & 1;
         }
-        // pass 1: decoded length of every code byte (0 for literals and bytes outside the
-        // tile), packed as 4-bit fields, and their sum
-        uint64_t lp[2] = {0, 0};
-        int sum = 0;
-        {
+        uint32_t wd[kMaxDw];
+#pragma unroll
+        for (int d = 0; d < kMaxDw; d++) {
+            wd[d] = 0;
+            if (d < nd && s0 + 4 * d < span) {
+                wd[d] = *reinterpret_cast<const uint32_t*>(s_codes + s0 + 4 * d);
+                const uint32_t x = wd[d];
+                slow |= (((x & 0x7F7F7F7Fu) + 0x01010101u) & x & 0x80808080u) != 0;  // a 0xFF byte
+            }
+        }
+        const bool fast = __ballot(slow) == 0;  // wave-uniform
+        // pass 1: pk[d] byte j = decoded length x 8 of code byte 4d + j (0 for literals and
+        // bytes past the tile)
+        uint32_t pk[kMaxDw];
+        uint32_t sum8 = 0;
+        if (fast) {
+#pragma unroll
+            for (int d = 0; d < kMaxDw; d++) {
+                pk[d] = 0;
+                if (d < nd && s0 + 4 * d < span) {
+                    const uint32_t x = wd[d];
+                    uint32_t ls[4];
+#pragma unroll
+                    for (int j = 0; j < 4; j++) ls[j] = s_len[(x >> (8 * j)) & 0xFFu];
+                    uint32_t k = 0;
+#pragma unroll
+                    for (int j = 0; j < 4; j++) k |= ls[j] << (8 * j + 3);
+                    const int vb = span - (s0 + 4 * d);  // valid bytes of this dword
+                    if (vb < 4) k &= (1u << (8 * vb)) - 1u;
+                    pk[d] = k;
+                    sum8 = __builtin_amdgcn_sad_u8(k, 0u, sum8);
+                }
+            }
+        } else {
             bool skp = skip0;
 #pragma unroll
-            for (int h = 0; h < 2; h++) {
-                if (h < nch) {
-                    const int q = s0 + 16 * h;
-                    const uint4 ch = *reinterpret_cast<const uint4*>(s_codes + q);
-                    const int lo = cshift - q, hi = span - q;  // in-tile bytes j: lo <= j < hi
-                    uint32_t ls[16];
+            for (int d = 0; d < kMaxDw; d++) {
+                pk[d] = 0;
+                if (d < nd && s0 + 4 * d < span) {
+                    const uint32_t x = wd[d];
+                    uint32_t k = 0;
 #pragma unroll
-                    for (int j = 0; j < 16; j++) ls[j] = s_len[byte_of(ch, j)];  // 16 reads in flight
-                    uint64_t pk = 0;
-#pragma unroll
-                    for (int j = 0; j < 16; j++) {
-                        const uint32_t c = byte_of(ch, j);
-                        const bool emit = j >= lo && j < hi && !skp;
+                    for (int j = 0; j < 4; j++) {
+                        const uint32_t c = (x >> (8 * j)) & 0xFFu;
+                        const bool emit = s0 + 4 * d + j < span && !skp;
                         skp = emit && c == 255;
-                        const uint32_t L = emit ? ls[j] : 0u;
-                        pk |= uint64_t(L) << (4 * j);
-                        sum += int(L);
+                        const uint32_t L = emit ? uint32_t(s_len[c]) : 0u;
+                        k |= L << (8 * j + 3);
                     }
-                    lp[h] = pk;
+                    pk[d] = k;
+                    sum8 = __builtin_amdgcn_sad_u8(k, 0u, sum8);
                 }
             }
         }
         int dec_total;
-        const int seg_rel = block_excl_scan32(sum, ws_b, dec_total);
+        const int seg_rel = block_excl_scan32(int(sum8 >> 3), ws_b, dec_total);
         if (tid == 0 && dec_total != ttot)
             __hip_atomic_fetch_or(err, kErrFsst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // pass 2: every code ORs its (zero-padded) bytes into <= 3 dwords of the image.  All 16
-        // symbol reads of a chunk are issued before its first ds_or; the ORs are unconditional
-        // (zero for literals / outside the tile) so the chunk runs without branches.  Offsets
-        // are clamped to the tile's end (only corrupt input, already flagged, reaches it).
-        {
-            int o = hshift + seg_rel;
-            const int o_end = hshift + ttot;
+        // pass 2: every code ORs its (zero-padded) bytes into <= 3 dwords of the zeroed image:
+        // (w1:w0) = sym << 8(o & 3) and w2 = the bytes shifted past them.  Fast path: all 4
+        // symbol reads of a dword issued first, no selects.  Codes past the tile (fast path,
+        // last segment) OR into the image slack after the tile.  A tile whose codes do not
+        // decode to its length sum (corrupt input, flagged above) is not written.
+        if (dec_total == ttot) {
+            uint32_t o8 = uint32_t(hshift + seg_rel) << 3;  // bit position in the image
+            auto put = [&](uint64_t m, uint32_t L8) {
+                const uint32_t sh = o8 & 24u;
+                const uint32_t w = o8 >> 5;
+                const uint64_t lo64 = m << sh;
+                const uint32_t hi32 = uint32_t((m >> 32) << sh >> 32);
+                __hip_atomic_fetch_or(&s_heap32[w], uint32_t(lo64), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_or(&s_heap32[w + 1], uint32_t(lo64 >> 32), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_or(&s_heap32[w + 2], hi32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                o8 += L8;
+            };
+            if (fast) {
 #pragma unroll
-            for (int h = 0; h < 2; h++) {
-                if (h < nch) {
-                    const int q = s0 + 16 * h;
-                    const uint4 ch = *reinterpret_cast<const uint4*>(s_codes + q);
-                    const uint32_t after = s_codes[q + 16];  // literal of an escape in byte 15
-                    uint64_t sy[16];
+                for (int d = 0; d < kMaxDw; d++) {
+                    if (d < nd && s0 + 4 * d < span) {
+                        const uint32_t x = wd[d];
+                        uint64_t sy[4];
 #pragma unroll
-                    for (int j = 0; j < 16; j++) sy[j] = s_sym[byte_of(ch, j)];
-                    const uint64_t pk = lp[h];
+                        for (int j = 0; j < 4; j++) sy[j] = s_sym[(x >> (8 * j)) & 0xFFu];
 #pragma unroll
-                    for (int j = 0; j < 16; j++) {
-                        const uint32_t c = byte_of(ch, j);
-                        const int L = int((pk >> (4 * j)) & 15u);
-                        const uint64_t lit = j < 15 ? byte_of(ch, j + 1) : after;
-                        uint64_t m = c == 255 ? lit : sy[j];
-                        m = (L > 0 && o < o_end) ? m : 0ull;
-                        const int oc = min(o, o_end);
-                        const uint32_t sh = 8u * uint32_t(oc & 3);
-                        const int w = oc >> 2;
-                        const uint64_t lo64 = m << sh;
-                        const uint32_t hi32 = sh ? uint32_t(m >> (64u - sh)) : 0u;
-                        __hip_atomic_fetch_or(&s_heap32[w], uint32_t(lo64), __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_WORKGROUP);
-                        __hip_atomic_fetch_or(&s_heap32[w + 1], uint32_t(lo64 >> 32), __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_WORKGROUP);
-                        __hip_atomic_fetch_or(&s_heap32[w + 2], hi32, __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_WORKGROUP);
-                        o += L;
+                        for (int j = 0; j < 4; j++) put(sy[j], (pk[d] >> (8 * j)) & 0xFFu);
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int d = 0; d < kMaxDw; d++) {
+                    if (d < nd && s0 + 4 * d < span) {
+                        const uint32_t x = wd[d];
+                        const uint32_t after = s_codes[s0 + 4 * d + 4];  // literal of an escape in byte 3
+                        uint64_t sy[4];
+#pragma unroll
+                        for (int j = 0; j < 4; j++) sy[j] = s_sym[(x >> (8 * j)) & 0xFFu];
+#pragma unroll
+                        for (int j = 0; j < 4; j++) {
+                            const uint32_t c = (x >> (8 * j)) & 0xFFu;
+                            const uint32_t L8 = (pk[d] >> (8 * j)) & 0xFFu;
+                            const uint64_t lit = j < 3 ? ((x >> (8 * j + 8)) & 0xFFu) : after;
+                            uint64_t m = c == 255 ? lit : sy[j];
+                            put(L8 ? m : 0ull, L8);
+                        }
                     }
                 }
             }
@@ -593,7 +658,7 @@ vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint
                     using LA = std::remove_pointer_t<decltype(la)>;
                     if (std::get<2>(key) < 0)
                         hipLaunchKernelGGL((fsst_tile_scan<LA>), dim3(unsigned(scans)), dim3(kTile), 0, s, tab, tp, bt);
-                    hipLaunchKernelGGL((fsst_decode<OA, LA>), dim3(unsigned(tiles)), dim3(kTile), 0, s, tab, tp, bt,
+                    hipLaunchKernelGGL((fsst_decode<OA, LA>), dim3(unsigned(tiles)), dim3(kTile), 0, s, tab, tiles, tp, bt,
                                        err);
                 });
             });
