@@ -150,47 +150,60 @@ def make_c5_shard(rng, world: int, rank: int):
 # ------------------------------------------------------------------------------ timing
 class Workload:
     """One or more arrays (C5: the 16 lineitem columns) with preallocated canonical outputs; a
-    step canonicalizes each of them once through the C ABI, on one stream."""
+    step canonicalizes each of them once through the C ABI, on one stream.  By default a step
+    is one replay of a vxg_plan (the planner's launches recorded once as a HIP graph: every
+    kernel runs every step, without per-step host planning and per-kernel submission);
+    graph=False calls vxg_canonicalize per array per step instead."""
 
-    def __init__(self, arrs, info, ctx, copies: int):
+    def __init__(self, arrs, info, ctx, copies: int, graph: bool = True):
         import torch
         import vortex_amd.arrays as A
-        self.info, self.ctx = info, ctx
+        self.info, self.ctx, self.graph = info, ctx, graph
         arrs = arrs if isinstance(arrs, list) else [arrs]
         dev = torch.device("cuda", ctx.device)
-        self.keep = []
-        self.cols = []
-        for arr in arrs:
-            trees = [arr.to(dev) for _ in range(copies)]
-            nodes = [A.flatten(t, self.keep) for t in trees]
-            vb, db, nb = C.c_uint64(), C.c_uint64(), C.c_uint32()
-            table = (A._lib.VxgDataBuffer * 4096)()
-            chk(ctx.lib.vxg_canonical_layout(ctx.handle, C.byref(nodes[0]), C.byref(vb), C.byref(db), table, 4096,
-                                             C.byref(nb)))
-            out = A._lib.VxgCanonical()
-            if arr.dtype == A.DTYPE["PRIMITIVE"]:
-                vals = torch.empty(max(vb.value, 16), dtype=torch.uint8, device=dev)
-                out.values = vals.data_ptr()
-                self.keep.append(vals)
-            else:
-                views = torch.empty(max(vb.value, 16), dtype=torch.uint8, device=dev)
-                data = torch.empty(db.value + 16, dtype=torch.uint8, device=dev)
-                out.views, out.data, out.data_bytes = views.data_ptr(), data.data_ptr(), db.value
-                out.data_buffers, out.n_data_buffers, out.data_buffers_cap = table, nb.value, 4096
-                self.keep += [views, data, table]
-            if arr.nullable:
-                vt = torch.empty(((arr.len + 31) // 32) * 4 + 4, dtype=torch.uint8, device=dev)
-                out.validity = vt.data_ptr()
-                self.keep.append(vt)
-            self.cols.append((trees, nodes, out))
+        self.copies = [[arr.to(dev) for arr in arrs] for _ in range(copies)]
+        if graph:
+            self.plans = [A.Plan(trees, ctx) for trees in self.copies]
+        else:
+            self.keep = []
+            self.cols = []
+            for j, arr in enumerate(arrs):
+                nodes = [A.flatten(trees[j], self.keep) for trees in self.copies]
+                vb, db, nb = C.c_uint64(), C.c_uint64(), C.c_uint32()
+                table = (A._lib.VxgDataBuffer * 4096)()
+                chk(ctx.lib.vxg_canonical_layout(ctx.handle, C.byref(nodes[0]), C.byref(vb), C.byref(db), table,
+                                                 4096, C.byref(nb)))
+                out = A._lib.VxgCanonical()
+                if arr.dtype == A.DTYPE["PRIMITIVE"]:
+                    vals = torch.empty(max(vb.value, 16), dtype=torch.uint8, device=dev)
+                    out.values = vals.data_ptr()
+                    self.keep.append(vals)
+                else:
+                    views = torch.empty(max(vb.value, 16), dtype=torch.uint8, device=dev)
+                    data = torch.empty(db.value + 16, dtype=torch.uint8, device=dev)
+                    out.views, out.data, out.data_bytes = views.data_ptr(), data.data_ptr(), db.value
+                    out.data_buffers, out.n_data_buffers, out.data_buffers_cap = table, nb.value, 4096
+                    self.keep += [views, data, table]
+                if arr.nullable:
+                    vt = torch.empty(((arr.len + 31) // 32) * 4 + 4, dtype=torch.uint8, device=dev)
+                    out.validity = vt.data_ptr()
+                    self.keep.append(vt)
+                self.cols.append((nodes, out))
         self.i = 0
 
     def step(self):
         k = self.i
         self.i += 1
-        for trees, nodes, out in self.cols:
+        if self.graph:
+            self.plans[k % len(self.plans)].launch()
+            return
+        for nodes, out in self.cols:
             chk(self.ctx.lib.vxg_canonicalize(self.ctx.handle, C.byref(nodes[k % len(nodes)]), C.byref(out),
                                               self.ctx.stream_ptr()))
+
+    def close(self):
+        for p in getattr(self, "plans", []):
+            p.close()
 
 
 def chk(st):
@@ -334,6 +347,8 @@ def main():
                     help="comma list; c1 is the headline, others go under 'encodings'")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-graph", action="store_true",
+                    help="call vxg_canonicalize per array per step instead of replaying a vxg_plan graph")
     ap.add_argument("--simulate-world", type=int, default=0,
                     help="diagnostic: with one process, build rank 0's shard of an N-GPU run of C3/C5")
     ap.add_argument("--e2e", action="store_true",
@@ -366,7 +381,10 @@ def main():
         t0 = time.perf_counter()
         arr, info = makers[key](rng)
         e2e = run_e2e(arr, info, ctx) if args.e2e and not isinstance(arr, list) else None
-        wl = Workload(arr, info, ctx, copies[key])
+        # one-array steps are one or two back-to-back kernel launches: direct calls overlap the
+        # next submission with the running kernel (a graph replay measured 2-6 us slower per
+        # step on C1-C4); multi-array steps (C5: 16 columns, ~30 kernels) replay a graph
+        wl = Workload(arr, info, ctx, copies[key], graph=isinstance(arr, list) and not args.no_graph)
         del arr
         if rank == 0:
             log(f"[bench] {info['name']}: built in {time.perf_counter() - t0:.1f}s; timing...")
@@ -382,6 +400,7 @@ def main():
         results[key] = dict(info=info, elapsed=elapsed, ms_per_step=per_step * 1e3, kernel_ms_mean=kmean,
                             kernel_ms_median=kmed, algo_bytes=algo,
                             value=total_write * steps / elapsed / 1e9, e2e=e2e)
+        wl.close()
         del wl
         torch.cuda.empty_cache()
 
@@ -403,6 +422,8 @@ def main():
             "vs_baseline": None,
             "dtype": info["dtype"],
             "data": "synthetic (seeded; inputs resident in HBM, rotated across copies)",
+            "launch": "headline: direct vxg_canonicalize per step; multi-array steps (C5): vxg_plan HIP-graph replay"
+                      + (" disabled (--no-graph)" if args.no_graph else ""),
             "config": {"workload": f"{info['name']}: {info['encoding']}, {info['values']} values per GPU, "
                                    f"one chunk per GPU", "values_per_gpu": info["values"],
                        "parallelism": f"chunk-per-GPU x{world}"},

@@ -156,6 +156,9 @@ GPU_SIGNATURES = {
     "vxg_stream_sync": (ST, [VP, VP]),
     "vxg_canonical_size": (ST, [VP, C.POINTER(VxgArray), C.POINTER(U64), C.POINTER(U64)]),
     "vxg_canonicalize": (ST, [VP, C.POINTER(VxgArray), C.POINTER(VxgCanonical), VP]),
+    "vxg_plan_create": (ST, [VP, C.POINTER(VxgArray), C.POINTER(VxgCanonical), U32, C.POINTER(VP)]),
+    "vxg_plan_launch": (ST, [VP, VP]),
+    "vxg_plan_destroy": (ST, [VP]),
     "vxg_canonical_layout": (ST, [VP, C.POINTER(VxgArray), C.POINTER(U64), C.POINTER(U64),
                                   C.POINTER(VxgDataBuffer), U32, C.POINTER(U32)]),
     "vxg_bitunpack": (ST, [VP, INT, UINT, UINT, U64, VP, U64, VP, VP]),

@@ -497,3 +497,70 @@ def canonicalize(a: Array, ctx: Context, out_values=None, sync: bool = True) -> 
     if sync:
         ctx.sync()
     return res
+
+
+class Plan:
+    """vxg_plan: the launches of canonicalizing `arrays` into preallocated outputs, recorded
+    once as a HIP graph and replayed by launch() (one hipGraphLaunch; every kernel runs on
+    every replay).  Outputs are allocated here with vxg_canonical_layout and exposed as
+    Canonical objects; the device arrays must stay alive (and in place) with the plan."""
+
+    def __init__(self, arrays: Sequence[Array], ctx: Context):
+        import torch
+        self.ctx = ctx
+        self.keep: list = []
+        dev = torch.device("cuda", ctx.device)
+        n = len(arrays)
+        self.nodes = (_lib.VxgArray * max(n, 1))()
+        self.outs = (_lib.VxgCanonical * max(n, 1))()
+        self.results = []
+        for i, a in enumerate(arrays):
+            self.nodes[i] = flatten(a, self.keep)
+            vb, db, nb = C.c_uint64(), C.c_uint64(), C.c_uint32()
+            table = (_lib.VxgDataBuffer * 4096)()
+            _lib.check(ctx.lib.vxg_canonical_layout(ctx.handle, C.byref(self.nodes[i]), C.byref(vb), C.byref(db),
+                                                    table, 4096, C.byref(nb)))
+            res = Canonical("primitive" if a.dtype == DTYPE["PRIMITIVE"] else "varbinview", a.len, a.ptype)
+            o = self.outs[i]
+            if a.dtype == DTYPE["PRIMITIVE"]:
+                vals = torch.empty(max(vb.value, 16), dtype=torch.uint8, device=dev)
+                o.values = vals.data_ptr()
+                res.values = vals[: vb.value]
+            else:
+                views = torch.empty(max(vb.value, 16), dtype=torch.uint8, device=dev)
+                data = torch.empty(db.value + 16, dtype=torch.uint8, device=dev)
+                o.views, o.data, o.data_bytes = views.data_ptr(), data.data_ptr(), db.value
+                o.data_buffers, o.n_data_buffers, o.data_buffers_cap = table, nb.value, 4096
+                res.views, res.data = views[: vb.value], data[: db.value]
+                res.data_buffers = [(int(table[k].offset), int(table[k].len)) for k in range(nb.value)]
+                self.keep.append(table)
+            if a.nullable:
+                vt = torch.empty(((a.len + 31) // 32) * 4 + 4, dtype=torch.uint8, device=dev)
+                o.validity = vt.data_ptr()
+                res.validity = vt[: (a.len + 7) // 8]
+            self.keep.append(res)
+            self.results.append(res)
+        h = C.c_void_p()
+        _lib.check(ctx.lib.vxg_plan_create(ctx.handle, self.nodes, self.outs, n, C.byref(h)))
+        self.handle = h
+        # a nullable array whose validity turned out all-valid leaves out.validity NULL
+        for i, res in enumerate(self.results):
+            if res.validity is not None and not self.outs[i].validity:
+                res.validity = None
+
+    def launch(self, sync: bool = False):
+        _lib.check(self.ctx.lib.vxg_plan_launch(self.handle, self.ctx.stream_ptr()))
+        if sync:
+            self.ctx.sync()
+        return self.results
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self.ctx.lib.vxg_plan_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -200,7 +200,7 @@ vxg_status bitunpack_common(vxg_ctx* ctx, int T, unsigned W, unsigned offset, ui
 // ===================================================================================
 class Planner {
   public:
-    Planner(vxg_ctx* ctx, hipStream_t s) : ctx_(ctx), s_(s) {}
+    Planner(vxg_ctx* ctx, hipStream_t s, std::vector<void*>* owned = nullptr) : ctx_(ctx), s_(s), owned_(owned) {}
     ~Planner() {
         for (void* p : temps_) (void)hipFreeAsync(p, s_);
     }
@@ -215,6 +215,9 @@ class Planner {
     vxg_ctx* ctx_;
     hipStream_t s_;
     std::vector<void*> temps_;
+    // Recording a plan: temporaries are plain allocations owned by the plan (alive for all its
+    // replays) instead of stream-ordered ones.
+    std::vector<void*>* owned_ = nullptr;
     // Deferred K1 decodes of the chunks of a ChunkedArray (grouped into shared launches) and
     // the patch scatters that must follow them; null = launch immediately.
     struct PatchJob {
@@ -233,6 +236,11 @@ class Planner {
 
     vxg_status temp(uint64_t bytes, void** p) {
         if (bytes == 0) bytes = 16;
+        if (owned_) {
+            VXG_TRY(hip_check(hipMalloc(p, (bytes + 15) & ~15ull), "hipMalloc (plan temporary)"));
+            owned_->push_back(*p);
+            return VXG_OK;
+        }
         VXG_TRY(hip_check(hipMallocAsync(p, (bytes + 15) & ~15ull, s_), "hipMallocAsync"));
         temps_.push_back(*p);
         return VXG_OK;
@@ -1264,6 +1272,71 @@ vxg_status vxg_canonicalize(vxg_ctx* ctx, const vxg_array* a, vxg_canonical* out
     if (!a || !out) return set_error(VXG_ERR_INVALID_ARGUMENT, "null array/out");
     Planner p(ctx, S(stream));
     return p.canonical(*a, *out);
+}
+
+// ---- prepared canonicalize --------------------------------------------------------------
+}  // extern "C"
+
+struct vxg_plan {
+    vxg_ctx* ctx = nullptr;
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+    std::vector<void*> temps;  // the recorded launches' temporaries
+};
+
+extern "C" {
+
+vxg_status vxg_plan_create(vxg_ctx* ctx, const vxg_array* arrays, vxg_canonical* outs, uint32_t n, vxg_plan** plan) {
+    VXG_TRY(use_device(ctx));
+    if (!plan || (n && (!arrays || !outs))) return set_error(VXG_ERR_INVALID_ARGUMENT, "null plan/arrays/outs");
+    *plan = nullptr;
+    for (uint32_t i = 0; i < n; i++) {  // nothing may allocate or synchronise while recording
+        const vxg_array& a = arrays[i];
+        const vxg_canonical& o = outs[i];
+        const bool str = a.dtype == VXG_DTYPE_UTF8 || a.dtype == VXG_DTYPE_BINARY;
+        if (str ? (!o.views || !o.data) : !o.values)
+            return set_error(VXG_ERR_INVALID_ARGUMENT, "a plan needs caller-allocated outputs");
+        if (a.nullable && !o.validity)
+            return set_error(VXG_ERR_INVALID_ARGUMENT, "a plan needs caller-allocated validity for nullable arrays");
+    }
+    hipStream_t cs;
+    VXG_TRY(hip_check(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking), "plan stream"));
+    auto* pl = new vxg_plan();
+    pl->ctx = ctx;
+    vxg_status st = hip_check(hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed), "hipStreamBeginCapture");
+    if (st == VXG_OK) {
+        for (uint32_t i = 0; i < n && st == VXG_OK; i++) {
+            Planner p(ctx, cs, &pl->temps);
+            st = p.canonical(arrays[i], outs[i]);
+        }
+        hipGraph_t g = nullptr;
+        const hipError_t e = hipStreamEndCapture(cs, &g);
+        if (st == VXG_OK) st = hip_check(e, "hipStreamEndCapture");
+        pl->graph = g;
+        if (st == VXG_OK)
+            st = hip_check(hipGraphInstantiate(&pl->exec, g, nullptr, nullptr, 0), "hipGraphInstantiate");
+    }
+    (void)hipStreamDestroy(cs);
+    if (st == VXG_OK) *plan = pl;
+    else vxg_plan_destroy(pl);
+    return st;
+}
+
+vxg_status vxg_plan_launch(vxg_plan* plan, void* stream) {
+    if (!plan || !plan->exec) return set_error(VXG_ERR_INVALID_ARGUMENT, "null plan");
+    VXG_TRY(use_device(plan->ctx));
+    return hip_check(hipGraphLaunch(plan->exec, S(stream)), "hipGraphLaunch");
+}
+
+vxg_status vxg_plan_destroy(vxg_plan* plan) {
+    if (!plan) return VXG_OK;
+    if (plan->ctx) (void)hipSetDevice(plan->ctx->c.device);
+    if (plan->exec) (void)hipGraphExecDestroy(plan->exec);
+    if (plan->graph) (void)hipGraphDestroy(plan->graph);
+    if (!plan->temps.empty()) (void)hipDeviceSynchronize();  // no replay may still use them
+    for (void* p : plan->temps) (void)hipFree(p);
+    delete plan;
+    return VXG_OK;
 }
 
 static int unsigned_T(int ptype) { return 8 * ptype_width(ptype); }
