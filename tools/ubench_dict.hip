@@ -130,8 +130,20 @@ int main(int argc, char** argv) {
     ep.dict_len = 1024;
     ep.err = err;
     const unsigned g1 = unsigned(n_blocks / 32), g2 = unsigned(n_blocks / 16), g4 = unsigned(n_blocks / 8);
-    hipLaunchKernelGGL((fl_unpack_kernel<T, W, Epi::Dict, VW>), dim3(g1), dim3(256), 0, 0, in[0], ref, n_blocks, 0u,
-                       n_vals, ep);
+    // the library kernel takes a chunk table (one chunk here)
+    auto tab_of = [&](const uint8_t* src, void* dst) {
+        ChunkTable t{};
+        t.n = 1;
+        t.err = err;
+        t.c[0].packed = src;
+        t.c[0].out = dst;
+        t.c[0].n_blocks = n_blocks;
+        t.c[0].len = n_vals;
+        t.c[0].dict = dict;
+        t.c[0].dict_len = 1024;
+        return t;
+    };
+    hipLaunchKernelGGL((fl_unpack_kernel<T, W, Epi::Dict, VW>), dim3(g1), dim3(256), 0, 0, tab_of(in[0], ref));
     CK(hipDeviceSynchronize());
 
     struct Var { const char* name; int id; };
@@ -141,13 +153,13 @@ int main(int argc, char** argv) {
     const uint64_t cw = n_blocks / 8;  // copy: a wave per 8 blocks: reads 8*1280 B = 80 x 1 KiB? use rd=10 (x1KiB / 64 lanes*16B)
     auto launch = [&](int id, const uint8_t* src) {
         switch (id) {
-        case 0: hipLaunchKernelGGL((fl_unpack_kernel<T, W, Epi::Dict, VW, false>), dim3(g1), dim3(256), 0, 0, src, out, n_blocks, 0u, n_vals, ep); break;
-        case 1: hipLaunchKernelGGL((fl_unpack_kernel<T, W, Epi::Dict, VW, true>), dim3(g1), dim3(256), 0, 0, src, out, n_blocks, 0u, n_vals, ep); break;
+        case 0: hipLaunchKernelGGL((fl_unpack_kernel<T, W, Epi::Dict, VW, false>), dim3(g1), dim3(256), 0, 0, tab_of(src, out)); break;
+        case 1: hipLaunchKernelGGL((fl_unpack_kernel<T, W, Epi::Dict, VW, true>), dim3(g1), dim3(256), 0, 0, tab_of(src, out)); break;
         case 2: hipLaunchKernelGGL((k_split<T, W, Epi::Dict, VW, 1, true>), dim3(g1), dim3(256), 0, 0, src, out, n_blocks, ep); break;
         case 3: hipLaunchKernelGGL((k_split<T, W, Epi::Dict, VW, 2, true>), dim3(g2), dim3(256), 0, 0, src, out, n_blocks, ep); break;
         case 4: hipLaunchKernelGGL((k_split<T, W, Epi::Dict, VW, 4, true>), dim3(g4), dim3(256), 0, 0, src, out, n_blocks, ep); break;
         case 5: hipLaunchKernelGGL((k_split<T, W, Epi::Dict, VW, 4, false>), dim3(g4), dim3(256), 0, 0, src, out, n_blocks, ep); break;
-        case 6: hipLaunchKernelGGL((fl_unpack_kernel<T, W, Epi::Plain, 0>), dim3(g1), dim3(256), 0, 0, src, out, n_blocks, 0u, n_vals, ep); break;
+        case 6: hipLaunchKernelGGL((fl_unpack_kernel<T, W, Epi::Plain, 0>), dim3(g1), dim3(256), 0, 0, tab_of(src, out)); break;
         case 7: hipLaunchKernelGGL((k_split<T, W, Epi::Plain, 0, 4, false>), dim3(g4), dim3(256), 0, 0, src, out, n_blocks, ep); break;
         case 8: hipLaunchKernelGGL(k_copy<1>, dim3(unsigned(cw * 64 / 256)), dim3(256), 0, 0, (const uint4*)src, (uint4*)out, cw, 10, 64); break;
         }
