@@ -1299,15 +1299,35 @@ vxg_status vxg_plan_create(vxg_ctx* ctx, const vxg_array* arrays, vxg_canonical*
         if (a.nullable && !o.validity)
             return set_error(VXG_ERR_INVALID_ARGUMENT, "a plan needs caller-allocated validity for nullable arrays");
     }
+    // Record on an origin stream forked into up to kPlanBranches streams: the arrays are
+    // independent, so their launches become parallel graph branches (the graph runs them on
+    // several hardware queues, overlapping the ramp and drain of the many small kernels of a
+    // chunked scan), joined back into the origin stream.
+    constexpr uint32_t kPlanBranches = 4;
+    const uint32_t nb = n < kPlanBranches ? (n ? n : 1) : kPlanBranches;
     hipStream_t cs;
     VXG_TRY(hip_check(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking), "plan stream"));
+    std::vector<hipStream_t> br(nb, nullptr);
+    std::vector<hipEvent_t> ev(nb + 1, nullptr);
+    vxg_status st = VXG_OK;
+    for (uint32_t b = 0; b < nb && st == VXG_OK; b++)
+        st = hip_check(hipStreamCreateWithFlags(&br[b], hipStreamNonBlocking), "plan branch stream");
+    for (uint32_t b = 0; b <= nb && st == VXG_OK; b++)
+        st = hip_check(hipEventCreateWithFlags(&ev[b], hipEventDisableTiming), "plan event");
     auto* pl = new vxg_plan();
     pl->ctx = ctx;
-    vxg_status st = hip_check(hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed), "hipStreamBeginCapture");
+    if (st == VXG_OK) st = hip_check(hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed), "hipStreamBeginCapture");
     if (st == VXG_OK) {
+        st = hip_check(hipEventRecord(ev[nb], cs), "fork");
+        for (uint32_t b = 0; b < nb && st == VXG_OK; b++)
+            st = hip_check(hipStreamWaitEvent(br[b], ev[nb], 0), "fork wait");
         for (uint32_t i = 0; i < n && st == VXG_OK; i++) {
-            Planner p(ctx, cs, &pl->temps);
+            Planner p(ctx, br[i % nb], &pl->temps);
             st = p.canonical(arrays[i], outs[i]);
+        }
+        for (uint32_t b = 0; b < nb && st == VXG_OK; b++) {
+            st = hip_check(hipEventRecord(ev[b], br[b]), "join");
+            if (st == VXG_OK) st = hip_check(hipStreamWaitEvent(cs, ev[b], 0), "join wait");
         }
         hipGraph_t g = nullptr;
         const hipError_t e = hipStreamEndCapture(cs, &g);
@@ -1316,6 +1336,10 @@ vxg_status vxg_plan_create(vxg_ctx* ctx, const vxg_array* arrays, vxg_canonical*
         if (st == VXG_OK)
             st = hip_check(hipGraphInstantiate(&pl->exec, g, nullptr, nullptr, 0), "hipGraphInstantiate");
     }
+    for (hipEvent_t e : ev)
+        if (e) (void)hipEventDestroy(e);
+    for (hipStream_t b : br)
+        if (b) (void)hipStreamDestroy(b);
     (void)hipStreamDestroy(cs);
     if (st == VXG_OK) *plan = pl;
     else vxg_plan_destroy(pl);
