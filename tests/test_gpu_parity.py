@@ -579,3 +579,38 @@ def test_plan_lineitem_columns(ctx):
             else:
                 assert r.numpy().tobytes() == np.concatenate(plain[name]).tobytes(), name
     plan.close()
+
+
+# ------------------------------------------------------------------ edge cases: empty inputs
+def test_empty_arrays_every_encoding(ctx):
+    """len = 0 through every encoding and container (the reference canonicalizes empty arrays
+    to empty canonical arrays): no launch may touch memory, outputs are empty."""
+    empty_u32 = np.zeros(0, np.uint32)
+    cases = [
+        E.encode_bitpacked(empty_u32, bit_width=5, allow_patches=False),
+        E.encode_for_bitpacked(np.zeros(0, np.int64)),
+        E.encode_zigzag(np.zeros(0, np.int32)),
+        E.encode_alp(np.zeros(0, np.float64), cascade=False),
+        A.dict_array(A.primitive(np.array([7, 9], np.uint16)), A.primitive(np.zeros(0, np.uint32))),
+        A.constant(5, 0, "i64"),
+        A.chunked([E.encode_bitpacked(np.arange(3000, dtype=np.uint32) % 64, bit_width=6),
+                   A.primitive(np.zeros(0, np.uint32)),
+                   E.encode_bitpacked(np.arange(100, dtype=np.uint32) % 64, bit_width=6)]),
+    ]
+    for arr in cases:
+        assert_primitive_parity(arr, ctx)
+    heap, offs, _ = E.strings_to_heap([])
+    assert_string_parity(A.varbin(A.primitive(offs.astype(np.int32)), A.primitive(heap)), ctx, [])
+    assert_string_parity(A.chunked([E.encode_fsst([b"only one string here!"]), E.encode_varbinview([])]), ctx,
+                         [b"only one string here!"])
+
+
+def test_ragged_single_element_chunks(ctx):
+    """Chunks of 1, 2, 1023, 1025 values (ragged FastLanes tails) in one grouped launch."""
+    rng = np.random.default_rng(77)
+    chunks, expect = [], []
+    for n in [1, 2, 1023, 1024, 1025, 1, 7, 4097]:
+        v = rng.integers(0, 1 << 9, n, dtype=np.uint64).astype(np.uint16)
+        chunks.append(E.encode_bitpacked(v, bit_width=9, allow_patches=False))
+        expect.append(v)
+    assert_primitive_parity(A.chunked(chunks), ctx, np.concatenate(expect))

@@ -66,6 +66,8 @@ class Array:
             if isinstance(b, torch.Tensor):
                 return b.to(device)
             a = np.ascontiguousarray(b).view(np.uint8).reshape(-1)
+            if not a.flags.writeable:
+                a = a.copy()  # torch.from_numpy needs a writable buffer
             t = torch.empty(max(a.size, 16), dtype=torch.uint8, device=device)
             if a.size:
                 t[: a.size].copy_(torch.from_numpy(a))
