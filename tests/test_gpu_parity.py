@@ -557,15 +557,17 @@ def test_plan_graph_replay_matches_direct(ctx):
     plan.close()
 
 
-def test_plan_lineitem_columns(ctx):
+@pytest.mark.parametrize("rows,cr", [(3 * 8192 + 99, 8192), (100 * 1024 + 77, 1024)])
+def test_plan_lineitem_columns(ctx, rows, cr):
     """vxg_plan over the lineitem columns (RunEnd, Dict strings, FSST chunks: planner
-    temporaries live with the plan) equals the oracle on every replay."""
+    temporaries live with the plan) equals the oracle on every replay.  101 chunks per column
+    exceed every kernel-argument table (K1 32, FSST 24, RunEnd/VarBin 48): the plan records
+    one launch per kernel group over a device-resident chunk table."""
     import sys
     import torch
     from pathlib import Path
     sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
     from tools import lineitem as L
-    rows, cr = 3 * 8192 + 99, 8192
     cols, plain = L.lineitem_columns(range(L.n_chunks(rows, cr)), rows=rows, chunk_rows=cr)
     arrs = [cols[name] for name, _ in L.COLUMNS]
     plan = V.Plan([a.to(torch.device("cuda", 0)) for a in arrs], ctx)

@@ -10,7 +10,8 @@ import os
 from pathlib import Path
 
 _HERE = Path(__file__).resolve().parent
-GPU_LIB_PATH = _HERE / "libvortex_gpu.so"
+# VXG_GPU_LIB: load another build of the engine (A/B experiments); default the in-tree one
+GPU_LIB_PATH = Path(os.environ["VXG_GPU_LIB"]) if os.environ.get("VXG_GPU_LIB") else _HERE / "libvortex_gpu.so"
 ENC_LIB_PATH = _HERE / "libvortex_enc.so"
 
 # ---- ids mirrored from include/vortex_gpu.h (reference encoding/mod.rs:106-147) ----------

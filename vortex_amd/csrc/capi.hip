@@ -97,6 +97,12 @@ using namespace vxg;
 
 namespace {
 
+#define VXG_TRY_S(expr)                       \
+    do {                                      \
+        vxg_status _s = (expr);               \
+        if (_s != VXG_OK) return _s;          \
+    } while (0)
+
 // One K1 decode (a whole BitPacked-rooted cascade of one array or one chunk) and the kernel
 // it needs.  Jobs with the same kernel share launches.
 struct K1Job {
@@ -112,20 +118,30 @@ bool same_kernel(const K1Job& a, const K1Job& b) {
 
 // Launch K1 jobs grouped by kernel (T, W, epilogue, value width), kArgChunks chunks per launch
 // with the chunk table as the kernel argument (no device table, no upload, no host sync).
-vxg_status launch_k1_jobs(std::vector<K1Job>& jobs, uint32_t* err, hipStream_t s) {
+// While a plan is recorded (dt set), a group of any size is one launch over a device table.
+vxg_status launch_k1_jobs(std::vector<K1Job>& jobs, uint32_t* err, hipStream_t s, DevTables* dt = nullptr) {
     std::stable_sort(jobs.begin(), jobs.end(), [](const K1Job& a, const K1Job& b) {
         return std::make_tuple(a.T, a.W, int(a.epi), a.vw) < std::make_tuple(b.T, b.W, int(b.epi), b.vw);
     });
     size_t i = 0;
     while (i < jobs.size()) {
-        size_t j = i;
-        while (j < jobs.size() && j - i < size_t(kArgChunks) && same_kernel(jobs[i], jobs[j])) j++;
+        size_t j = i, live = 0;
+        while (j < jobs.size() && (dt || j - i < size_t(kArgChunks)) && same_kernel(jobs[i], jobs[j])) {
+            live += jobs[j].d.n_blocks != 0;
+            j++;
+        }
         ChunkTable tab{};
         tab.err = err;
+        ChunkDev* cs = tab.c;
+        if (live > size_t(kArgChunks)) {  // only when dt is set
+            if (live > 0xFFFFFFFFull) return set_error(VXG_ERR_INVALID_ARGUMENT, "too many chunks");
+            VXG_TRY_S(dt->table(live, &tab.host, &tab.ext));
+            cs = tab.host;
+        }
         uint64_t groups = 0;
         for (size_t k = i; k < j; k++) {
             if (jobs[k].d.n_blocks == 0) continue;
-            ChunkDev& c = tab.c[tab.n++];
+            ChunkDev& c = cs[tab.n++];
             c = jobs[k].d;
             c.first_group = groups;
             groups += (c.n_blocks + 31) / 32;
@@ -200,7 +216,7 @@ vxg_status bitunpack_common(vxg_ctx* ctx, int T, unsigned W, unsigned offset, ui
 // ===================================================================================
 class Planner {
   public:
-    Planner(vxg_ctx* ctx, hipStream_t s, std::vector<void*>* owned = nullptr) : ctx_(ctx), s_(s), owned_(owned) {}
+    Planner(vxg_ctx* ctx, hipStream_t s, DevTables* plan = nullptr) : ctx_(ctx), s_(s), plan_(plan) {}
     ~Planner() {
         for (void* p : temps_) (void)hipFreeAsync(p, s_);
     }
@@ -216,8 +232,9 @@ class Planner {
     hipStream_t s_;
     std::vector<void*> temps_;
     // Recording a plan: temporaries are plain allocations owned by the plan (alive for all its
-    // replays) instead of stream-ordered ones.
-    std::vector<void*>* owned_ = nullptr;
+    // replays) instead of stream-ordered ones, and chunk tables longer than a kernel argument
+    // holds become device tables (one launch per kernel group).
+    DevTables* plan_ = nullptr;
     // Deferred K1 decodes of the chunks of a ChunkedArray (grouped into shared launches) and
     // the patch scatters that must follow them; null = launch immediately.
     struct PatchJob {
@@ -236,9 +253,9 @@ class Planner {
 
     vxg_status temp(uint64_t bytes, void** p) {
         if (bytes == 0) bytes = 16;
-        if (owned_) {
+        if (plan_) {
             VXG_TRY(hip_check(hipMalloc(p, (bytes + 15) & ~15ull), "hipMalloc (plan temporary)"));
-            owned_->push_back(*p);
+            plan_->allocs.push_back(*p);
             return VXG_OK;
         }
         VXG_TRY(hip_check(hipMallocAsync(p, (bytes + 15) & ~15ull, s_), "hipMallocAsync"));
@@ -369,7 +386,7 @@ vxg_status Planner::decode_bitpacked(const vxg_array& bp, Epi epi, int vw, Unpac
         return VXG_OK;
     }
     std::vector<K1Job> one{j};
-    VXG_TRY(launch_k1_jobs(one, ctx_->c.err_word, s_));
+    VXG_TRY(launch_k1_jobs(one, ctx_->c.err_word, s_, plan_));
     if (p) VXG_TRY(apply_sparse_patches(*p, T, epi, vw, a, dst, bp.len));
     return VXG_OK;
 }
@@ -554,15 +571,22 @@ vxg_status Planner::decode_chunked_primitive(const vxg_array& a, void* dst) {
         off += c.len;
     }
     if (off != a.len) return set_error(VXG_ERR_INVALID_ARGUMENT, "Chunked len != sum of chunk lens");
-    VXG_TRY(launch_k1_jobs(jobs, ctx_->c.err_word, s_));
+    VXG_TRY(launch_k1_jobs(jobs, ctx_->c.err_word, s_, plan_));
     for (const PatchJob& p : patches) VXG_TRY(apply_sparse_patches(*p.sp, p.T, p.epi, p.vw, p.a, p.dst, p.out_len));
-    for (size_t i = 0; i < runs.size(); i += kRunEndArgChunks) {
+    runs.erase(std::remove_if(runs.begin(), runs.end(), [](const RunEndChunk& r) { return r.len == 0; }), runs.end());
+    const size_t per = plan_ && runs.size() > size_t(kRunEndArgChunks) ? runs.size() : size_t(kRunEndArgChunks);
+    for (size_t i = 0; i < runs.size(); i += per) {
         RunEndTable tab{};
         tab.err = ctx_->c.err_word;
+        RunEndChunk* cs = tab.c;
+        RunEndChunk* host = nullptr;
+        if (per > size_t(kRunEndArgChunks)) {
+            VXG_TRY(plan_->table(runs.size(), &host, &tab.ext));
+            cs = host;
+        }
         uint64_t groups = 0;
-        for (size_t k = i; k < runs.size() && k - i < size_t(kRunEndArgChunks); k++) {
-            if (runs[k].len == 0) continue;
-            RunEndChunk& r = tab.c[tab.n++];
+        for (size_t k = i; k < runs.size() && k - i < per; k++) {
+            RunEndChunk& r = cs[tab.n++];
             r = runs[k];
             r.first_group = groups;
             groups += (r.len + 2047) / 2048;
@@ -956,7 +980,7 @@ vxg_status Planner::strings_into(const vxg_array& a, uint8_t* views, uint8_t* da
         std::vector<FsstChunk> one{f};
         void* scratch;
         VXG_TRY(temp(fsst_batch_scratch_bytes(one.data(), 1), &scratch));
-        return launch_fsst_batch(one, scratch, ctx_->c.err_word, s_);
+        return launch_fsst_batch(one, scratch, ctx_->c.err_word, s_, plan_);
     }
     case VXG_ENC_DICT: {
         // Dict over string values: take on the values' views (varbinview/compute.rs:68-76); the
@@ -1065,20 +1089,27 @@ vxg_status Planner::strings_into(const vxg_array& a, uint8_t* views, uint8_t* da
         if (!fssts.empty()) {
             void* scratch;
             VXG_TRY(temp(fsst_batch_scratch_bytes(fssts.data(), fssts.size()), &scratch));
-            VXG_TRY(launch_fsst_batch(fssts, scratch, ctx_->c.err_word, s_));
+            VXG_TRY(launch_fsst_batch(fssts, scratch, ctx_->c.err_word, s_, plan_));
         }
-        for (size_t i = 0; i < dicts.size(); i += kVarBinArgChunks) {
+        const size_t per = plan_ && dicts.size() > size_t(kVarBinArgChunks) ? dicts.size() : size_t(kVarBinArgChunks);
+        for (size_t i = 0; i < dicts.size(); i += per) {
             VarBinTable tab{};
+            VarBinChunk* cs = tab.c;
+            if (per > size_t(kVarBinArgChunks)) {
+                VarBinChunk* host;
+                VXG_TRY(plan_->table(dicts.size(), &host, &tab.ext));
+                cs = host;
+            }
             uint64_t groups = 0;
-            for (size_t j = i; j < dicts.size() && j - i < size_t(kVarBinArgChunks); j++) {
-                VarBinChunk& d = tab.c[tab.n++];
+            for (size_t j = i; j < dicts.size() && j - i < per; j++) {
+                VarBinChunk& d = cs[tab.n++];
                 d = dicts[j];
                 d.first_group = groups;
                 groups += d.n ? (d.n + 255) / 256 : 1;
             }
             VXG_TRY(launch_varbin_chunks(tab, groups, s_));
         }
-        VXG_TRY(launch_k1_jobs(jobs, ctx_->c.err_word, s_));
+        VXG_TRY(launch_k1_jobs(jobs, ctx_->c.err_word, s_, plan_));
         for (const PatchJob& p : patches) VXG_TRY(apply_sparse_patches(*p.sp, p.T, p.epi, p.vw, p.a, p.dst, p.out_len));
         return VXG_OK;
     }
@@ -1281,7 +1312,7 @@ struct vxg_plan {
     vxg_ctx* ctx = nullptr;
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
-    std::vector<void*> temps;  // the recorded launches' temporaries
+    DevTables store;  // the recorded launches' temporaries and device chunk tables
 };
 
 extern "C" {
@@ -1322,7 +1353,7 @@ vxg_status vxg_plan_create(vxg_ctx* ctx, const vxg_array* arrays, vxg_canonical*
         for (uint32_t b = 0; b < nb && st == VXG_OK; b++)
             st = hip_check(hipStreamWaitEvent(br[b], ev[nb], 0), "fork wait");
         for (uint32_t i = 0; i < n && st == VXG_OK; i++) {
-            Planner p(ctx, br[i % nb], &pl->temps);
+            Planner p(ctx, br[i % nb], &pl->store);
             st = p.canonical(arrays[i], outs[i]);
         }
         for (uint32_t b = 0; b < nb && st == VXG_OK; b++) {
@@ -1335,6 +1366,7 @@ vxg_status vxg_plan_create(vxg_ctx* ctx, const vxg_array* arrays, vxg_canonical*
         pl->graph = g;
         if (st == VXG_OK)
             st = hip_check(hipGraphInstantiate(&pl->exec, g, nullptr, nullptr, 0), "hipGraphInstantiate");
+        if (st == VXG_OK) st = pl->store.upload();  // device chunk tables, once for all replays
     }
     for (hipEvent_t e : ev)
         if (e) (void)hipEventDestroy(e);
@@ -1357,8 +1389,8 @@ vxg_status vxg_plan_destroy(vxg_plan* plan) {
     if (plan->ctx) (void)hipSetDevice(plan->ctx->c.device);
     if (plan->exec) (void)hipGraphExecDestroy(plan->exec);
     if (plan->graph) (void)hipGraphDestroy(plan->graph);
-    if (!plan->temps.empty()) (void)hipDeviceSynchronize();  // no replay may still use them
-    for (void* p : plan->temps) (void)hipFree(p);
+    if (!plan->store.allocs.empty()) (void)hipDeviceSynchronize();  // no replay may still use them
+    for (void* p : plan->store.allocs) (void)hipFree(p);
     delete plan;
     return VXG_OK;
 }

@@ -348,13 +348,18 @@ template <int T, int W, Epi EPI, int VW, bool LDSD = false, int S = 1>
 __global__ __launch_bounds__(256) void fl_unpack_kernel(ChunkTable tab) {
     using O = typename EpiOut<T, EPI, VW>::type;
     constexpr int BPG = 32 / S;  // blocks per workgroup
-    uint32_t lo = 0, hi = tab.n;
     const uint64_t g = blockIdx.x;
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (tab.c[mid].first_group <= g) lo = mid; else hi = mid;
+    ChunkDev c;  // this workgroup's chunk (scalar registers)
+    if (tab.ext) {
+        c = tab.ext[ext_chunk_index(tab.ext, tab.n, g, [](const ChunkDev& d) { return d.first_group; })];
+    } else {
+        uint32_t lo = 0, hi = tab.n;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (tab.c[mid].first_group <= g) lo = mid; else hi = mid;
+        }
+        c = tab.c[lo];
     }
-    const ChunkDev& c = tab.c[lo];
     const uint64_t blk = (g - c.first_group) * BPG + ((threadIdx.x >> 3) % BPG);
     const int t = int(threadIdx.x & 7);
     EpiParams ep;
@@ -397,10 +402,13 @@ constexpr uint64_t kSplitBelowGroups = 512;
 
 template <int T, int W, Epi EPI, int VW, bool LDSD, int S>
 vxg_status launch_s(ChunkTable tab, hipStream_t s) {
+    // first workgroup of each chunk at this launch's blocks per workgroup (a device table's
+    // host mirror is completed here and uploaded when the plan is finalised)
+    ChunkDev* cs = tab.ext ? tab.host : tab.c;
     uint64_t groups = 0;
     for (uint32_t k = 0; k < tab.n; k++) {
-        tab.c[k].first_group = groups;
-        groups += (tab.c[k].n_blocks + (32 / S) - 1) / (32 / S);
+        cs[k].first_group = groups;
+        groups += (cs[k].n_blocks + (32 / S) - 1) / (32 / S);
     }
     if (groups == 0) return VXG_OK;
     if (groups > 0xFFFFFFFFull) return set_error(VXG_ERR_INVALID_ARGUMENT, "array too long for one launch");
@@ -416,10 +424,11 @@ vxg_status launch_one(const ChunkTable& tab, uint64_t groups32, hipStream_t s) {
     const bool split = kSplit && groups32 < kSplitBelowGroups;
     bool lds = false;
     if constexpr (EPI == Epi::Dict) {
+        const ChunkDev* cs = tab.ext ? tab.host : tab.c;
         lds = true;
         for (uint32_t k = 0; k < tab.n; k++)
-            lds = lds && tab.c[k].dict_len * VW <= uint64_t(kDictLdsBytes) &&
-                  (reinterpret_cast<uintptr_t>(tab.c[k].dict) & 15) == 0;
+            lds = lds && cs[k].dict_len * VW <= uint64_t(kDictLdsBytes) &&
+                  (reinterpret_cast<uintptr_t>(cs[k].dict) & 15) == 0;
     }
     if constexpr (kSplit) {
         if (split) return lds ? launch_s<T, W, EPI, VW, true, 4>(tab, s) : launch_s<T, W, EPI, VW, false, 4>(tab, s);

@@ -177,19 +177,20 @@ __device__ __forceinline__ void scan_tile_sums(const int64_t* s_ts, int64_t* ws,
     if (tid == 0) block_totals[sb] = tot;
 }
 
-// Chunk of workgroup g in a launch (workgroup-uniform binary search on the table's first_*).
+// Chunk of workgroup g in a launch: workgroup-uniform binary search on the kernarg table's
+// first_*, or the wave-wide count over a recorded plan's device table (returned by value:
+// the fields the kernel uses land in scalar registers).
 template <bool SCAN>
-__device__ __forceinline__ uint32_t fsst_chunk_index(const FsstTable& tab, uint64_t g) {
+__device__ __forceinline__ FsstChunk fsst_chunk_of(const FsstTable& tab, uint64_t g) {
+    if (tab.ext)
+        return tab.ext[ext_chunk_index(tab.ext, tab.n, g,
+                                       [](const FsstChunk& d) { return SCAN ? d.first_scan : d.first_tile; })];
     uint32_t lo = 0, hi = tab.n;
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
         if ((SCAN ? tab.c[mid].first_scan : tab.c[mid].first_tile) <= g) lo = mid; else hi = mid;
     }
-    return lo;
-}
-template <bool SCAN>
-__device__ __forceinline__ const FsstChunk& fsst_chunk_of(const FsstTable& tab, uint64_t g) {
-    return tab.c[fsst_chunk_index<SCAN>(tab, g)];
+    return tab.c[lo];
 }
 
 // Any length column: wave w sums tile 4r + w in round r (4 consecutive lengths per lane).
@@ -199,7 +200,7 @@ __global__ __launch_bounds__(kTile) void fsst_tile_scan(FsstTable tab, int64_t* 
     __shared__ int64_t s_ts[kScanTiles];
     __shared__ int64_t ws[kTile / 64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const FsstChunk& c = fsst_chunk_of<true>(tab, blockIdx.x);
+    const FsstChunk c = fsst_chunk_of<true>(tab, blockIdx.x);
     const LenAcc lens(c.lens);
     const uint64_t n = c.n, n_tiles = (n + kTile - 1) / kTile, sb = blockIdx.x - c.first_scan;
     int64_t* const tile_prefix = tile_prefix_all + c.first_tile;
@@ -257,7 +258,7 @@ __global__ __launch_bounds__(kTile) void fsst_tile_scan_fl32(FsstTable tab, int6
     __shared__ int64_t s_ts[kScanTiles];
     __shared__ int64_t ws[kTile / 64];
     const int tid = threadIdx.x, t = tid & 7;
-    const FsstChunk& c = fsst_chunk_of<true>(tab, blockIdx.x);
+    const FsstChunk c = fsst_chunk_of<true>(tab, blockIdx.x);
     const uint8_t* __restrict__ packed = static_cast<const uint8_t*>(c.lens.p);
     const uint32_t shift = c.lens.shift, reference = uint32_t(c.lens.reference);
     const bool sgn = c.lens.sgn;
@@ -305,7 +306,7 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
     uint8_t* const s_heap = reinterpret_cast<uint8_t*>(s_heap32);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 
-    const FsstChunk& ch = fsst_chunk_of<false>(tab, blockIdx.x);
+    const FsstChunk ch = fsst_chunk_of<false>(tab, blockIdx.x);
     const uint64_t* __restrict__ symbols = ch.symbols;
     const uint8_t* __restrict__ sym_lens = ch.sym_lens;
     const unsigned n_symbols = ch.n_symbols;
@@ -616,7 +617,8 @@ bool with_acc(int kind, F&& f) {
 
 }  // namespace
 
-vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint32_t* err, hipStream_t s) {
+vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint32_t* err, hipStream_t s,
+                             DevTables* dt) {
     for (const FsstChunk& c : chunks) {
         if (c.n_symbols > 255) return set_error(VXG_ERR_INVALID_ARGUMENT, "FSST symbol table > 255 entries");
         if ((c.n + kTile - 1) / kTile > 0xFFFFFFFFull) return set_error(VXG_ERR_INVALID_ARGUMENT, "FSST array too long");
@@ -632,11 +634,22 @@ vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint
     while (i < chunks.size()) {
         FsstTable tab{};
         uint64_t tiles = 0, scans = 0;
-        size_t j = i;
-        for (; j < chunks.size() && j - i < size_t(kFsstArgChunks) && fsst_key(chunks[j]) == fsst_key(chunks[i]); j++) {
-            if (chunks[j].n == 0) continue;
-            FsstChunk& c = tab.c[tab.n++];
-            c = chunks[j];
+        // one launch pair per kernarg table of kFsstArgChunks, or (recording a plan) per
+        // accessor group over a device table
+        size_t j = i, live = 0;
+        while (j < chunks.size() && (dt || j - i < size_t(kFsstArgChunks)) && fsst_key(chunks[j]) == fsst_key(chunks[i]))
+            live += chunks[j++].n != 0;
+        FsstChunk* cs = tab.c;
+        if (live > size_t(kFsstArgChunks)) {
+            FsstChunk* host;
+            const vxg_status st = dt->table(live, &host, &tab.ext);
+            if (st != VXG_OK) return st;
+            cs = host;
+        }
+        for (size_t k = i; k < j; k++) {
+            if (chunks[k].n == 0) continue;
+            FsstChunk& c = cs[tab.n++];
+            c = chunks[k];
             const uint64_t nt = (c.n + kTile - 1) / kTile;
             c.first_tile = tiles;
             c.first_scan = scans;
@@ -647,7 +660,7 @@ vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint
             int64_t* tp = tiles_all;
             int64_t* bt = tiles_all + tiles;
             tiles_all += tiles + scans;
-            const auto key = fsst_key(tab.c[0]);
+            const auto key = fsst_key(cs[0]);
             if (std::get<2>(key) >= 0)
                 launch_tile_scan_fl32(std::get<2>(key), dim3(unsigned(scans)), s, tab, tp, bt,
                                       std::make_integer_sequence<int, 33>{});

@@ -573,13 +573,18 @@ __global__ __launch_bounds__(kBlock) void runend_chunks_kernel(RunEndTable tab) 
     __shared__ uint32_t s_head[SPAN];
     __shared__ uint32_t s_wmax[kBlock / 64];
     __shared__ uint64_t s_r[2];
-    uint32_t lo = 0, hi = tab.n;
     const uint64_t g = blockIdx.x;
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (tab.c[mid].first_group <= g) lo = mid; else hi = mid;
+    RunEndChunk c;  // this workgroup's chunk: kernarg table (binary search) or a plan's device table
+    if (tab.ext) {
+        c = tab.ext[ext_chunk_index(tab.ext, tab.n, g, [](RunEndChunk const& d) { return d.first_group; })];
+    } else {
+        uint32_t lo = 0, hi = tab.n;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (tab.c[mid].first_group <= g) lo = mid; else hi = mid;
+        }
+        c = tab.c[lo];
     }
-    const RunEndChunk& c = tab.c[lo];
     const V* __restrict__ values = static_cast<const V*>(c.values);
     V* __restrict__ out = static_cast<V*>(c.out);
     const int ew = int(c.ends_width), tid = threadIdx.x;
@@ -726,13 +731,18 @@ vxg_status launch_varbin_views(const uint8_t* heap, int offs_width, const void* 
 // Chunk-table VarBin -> views: workgroup g of a chunk copies its share of the bytes into the
 // output data buffer and builds the views of rows [256 (g - first_group), +256).
 __global__ __launch_bounds__(kBlock) void varbin_chunks_kernel(VarBinTable tab) {
-    uint32_t lo = 0, hi = tab.n;
     const uint64_t g = blockIdx.x;
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (tab.c[mid].first_group <= g) lo = mid; else hi = mid;
+    VarBinChunk c;  // this workgroup's chunk: kernarg table (binary search) or a plan's device table
+    if (tab.ext) {
+        c = tab.ext[ext_chunk_index(tab.ext, tab.n, g, [](VarBinChunk const& d) { return d.first_group; })];
+    } else {
+        uint32_t lo = 0, hi = tab.n;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (tab.c[mid].first_group <= g) lo = mid; else hi = mid;
+        }
+        c = tab.c[lo];
     }
-    const VarBinChunk& c = tab.c[lo];
     const uint64_t lg = g - c.first_group;
     const uint64_t ng = (c.n + kBlock - 1) / kBlock > 0 ? (c.n + kBlock - 1) / kBlock : 1;
     const uint64_t per = (c.bytes + ng - 1) / ng;

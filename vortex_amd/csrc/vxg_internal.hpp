@@ -65,6 +65,51 @@ struct Ctx {
 vxg_status set_error(vxg_status s, const std::string& msg);
 vxg_status hip_check(hipError_t e, const char* what);
 
+// ---- chunk tables beyond the kernel-argument limit --------------------------------------
+// A launch's chunk table normally travels as the kernel argument (<= 4 KiB: no upload, no host
+// sync).  While a vxg_plan is recorded, a launch may instead cover any number of chunks with a
+// device-resident table ("ext"): its entries are built in a host mirror during recording and
+// copied to the device once when the plan is finalised, so replays cost nothing extra.
+struct DevTables {
+    std::vector<void*> allocs;                                     // owned device memory
+    std::vector<std::pair<void*, std::vector<uint8_t>>> uploads;   // (device, host mirror)
+    // n zeroed entries: returns the host mirror (valid until upload()), *dev its device copy
+    template <class E>
+    vxg_status table(size_t n, E** host, const E** dev) {
+        void* d = nullptr;
+        const hipError_t e = hipMalloc(&d, n * sizeof(E) + 16);
+        if (e != hipSuccess) return hip_check(e, "hipMalloc (plan chunk table)");
+        allocs.push_back(d);
+        uploads.emplace_back(d, std::vector<uint8_t>(n * sizeof(E), 0));
+        *host = reinterpret_cast<E*>(uploads.back().second.data());
+        *dev = static_cast<const E*>(d);
+        return VXG_OK;
+    }
+    vxg_status upload() {
+        for (auto& u : uploads) {
+            const hipError_t e = hipMemcpy(u.first, u.second.data(), u.second.size(), hipMemcpyHostToDevice);
+            if (e != hipSuccess) return hip_check(e, "plan chunk table upload");
+        }
+        uploads.clear();
+        return VXG_OK;
+    }
+};
+
+// Index of the entry of a device-resident table (sorted by its first workgroup, entry 0 first
+// = 0) that covers workgroup g: every lane of the wave compares one entry per round (all loads
+// in flight together) and the ballot counts give the index -- wave-uniform, no dependent chain.
+template <class E, class Key>
+__device__ __forceinline__ uint32_t ext_chunk_index(const E* __restrict__ ext, uint32_t n, uint64_t g, Key key) {
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t cnt = 0;
+    for (uint32_t base = 0; base < n; base += 64) {
+        const uint32_t i = base + lane;
+        const bool le = i < n && key(ext[i]) <= g;
+        cnt += uint32_t(__popcll(__ballot(le)));
+    }
+    return cnt ? cnt - 1 : 0;
+}
+
 // ---- launchers implemented in the .hip translation units -----------------------------
 // Epilogue kinds of the fused FastLanes unpack.
 enum class Epi : int { Plain = 0, For = 1, ForZigZag = 2, AlpF32 = 3, AlpF64 = 4, Dict = 5 };
@@ -98,12 +143,16 @@ struct ChunkDev {
     uint32_t offset;        // values to skip in block 0 (< 1024)
     uint32_t shift;         // FoR shift
 };
-// Up to kArgChunks descriptors travel as the kernel argument (~2.8 KB kernarg).
+// Up to kArgChunks descriptors travel as the kernel argument (~2.8 KB kernarg); a recorded
+// plan's launch may use a device table of any length instead (ext: device, host: its mirror,
+// which the host-side launch code reads and completes before the upload).
 constexpr int kArgChunks = 32;
 struct ChunkTable {
     ChunkDev c[kArgChunks];
     uint32_t n;
     uint32_t* err;
+    const ChunkDev* ext;
+    ChunkDev* host;
 };
 
 // T in {8,16,32,64} bits; value_width only used for Epi::Dict.  `groups` = total 32-block
@@ -180,6 +229,7 @@ struct RunEndTable {
     RunEndChunk c[kRunEndArgChunks];
     uint32_t n;
     uint32_t* err;
+    const RunEndChunk* ext;  // device table of n entries (plans), or null
 };
 vxg_status launch_runend_chunks(int value_width, const RunEndTable& t, uint64_t groups, hipStream_t s);
 
@@ -200,6 +250,7 @@ constexpr int kVarBinArgChunks = 48;
 struct VarBinTable {
     VarBinChunk c[kVarBinArgChunks];
     uint32_t n;
+    const VarBinChunk* ext;  // device table of n entries (plans), or null
 };
 vxg_status launch_varbin_chunks(const VarBinTable& t, uint64_t groups, hipStream_t s);
 
@@ -225,13 +276,15 @@ constexpr int kFsstArgChunks = 24;
 struct FsstTable {
     FsstChunk c[kFsstArgChunks];
     uint32_t n;
+    const FsstChunk* ext;  // device table of n entries (plans), or null
 };
 // Scratch for a set of chunks (tile prefixes + scan-block totals).
 uint64_t fsst_scratch_bytes(uint64_t n);
 uint64_t fsst_batch_scratch_bytes(const FsstChunk* chunks, size_t n_chunks);
 // Decode every chunk: grouped by accessor kinds, kFsstArgChunks per launch pair (pre-pass +
 // decode).  `scratch` >= fsst_batch_scratch_bytes.
-vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint32_t* err, hipStream_t s);
+vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint32_t* err, hipStream_t s,
+                             DevTables* dt = nullptr);
 // Views carry `bidx` as the buffer_index of non-inlined rows.
 vxg_status launch_varbin_views(const uint8_t* heap, int offs_width, const void* offsets, uint64_t n,
                                const uint8_t* validity, uint32_t bidx, uint8_t* views, hipStream_t s);
