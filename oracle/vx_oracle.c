@@ -380,6 +380,60 @@ int vxo_runend_decode(int val_width, const void* values, int ends_ptype, const v
     return pos == len ? 0 : -1;
 }
 
+/* ======================================================================================
+ * Bool encodings.  RunEndBool: encodings/runend-bool/src/compress.rs:46-93 (decode), :16-41
+ * (encode, BooleanBuffer::set_slices = maximal runs of set bits); ByteBool:
+ * encodings/bytebool/src/array.rs:138-146 (bytes reinterpreted as bools -> BooleanBuffer).
+ * ====================================================================================== */
+static int get_bit(const uint8_t* b, size_t i) { return (b[i >> 3] >> (i & 7)) & 1; }
+static void put_bit(uint8_t* b, size_t i, int v) {
+    if (v) b[i >> 3] |= (uint8_t)(1u << (i & 7));
+}
+
+int vxo_runend_bool_decode(int ends_ptype, const void* ends, size_t n_runs, size_t offset, int start,
+                           size_t len, uint8_t* out_bits) {
+    const unsigned ew = 8u * (unsigned)vxo_ptype_width(ends_ptype);
+    memset(out_bits, 0, (len + 7) / 8);
+    size_t pos = 0;
+    for (size_t r = 0; r < n_runs; r++) {
+        uint64_t end = load_word(ew, ends, r) - (uint64_t)offset; /* trimmed_ends */
+        if (end > len) end = len;
+        if (end < pos) return -1;
+        const int v = (r % 2 == 0) ? (start != 0) : (start == 0); /* value_at_index */
+        for (; pos < end; pos++) put_bit(out_bits, pos, v);
+    }
+    return pos == len ? 0 : -1;
+}
+
+size_t vxo_runend_bool_encode(const uint8_t* bits, size_t len, uint64_t* ends, int* start) {
+    size_t n = 0, i = 0;
+    /* first set slice */
+    while (i < len && !get_bit(bits, i)) i++;
+    if (i == len) { /* no set bits */
+        ends[0] = len;
+        *start = 0;
+        return 1;
+    }
+    *start = i == 0;
+    if (i != 0) ends[n++] = i;
+    for (;;) {
+        size_t e = i;
+        while (e < len && get_bit(bits, e)) e++;
+        ends[n++] = e; /* end of the set slice */
+        i = e;
+        while (i < len && !get_bit(bits, i)) i++;
+        if (i == len) break;
+        ends[n++] = i; /* start of the next set slice */
+    }
+    if (ends[n - 1] != len) ends[n++] = len;
+    return n;
+}
+
+void vxo_bytebool_to_bits(const uint8_t* bytes, size_t n, uint8_t* out_bits) {
+    memset(out_bits, 0, (n + 7) / 8);
+    for (size_t i = 0; i < n; i++) put_bit(out_bits, i, bytes[i] != 0);
+}
+
 void vxo_fill(int val_width, const void* scalar, size_t n, void* out) {
     for (size_t i = 0; i < n; i++) memcpy((uint8_t*)out + i * val_width, scalar, val_width);
 }

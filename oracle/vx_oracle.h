@@ -97,6 +97,19 @@ int vxo_take(int val_width, const void* values, size_t n_values,
 int vxo_runend_decode(int val_width, const void* values, int ends_ptype, const void* ends,
                       size_t n_runs, size_t offset, size_t len, void* out);
 
+/* ---- Bool encodings (canonical Bool = LSB bit buffer, arrow BooleanBuffer) -------------- */
+/* encodings/runend-bool/src/compress.rs:46-93 runend_bool_decode_slice: ends' = min(end -
+ * offset, len); run r holds value_at_index(r, start) = start ^ (r odd) for positions
+ * [ends'[r-1], ends'[r]).  Writes len bits into out_bits (zeroed first, ceil(len/8) bytes).
+ * Returns -1 if the ends are not non-decreasing or do not reach len. */
+int vxo_runend_bool_decode(int ends_ptype, const void* ends, size_t n_runs, size_t offset, int start,
+                           size_t len, uint8_t* out_bits);
+/* runend-bool/src/compress.rs:16-41 runend_bool_encode_slice over an LSB bit buffer of len bits:
+ * writes the u64 ends (room for len + 1) and *start; returns the number of ends. */
+size_t vxo_runend_bool_encode(const uint8_t* bits, size_t len, uint64_t* ends, int* start);
+/* bytebool/src/array.rs:138-146 into_canonical: one byte per bool -> bit (byte != 0). */
+void vxo_bytebool_to_bits(const uint8_t* bytes, size_t n, uint8_t* out_bits);
+
 /* ---- Sparse / Constant canonical (array/sparse/flatten.rs:68-98; constant/canonical.rs) - */
 void vxo_fill(int val_width, const void* scalar, size_t n, void* out);
 

@@ -101,6 +101,22 @@ def kats() -> list[dict]:
         name="runend_decode", ref="encodings/runend/src/compress.rs:168-178",
         kind="runend_decode", ptype="i32", ends=[2, 5, 10], run_values=[1, 2, 3], offset=0, len=10,
         expect_decoded=[1, 1, 2, 2, 2, 3, 3, 3, 3, 3]))
+    # ---- RunEndBool (encodings/runend-bool/src/{compress.rs,array.rs} tests) ----------------
+    out.append(dict(
+        name="runend_bool_encode", ref="encodings/runend-bool/src/compress.rs:107-129",
+        kind="runend_bool_encode",
+        cases=[dict(input=[True, True, False, True], expect_ends=[2, 3, 4], expect_start=True),
+               dict(input=[False] * 66 + [True, True], expect_ends=[66, 68], expect_start=False),
+               dict(input=[False, False, True, False], expect_ends=[2, 3, 4], expect_start=False)]))
+    out.append(dict(
+        name="runend_bool_decode", ref="encodings/runend-bool/src/array.rs:186-254",
+        kind="runend_bool_decode", ends_ptype="u32",
+        cases=[dict(ends=[2, 4, 5], start=False, offset=0, len=5, expect=[False, False, True, True, False]),
+               dict(ends=[2, 4, 5], start=True, offset=0, len=5, expect=[True, True, False, False, True]),
+               # slice(2, 8) of ends [2,5,6,7,10] start true (compute.rs:72-84): ends[1..5], start
+               # = value_at_index(1, true), offset 2, len 6
+               dict(ends=[5, 6, 7, 10], start=False, offset=2, len=6,
+                    expect=[False, False, False, True, False, True])]))
     # ---- Dict / take ------------------------------------------------------------------------
     out.append(dict(
         name="dict_encode_primitive", ref="encodings/dict/src/compress.rs:203-209",

@@ -37,12 +37,16 @@ def _validity(a: Array):
         if a.validity == VALIDITY["ALL_INVALID"]:
             return np.zeros(a.len, dtype=bool)
         v = a.children[idx]
+        if v.encoding != ENC["BOOL"]:  # a compressed Bool array: its canonical bits
+            return canon_bool(v)
         bits = _buf(v.buffers[0])
         off = v.meta.get("first_byte_bit_offset", 0)
         return np.unpackbits(bits, bitorder="little")[off: off + a.len].astype(bool)
 
-    if e == ENC["PRIMITIVE"]:
+    if e in (ENC["PRIMITIVE"], ENC["BOOL"], ENC["BYTE_BOOL"]):
         return from_meta(0)
+    if e == ENC["RUN_END_BOOL"]:
+        return from_meta(1)
     if e == ENC["FL_BITPACKED"]:
         return from_meta(1 if a.meta["has_patches"] else 0)
     if e in (ENC["FL_DELTA"], ENC["RUN_END"], ENC["VARBIN"]):
@@ -58,7 +62,9 @@ def _validity(a: Array):
     if e == ENC["DICT"]:
         return None
     if e == ENC["SPARSE"]:
-        if not a.meta["fill_is_null"]:
+        # primitives: validity only with a null fill; bools: always the indices
+        # (sparse/flatten.rs:41-61 vs :72-96)
+        if not a.meta["fill_is_null"] and a.dtype != DTYPE["BOOL"]:
             return None
         m = np.zeros(a.len, dtype=bool)
         idx = canon(a.children[0])[0].astype(np.int64) - a.meta["indices_offset"]
@@ -98,6 +104,8 @@ def canon(a: Array):
     e = a.encoding
     if a.dtype in (DTYPE["UTF8"], DTYPE["BINARY"]):
         return _canon_string(a), _validity(a)
+    if a.dtype == DTYPE["BOOL"]:
+        return canon_bool(a), _validity(a)
     dt = NP_OF_PTYPE[a.ptype]
     val = _validity(a)
     if e == ENC["PRIMITIVE"]:
@@ -188,6 +196,38 @@ def canon(a: Array):
         parts = [canon(c)[0] for c in a.children[1:]]
         return (np.concatenate(parts).astype(dt) if parts else np.zeros(0, dt)), val
     raise NotImplementedError(f"oracle canonicalize for encoding {e}")
+
+
+def canon_bool(a: Array) -> np.ndarray:
+    """Canonical::Bool values of a Bool-dtype tree as a bool mask."""
+    L = O.lib()
+    e, n = a.encoding, a.len
+    if e == ENC["BOOL"]:  # array/bool/mod.rs: bits from first_byte_bit_offset
+        off = a.meta.get("first_byte_bit_offset", 0)
+        return np.unpackbits(_buf(a.buffers[0]), bitorder="little")[off: off + n].astype(bool)
+    if e == ENC["BYTE_BOOL"]:  # bytebool/src/array.rs:138-146
+        out = np.zeros((n + 7) // 8 + 1, np.uint8)
+        L.vxo_bytebool_to_bits(O.p(np.ascontiguousarray(_buf(a.buffers[0])[:n])), n, O.p(out))
+        return np.unpackbits(out, bitorder="little")[:n].astype(bool)
+    if e == ENC["RUN_END_BOOL"]:  # runend-bool/src/array.rs:152-163 -> compress.rs:46-93
+        ends = np.ascontiguousarray(canon(a.children[0])[0])
+        out = np.zeros((n + 7) // 8 + 1, np.uint8)
+        rc = L.vxo_runend_bool_decode(O.PT[a.children[0].ptype], O.p(ends), ends.size, a.meta["offset"],
+                                      int(a.meta["start"]), n, O.p(out))
+        if rc:
+            raise ValueError("runend bool decode failed")
+        return np.unpackbits(out, bitorder="little")[:n].astype(bool)
+    if e == ENC["CONSTANT"]:  # constant/canonical.rs:26-33
+        return np.full(n, (not a.meta["is_null"]) and bytes(a.meta["scalar"])[0] != 0, dtype=bool)
+    if e == ENC["SPARSE"]:  # sparse/flatten.rs:41-61
+        out = np.full(n, (not a.meta["fill_is_null"]) and bytes(a.meta["fill"])[0] != 0, dtype=bool)
+        idx = canon(a.children[0])[0].astype(np.int64) - a.meta["indices_offset"]
+        out[idx] = canon_bool(a.children[1])
+        return out
+    if e == ENC["CHUNKED"]:  # chunked/canonical.rs:154-163 pack_bools
+        parts = [canon_bool(c) for c in a.children[1:]]
+        return np.concatenate(parts) if parts else np.zeros(0, bool)
+    raise NotImplementedError(f"oracle bool canonicalize for encoding {e}")
 
 
 def _canon_string(a: Array):

@@ -50,7 +50,11 @@ def test_struct_layouts_match_c(tmp_path):
               "vxg_data_buffer": (L.VxgDataBuffer, ["offset", "len"]),
               "vxg_dict_chunk": (L.VxgDictChunk, ["packed", "out", "n_blocks", "dict_len"])}
     src = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{ROOT}/include/vortex_gpu.h"', "int main(){",
-           'printf("vxg_meta %zu\\n", sizeof(vxg_meta));']
+           'printf("vxg_meta %zu\\n", sizeof(vxg_meta));',
+           'printf("runendbool.start %zu\\n", offsetof(vxg_meta, runendbool.start));',
+           'printf("runendbool.ends_ptype %zu\\n", offsetof(vxg_meta, runendbool.ends_ptype));',
+           'printf("runendbool.num_runs %zu\\n", offsetof(vxg_meta, runendbool.num_runs));',
+           'printf("runendbool.offset %zu\\n", offsetof(vxg_meta, runendbool.offset));']
     for st, (_, fs) in fields.items():
         src.append(f'printf("{st} %zu\\n", sizeof({st}));')
         for f in fs:
@@ -61,6 +65,8 @@ def test_struct_layouts_match_c(tmp_path):
     got = dict(ln.split() for ln in subprocess.run([str(tmp_path / "sz")], capture_output=True, text=True,
                                                     check=True).stdout.splitlines())
     assert int(got["vxg_meta"]) == C.sizeof(L.VxgMeta)
+    for f in ("start", "ends_ptype", "num_runs", "offset"):
+        assert int(got[f"runendbool.{f}"]) == getattr(L._MRunEndBool, f).offset, f
     for st, (cls, fs) in fields.items():
         assert int(got[st]) == C.sizeof(cls), st
         for f in fs:
@@ -70,7 +76,8 @@ def test_struct_layouts_match_c(tmp_path):
 def test_encoding_ids_match_reference():
     # vortex-array/src/encoding/mod.rs:106-147
     ref = dict(BOOL=2, PRIMITIVE=3, STRUCT=4, VARBIN=5, VARBINVIEW=6, SPARSE=8, CONSTANT=9, CHUNKED=10,
-               ALP=17, DICT=20, FL_BITPACKED=21, FL_DELTA=22, FL_FOR=23, FSST=24, RUN_END=27, ZIGZAG=29, ALP_RD=30)
+               ALP=17, BYTE_BOOL=18, DICT=20, FL_BITPACKED=21, FL_DELTA=22, FL_FOR=23, FSST=24, RUN_END=27,
+               RUN_END_BOOL=28, ZIGZAG=29, ALP_RD=30)
     assert L.ENC == ref
     hdr = (ROOT / "include" / "vortex_gpu.h").read_text()
     for k, v in ref.items():

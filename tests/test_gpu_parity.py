@@ -616,3 +616,116 @@ def test_ragged_single_element_chunks(ctx):
         chunks.append(E.encode_bitpacked(v, bit_width=9, allow_patches=False))
         expect.append(v)
     assert_primitive_parity(A.chunked(chunks), ctx, np.concatenate(expect))
+
+
+# ------------------------------------------------------------------ Bool canonical + compressed validity
+def _bool_case(ctx, arr):
+    got = A.canonicalize(arr.to(torch_dev()), ctx)
+    want, wvalid = canon(arr)
+    assert got.kind == "bool"
+    assert np.array_equal(got.numpy(), want)
+    gv = got.validity_mask()
+    if wvalid is None:
+        assert gv is None or gv.all()
+    else:
+        assert np.array_equal(gv, wvalid)
+
+
+def torch_dev():
+    import torch
+    return torch.device("cuda", 0)
+
+
+@pytest.mark.parametrize("n", [1, 31, 32, 33, 8191, 8192, 8193, 100_003, 1 << 20])
+@pytest.mark.parametrize("kind", ["random", "long", "alternating"])
+def test_runend_bool(ctx, n, kind):
+    """RunEndBool -> BoolArray (runend-bool/src/compress.rs:46-93): flips at run ends inside
+    8192-bit workgroup spans; runs shorter than, equal to and much longer than a span."""
+    rng = np.random.default_rng(n)
+    if kind == "random":
+        m = rng.integers(0, 2, n).astype(bool)
+    elif kind == "long":
+        m = np.repeat(rng.integers(0, 2, n // 5000 + 2).astype(bool), 5000)[:n]
+    else:
+        m = (np.arange(n) % 2).astype(bool)
+    for bp in (False, True):
+        _bool_case(ctx, E.encode_runend_bool(m, bitpack_ends=bp))
+
+
+def test_runend_bool_sliced_and_zero_length_runs(ctx):
+    # the reference's slice KAT (compute.rs:72-84): ends [5,6,7,10] start false offset 2 len 6
+    _bool_case(ctx, A.run_end_bool(A.primitive(np.array([5, 6, 7, 10], np.uint32)), False, length=6, offset=2))
+    # slices of a long random array at many offsets, u16/u32/u64 ends
+    rng = np.random.default_rng(9)
+    m = rng.integers(0, 2, 50_000).astype(bool)
+    ends, start = E.runend_bool_encode(m)
+    for lo, hi in [(0, 50_000), (3, 49_000), (8191, 8193 * 3), (20_000, 20_001)]:
+        b = int(np.searchsorted(ends, lo, side="right"))
+        e = int(np.searchsorted(ends, hi, side="right"))
+        st = start if b % 2 == 0 else (not start)
+        for pt in (np.uint32, np.uint64):
+            arr = A.run_end_bool(A.primitive(ends[b:e + 1].astype(pt)), st, length=hi - lo, offset=lo)
+            _bool_case(ctx, arr)
+    # zero-length runs (repeated ends) flip twice
+    _bool_case(ctx, A.run_end_bool(A.primitive(np.array([0, 3, 3, 7, 7, 7, 40], np.uint64)), True, length=40))
+
+
+def test_bool_encodings(ctx):
+    rng = np.random.default_rng(3)
+    m = rng.integers(0, 2, 70_001).astype(bool)
+    _bool_case(ctx, A.bool_array(m))
+    _bool_case(ctx, A.bool_array(m, bit_offset=3))
+    _bool_case(ctx, A.byte_bool(m.astype(np.uint8) * rng.integers(1, 255, m.size).astype(np.uint8)))
+    _bool_case(ctx, A.constant_bool(True, 1000))
+    _bool_case(ctx, A.constant_bool(False, 1000))
+    for fill in (None, True, False):
+        idx = np.sort(rng.choice(m.size, 500, replace=False)).astype(np.uint64) + 7
+        _bool_case(ctx, A.sparse_bool(A.primitive(idx), A.bool_array(rng.integers(0, 2, 500).astype(bool)),
+                                      m.size, indices_offset=7, fill=fill))
+
+
+def test_chunked_bools_ragged(ctx):
+    """pack_bools (chunked/canonical.rs:154-163) at bit offsets that are not word aligned."""
+    rng = np.random.default_rng(4)
+    chunks = []
+    for i, n in enumerate([5, 33, 1, 8192, 9000, 31, 100_000, 64, 3]):
+        m = rng.integers(0, 2, n).astype(bool)
+        k = i % 4
+        chunks.append([A.bool_array(m, bit_offset=i % 8), A.byte_bool(m), E.encode_runend_bool(m),
+                       A.constant_bool(bool(i % 2), n)][k])
+    _bool_case(ctx, A.chunked(chunks))
+
+
+def test_compressed_validity_children(ctx):
+    """A validity child may be any Bool array (validity.rs:25-110): RunEndBool, ByteBool,
+    Constant, Chunked; values and nulls both match the oracle."""
+    rng = np.random.default_rng(6)
+    n = 30_000
+    vals = rng.integers(0, 1 << 12, n).astype(np.uint32)
+    m = np.repeat(rng.integers(0, 2, n // 100 + 1).astype(bool), 100)[:n]
+    for v in (E.encode_runend_bool(m), A.byte_bool(m), A.chunked([E.encode_runend_bool(m[:777]), A.byte_bool(m[777:])])):
+        for arr in (A.primitive(vals, validity=v), E.encode_bitpacked(vals, bit_width=12, allow_patches=False, validity=v)):
+            got = A.canonicalize(arr.to(torch_dev()), ctx)
+            want, wvalid = canon(arr)
+            assert got.numpy()[:n].tobytes() == want.tobytes()
+            assert np.array_equal(got.validity_mask(), wvalid)
+    # strings with a RunEndBool validity
+    strs = [b"s%d" % i * (i % 7) for i in range(n)]
+    heap, offs, _ = E.strings_to_heap(strs)
+    sv = A.varbin(A.primitive(offs.astype(np.int32)), A.primitive(heap), validity=E.encode_runend_bool(m))
+    got = A.canonicalize(sv.to(torch_dev()), ctx)
+    (rv, rh), rvalid = canon(sv)
+    assert got.numpy()[0].tobytes() == rv.tobytes() and np.array_equal(got.validity_mask(), rvalid)
+
+
+def test_plan_with_bool_columns(ctx):
+    rng = np.random.default_rng(8)
+    m = rng.integers(0, 2, 200_000).astype(bool)
+    arrs = [E.encode_runend_bool(m), A.byte_bool(m), A.primitive(np.arange(m.size, dtype=np.uint32),
+                                                                  validity=E.encode_runend_bool(~m))]
+    plan = V.Plan([a.to(torch_dev()) for a in arrs], ctx)
+    for _ in range(2):
+        res = plan.launch(sync=True)
+        assert np.array_equal(res[0].numpy(), m) and np.array_equal(res[1].numpy(), m)
+        assert np.array_equal(res[2].validity_mask(), ~m)
+    plan.close()

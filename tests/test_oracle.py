@@ -391,3 +391,41 @@ def test_lineitem_generator_and_cascades():
             assert [view_bytes(views, bufs, i) for i in range(0, rows, 97)] == strings[::97]
         else:
             assert np.array_equal(canon(cols[name])[0], np.concatenate(plain[name]))
+
+
+# ------------------------------------------------------------------ Bool encodings (§8(f) row 2)
+def test_kat_runend_bool():
+    """RunEndBool encode/decode KATs of encodings/runend-bool/src/{compress.rs,array.rs}."""
+    for c in KATS["runend_bool_encode"]["cases"]:
+        ends, start = E.runend_bool_encode(c["input"])
+        assert ends.tolist() == c["expect_ends"] and start == c["expect_start"]
+    for c in KATS["runend_bool_decode"]["cases"]:
+        arr = A.run_end_bool(A.primitive(np.array(c["ends"], np.uint32)), c["start"], length=c["len"],
+                             offset=c["offset"])
+        assert canon(arr)[0].tolist() == c["expect"]
+
+
+@pytest.mark.parametrize("n", [0, 1, 7, 1024 * 4, 1024 * 8 - 61])
+def test_runend_bool_roundtrip(n):
+    """runend-bool compress.rs tests encode_decode_random / _offset_array: decode(encode(x)) = x."""
+    rng = np.random.default_rng(4352 + n)
+    for m in (rng.integers(0, 2, n).astype(bool), np.ones(n, bool), np.zeros(n, bool)):
+        assert np.array_equal(canon(E.encode_runend_bool(m))[0], m)
+        if n:
+            assert np.array_equal(canon(E.encode_runend_bool(m, bitpack_ends=True))[0], m)
+
+
+def test_bool_encodings_and_compressed_validity():
+    rng = np.random.default_rng(5)
+    m = rng.integers(0, 2, 300).astype(bool)
+    assert np.array_equal(canon(A.byte_bool(m.astype(np.uint8) * 7))[0], m)  # any nonzero byte is true
+    assert np.array_equal(canon(A.bool_array(m, bit_offset=5))[0], m)
+    assert canon(A.constant_bool(True, 9))[0].all() and not canon(A.constant_bool(False, 9))[0].any()
+    # sparse bools: validity = the indices, whatever the fill (sparse/flatten.rs:41-61)
+    sb = A.sparse_bool(A.primitive(np.array([2, 4], np.uint64)), A.bool_array([False, True]), 6, fill=True)
+    vals, valid = canon(sb)
+    assert vals.tolist() == [True, True, False, True, True, True]
+    assert valid.tolist() == [False, False, True, False, True, False]
+    # a RunEndBool validity child on a primitive column
+    p = A.primitive(np.arange(300, dtype=np.uint32), validity=E.encode_runend_bool(m))
+    assert np.array_equal(canon(p)[1], m)

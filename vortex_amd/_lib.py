@@ -16,13 +16,13 @@ ENC_LIB_PATH = _HERE / "libvortex_enc.so"
 
 # ---- ids mirrored from include/vortex_gpu.h (reference encoding/mod.rs:106-147) ----------
 ENC = dict(BOOL=2, PRIMITIVE=3, STRUCT=4, VARBIN=5, VARBINVIEW=6, SPARSE=8, CONSTANT=9,
-           CHUNKED=10, ALP=17, DICT=20, FL_BITPACKED=21, FL_DELTA=22, FL_FOR=23, FSST=24,
-           RUN_END=27, ZIGZAG=29, ALP_RD=30)
+           CHUNKED=10, ALP=17, BYTE_BOOL=18, DICT=20, FL_BITPACKED=21, FL_DELTA=22, FL_FOR=23,
+           FSST=24, RUN_END=27, RUN_END_BOOL=28, ZIGZAG=29, ALP_RD=30)
 PTYPES = ["u8", "u16", "u32", "u64", "i8", "i16", "i32", "i64", "f16", "f32", "f64"]
 PTYPE = {n: i for i, n in enumerate(PTYPES)}
 DTYPE = dict(NULL=0, BOOL=1, PRIMITIVE=2, UTF8=3, BINARY=4)
 VALIDITY = dict(NON_NULLABLE=0, ALL_VALID=1, ALL_INVALID=2, ARRAY=3)
-ABI_VERSION = 2  # VXG_ABI_VERSION
+ABI_VERSION = 3  # VXG_ABI_VERSION
 STATUS = {0: "OK", 1: "OutOfBounds", 2: "ComputeError", 3: "InvalidArgument", 4: "InvalidSerde",
           5: "NotImplemented", 6: "MismatchedTypes", 7: "AssertionFailed", 8: "HipError",
           9: "OutOfMemory"}
@@ -97,6 +97,11 @@ class _MBool(C.Structure):
     _fields_ = [("first_byte_bit_offset", C.c_uint8)]
 
 
+class _MRunEndBool(C.Structure):
+    _fields_ = [("start", C.c_uint8), ("ends_ptype", C.c_uint8), ("num_runs", C.c_uint64),
+                ("offset", C.c_uint64)]
+
+
 class _MVarBinView(C.Structure):
     _fields_ = [("n_buffers", C.c_uint32)]
 
@@ -105,8 +110,8 @@ class VxgMeta(C.Union):
     _fields_ = [("bitpacked", _MBitPacked), ("for_", _MFoR), ("delta", _MDelta), ("alp", _MAlp),
                 ("alprd", _MAlpRd), ("dict", _MDict), ("fsst", _MFsst), ("runend", _MRunEnd),
                 ("sparse", _MSparse), ("constant", _MConstant), ("chunked", _MChunked),
-                ("varbin", _MVarBin), ("boolean", _MBool), ("varbinview", _MVarBinView),
-                ("raw", C.c_uint64 * 5)]
+                ("varbin", _MVarBin), ("boolean", _MBool), ("runendbool", _MRunEndBool),
+                ("varbinview", _MVarBinView), ("raw", C.c_uint64 * 5)]
 
 
 class VxgArray(C.Structure):
@@ -175,6 +180,8 @@ GPU_SIGNATURES = {
     "vxg_take": (ST, [VP, UINT, VP, U64, INT, VP, U64, VP, VP]),
     "vxg_delta_decode": (ST, [VP, INT, VP, U64, VP, U64, U64, U64, VP, VP]),
     "vxg_runend_decode": (ST, [VP, UINT, VP, INT, VP, U64, U64, U64, VP, VP]),
+    "vxg_runend_bool_decode": (ST, [VP, INT, VP, U64, U64, INT, U64, VP, U64, VP]),
+    "vxg_bytebool_to_bits": (ST, [VP, VP, U64, VP, U64, VP]),
     "vxg_fsst_scratch_bytes": (U64, [U64]),
     "vxg_fsst_decode": (ST, [VP, VP, VP, UINT, VP, INT, VP, INT, VP, U64, VP, VP, VP, VP, VP]),
     "vxg_fill": (ST, [VP, UINT, VP, U64, VP, VP]),

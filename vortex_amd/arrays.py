@@ -106,6 +106,10 @@ def _validity_kind(nullable: bool, validity) -> tuple[int, Optional[Array]]:
         return (VALIDITY["ALL_VALID"] if nullable else VALIDITY["NON_NULLABLE"]), None
     if isinstance(validity, str):
         return VALIDITY[validity], None
+    if isinstance(validity, Array):  # any Bool-dtype array (RunEndBool, ByteBool, ...)
+        if validity.dtype != DTYPE["BOOL"]:
+            _bail("InvalidArgument", "validity must be a Bool array")
+        return VALIDITY["ARRAY"], validity
     return VALIDITY["ARRAY"], bool_validity(validity)
 
 
@@ -247,6 +251,62 @@ def run_end(ends: Array, values: Array, length: Optional[int] = None, offset: in
                  [ends, values] + ([vchild] if vchild is not None else []))
 
 
+def bool_array(mask, validity=None, bit_offset: int = 0) -> Array:
+    """BoolArray (array/bool/mod.rs:25-70): LSB bit buffer starting at bit `bit_offset` (< 8,
+    first_byte_bit_offset of a sliced BoolArray)."""
+    m = np.asarray(mask, dtype=bool)
+    bits = np.packbits(np.concatenate([np.zeros(bit_offset, bool), m]), bitorder="little")
+    nullable = validity is not None
+    vk, vchild = _validity_kind(nullable, validity)
+    return Array(ENC["BOOL"], len(m), DTYPE["BOOL"], "u8", nullable, vk, {"first_byte_bit_offset": bit_offset},
+                 [bits], [vchild] if vchild is not None else [])
+
+
+def byte_bool(mask, validity=None) -> Array:
+    """ByteBoolArray::try_new (encodings/bytebool/src/array.rs:36-54): one byte per bool."""
+    b = np.asarray(mask).astype(np.uint8)
+    nullable = validity is not None
+    vk, vchild = _validity_kind(nullable, validity)
+    return Array(ENC["BYTE_BOOL"], len(b), DTYPE["BOOL"], "u8", nullable, vk, {}, [b],
+                 [vchild] if vchild is not None else [])
+
+
+def run_end_bool(ends: Array, start: bool, length: Optional[int] = None, offset: int = 0, validity=None) -> Array:
+    """RunEndBoolArray::with_offset_and_size (encodings/runend-bool/src/array.rs:41-80): ends
+    strictly increasing unsigned ints (>= 1 element); length defaults to the last end."""
+    if ends.ptype[0] != "u":
+        _bail("InvalidArgument", f"Ends array must be an unsigned integer type, got {ends.ptype}")
+    if ends.len == 0:
+        _bail("InvalidArgument", "Ends array must have at least one element")
+    if length is None:
+        length = int(np.asarray(ends.buffers[0])[ends.len - 1]) if ends.encoding == ENC["PRIMITIVE"] else None
+        if length is None:
+            _bail("InvalidArgument", "length needed for compressed ends")
+    nullable = validity is not None
+    vk, vchild = _validity_kind(nullable, validity)
+    return Array(ENC["RUN_END_BOOL"], length, DTYPE["BOOL"], "u8", nullable, vk,
+                 {"start": bool(start), "ends_ptype": PTYPE[ends.ptype], "num_runs": ends.len, "offset": offset},
+                 [], [ends] + ([vchild] if vchild is not None else []))
+
+
+def constant_bool(value: Optional[bool], length: int) -> Array:
+    """ConstantArray of a Bool scalar (constant/canonical.rs:26-33); None = null."""
+    sc = bytes(16) if value is None else bytes([1 if value else 0]).ljust(16, b"\0")
+    return Array(ENC["CONSTANT"], length, DTYPE["BOOL"], "u8", value is None, VALIDITY["NON_NULLABLE"],
+                 {"is_null": value is None, "scalar": sc})
+
+
+def sparse_bool(indices: Array, values: Array, length: int, indices_offset: int = 0, fill=None) -> Array:
+    """SparseArray of bools (sparse/flatten.rs:41-61); fill None = null.  Canonicalizes with a
+    validity bitmap set exactly at the indices, whatever the fill (the reference's behaviour)."""
+    if values.dtype != DTYPE["BOOL"]:
+        _bail("MismatchedTypes", "sparse_bool values must be a Bool array")
+    fill_bytes = bytes(16) if fill is None else bytes([1 if fill else 0]).ljust(16, b"\0")
+    return Array(ENC["SPARSE"], length, DTYPE["BOOL"], "u8", True, VALIDITY["NON_NULLABLE"],
+                 {"indices_offset": indices_offset, "indices_len": indices.len,
+                  "fill_is_null": fill is None, "fill": fill_bytes}, [], [indices, values])
+
+
 def constant(value, length: int, ptype: str) -> Array:
     """ConstantArray (array/constant/mod.rs:22-60); value None = null scalar."""
     sc = bytes(16) if value is None else np.array([value], dtype=NP_OF_PTYPE[ptype]).tobytes().ljust(16, b"\0")
@@ -358,6 +418,9 @@ def _fill_meta(m: _lib.VxgMeta, a: Array) -> None:
         m.varbin.offsets_ptype, m.varbin.bytes_len = md["offsets_ptype"], md["bytes_len"]
     elif e == ENC["BOOL"]:
         m.boolean.first_byte_bit_offset = md.get("first_byte_bit_offset", 0)
+    elif e == ENC["RUN_END_BOOL"]:
+        m.runendbool.start, m.runendbool.ends_ptype = int(md["start"]), md["ends_ptype"]
+        m.runendbool.num_runs, m.runendbool.offset = md["num_runs"], md["offset"]
     elif e == ENC["VARBINVIEW"]:
         m.varbinview.n_buffers = md["n_buffers"]
 
@@ -427,20 +490,22 @@ class Context:
 
 @dataclass
 class Canonical:
-    """Canonical::Primitive or Canonical::VarBinView (canonical.rs:56-63), device tensors."""
+    """Canonical::Primitive, ::Bool or ::VarBinView (canonical.rs:56-63), device tensors."""
     kind: str
     len: int
     ptype: str
-    values: Any = None       # torch.uint8 tensor (len * width bytes) for Primitive
+    values: Any = None       # torch.uint8 tensor: len * width bytes (Primitive) / LSB bits (Bool)
     views: Any = None        # torch.uint8 tensor (16 * len) for VarBinView
     data: Any = None         # torch.uint8 tensor holding every data buffer of the view array
     validity: Any = None     # torch.uint8 LSB bitmap or None (no nulls)
     data_buffers: Any = None  # [(offset, len)] of each data buffer inside `data`
 
     def numpy(self):
-        """Host copy: values as the ptype's numpy dtype, or (views u8[n,16], data u8[])."""
+        """Host copy: values as the ptype's numpy dtype, a bool mask, or (views u8[n,16], data u8[])."""
         if self.kind == "primitive":
             return self.values.cpu().numpy().view(NP_OF_PTYPE[self.ptype])
+        if self.kind == "bool":
+            return np.unpackbits(self.values.cpu().numpy(), bitorder="little")[: self.len].astype(bool)
         return self.views.cpu().numpy().reshape(-1, 16), self.data.cpu().numpy()
 
     def buffers(self):
@@ -453,6 +518,10 @@ class Canonical:
             return None
         bits = self.validity.cpu().numpy()
         return np.unpackbits(bits, bitorder="little")[: self.len].astype(bool)
+
+
+def _kind(a: Array) -> str:
+    return {DTYPE["PRIMITIVE"]: "primitive", DTYPE["BOOL"]: "bool"}.get(a.dtype, "varbinview")
 
 
 def canonicalize(a: Array, ctx: Context, out_values=None, sync: bool = True) -> Canonical:
@@ -474,10 +543,10 @@ def canonicalize(a: Array, ctx: Context, out_values=None, sync: bool = True) -> 
         _lib.check(st)
         break
     out = _lib.VxgCanonical()
-    res = Canonical("primitive" if a.dtype == DTYPE["PRIMITIVE"] else "varbinview", a.len, a.ptype)
+    res = Canonical(_kind(a), a.len, a.ptype)
     nbits = ((a.len + 31) // 32) * 4
     valid_t = torch.empty(max(nbits, 4), dtype=torch.uint8, device=dev) if a.nullable else None
-    if a.dtype == DTYPE["PRIMITIVE"]:
+    if a.dtype in (DTYPE["PRIMITIVE"], DTYPE["BOOL"]):
         vals = out_values if out_values is not None else torch.empty(max(vb.value, 16), dtype=torch.uint8, device=dev)
         out.values = vals.data_ptr()
         res.values = vals[: vb.value]
@@ -522,9 +591,9 @@ class Plan:
             table = (_lib.VxgDataBuffer * 4096)()
             _lib.check(ctx.lib.vxg_canonical_layout(ctx.handle, C.byref(self.nodes[i]), C.byref(vb), C.byref(db),
                                                     table, 4096, C.byref(nb)))
-            res = Canonical("primitive" if a.dtype == DTYPE["PRIMITIVE"] else "varbinview", a.len, a.ptype)
+            res = Canonical(_kind(a), a.len, a.ptype)
             o = self.outs[i]
-            if a.dtype == DTYPE["PRIMITIVE"]:
+            if a.dtype in (DTYPE["PRIMITIVE"], DTYPE["BOOL"]):
                 vals = torch.empty(max(vb.value, 16), dtype=torch.uint8, device=dev)
                 o.values = vals.data_ptr()
                 res.values = vals[: vb.value]

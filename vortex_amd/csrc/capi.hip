@@ -289,6 +289,8 @@ class Planner {
     vxg_status decode_sparse_values(const vxg_array& a, void* dst);
 
     vxg_status validity_into(const vxg_array& a, void** bitmap);
+    // OR the values of a Bool-dtype array into the zeroed bit buffer `bits` at bit `off`.
+    vxg_status bools_into(const vxg_array& a, void* bits, uint64_t off);
     vxg_status validity_source(const vxg_array& a, const vxg_array** node, int* kind);
     vxg_status string_canonical(const vxg_array& a, vxg_canonical& out);
     vxg_status string_lens(const vxg_array& a, std::vector<uint64_t>& lens,
@@ -736,16 +738,19 @@ vxg_status Planner::validity_source(const vxg_array& a, const vxg_array** node, 
         case VXG_VALIDITY_ALL_INVALID: *kind = 1; return VXG_OK;
         default: {
             const vxg_array* v = child(a, child_idx);
-            if (!v || v->encoding != VXG_ENC_BOOL)
-                return set_error(VXG_ERR_NOT_IMPLEMENTED, "validity child must be a canonical BoolArray");
+            if (!v || v->dtype != VXG_DTYPE_BOOL)
+                return set_error(VXG_ERR_INVALID_ARGUMENT, "validity child must be a Bool array");
             *node = v;
-            *kind = 2;
+            *kind = v->encoding == VXG_ENC_BOOL ? 2 : 5;  // 5: compressed bools, decoded
             return VXG_OK;
         }
         }
     };
     switch (a.encoding) {
-    case VXG_ENC_PRIMITIVE: return from_meta(0);
+    case VXG_ENC_PRIMITIVE:
+    case VXG_ENC_BOOL:
+    case VXG_ENC_BYTE_BOOL: return from_meta(0);
+    case VXG_ENC_RUN_END_BOOL: return from_meta(1);
     case VXG_ENC_FL_BITPACKED: return from_meta(a.meta.bitpacked.has_patches ? 1 : 0);
     case VXG_ENC_FL_DELTA: return from_meta(2);
     case VXG_ENC_RUN_END: return from_meta(2);
@@ -765,7 +770,10 @@ vxg_status Planner::validity_source(const vxg_array& a, const vxg_array** node, 
         return VXG_OK;
     }
     case VXG_ENC_SPARSE:
-        if (a.meta.sparse.fill_is_null) { *kind = 3; *node = &a; }
+        // primitives: valid exactly at the indices when the fill is null; bools: always
+        // (canonicalize_sparse_bools builds its validity from the indices alone,
+        // sparse/flatten.rs:41-61)
+        if (a.meta.sparse.fill_is_null || a.dtype == VXG_DTYPE_BOOL) { *kind = 3; *node = &a; }
         return VXG_OK;
     case VXG_ENC_CHUNKED: {
         for (uint32_t i = 1; i < a.n_children; i++) {
@@ -798,6 +806,7 @@ vxg_status Planner::validity_into(const vxg_array& a, void** bitmap) {
         return launch_copy_bits(*bitmap, 0, static_cast<const uint8_t*>(b->ptr),
                                 node->meta.boolean.first_byte_bit_offset, a.len, false, s_);
     }
+    if (kind == 5) return bools_into(*node, *bitmap, 0);
     if (kind == 3) {  // Sparse with null fill: valid exactly at the indices (flatten.rs:82-93)
         const vxg_array* idx = child(a, 0);
         const void* pi;
@@ -817,6 +826,8 @@ vxg_status Planner::validity_into(const vxg_array& a, void** bitmap) {
         } else if (k2 == 2) {
             VXG_TRY(launch_copy_bits(*bitmap, off, static_cast<const uint8_t*>(n2->buffers[0].ptr),
                                      n2->meta.boolean.first_byte_bit_offset, c.len, false, s_));
+        } else if (k2 == 5) {
+            VXG_TRY(bools_into(*n2, *bitmap, off));
         } else if (k2 != 1) {
             void* sub = nullptr;
             VXG_TRY(temp(((c.len + 31) / 32) * 4, &sub));
@@ -826,6 +837,68 @@ vxg_status Planner::validity_into(const vxg_array& a, void** bitmap) {
         off += c.len;
     }
     return VXG_OK;
+}
+
+// ---- bools: canonical BoolArray = LSB bit buffer (bool/mod.rs), from every Bool encoding ----
+vxg_status Planner::bools_into(const vxg_array& a, void* bits, uint64_t off) {
+    if (a.dtype != VXG_DTYPE_BOOL) return set_error(VXG_ERR_MISMATCHED_TYPES, "expected a Bool array");
+    if (a.len == 0) return VXG_OK;
+    switch (a.encoding) {
+    case VXG_ENC_BOOL: {  // bool/mod.rs:25-28: bits from first_byte_bit_offset
+        const vxg_buffer* b = buf(a, 0);
+        const uint64_t fbo = a.meta.boolean.first_byte_bit_offset;
+        if (!b || b->len * 8 < fbo + a.len) return set_error(VXG_ERR_INVALID_ARGUMENT, "BoolArray buffer too short");
+        return launch_copy_bits(bits, off, static_cast<const uint8_t*>(b->ptr), fbo, a.len, false, s_);
+    }
+    case VXG_ENC_BYTE_BOOL: {  // bytebool/src/array.rs:138-146
+        const vxg_buffer* b = buf(a, 0);
+        if (!b || b->len < a.len) return set_error(VXG_ERR_INVALID_ARGUMENT, "ByteBoolArray buffer too short");
+        return launch_bytebool(static_cast<const uint8_t*>(b->ptr), a.len, bits, off, s_);
+    }
+    case VXG_ENC_RUN_END_BOOL: {  // runend-bool/src/array.rs:152-163 -> compress.rs:46-93
+        const vxg_array* e = child(a, 0);
+        if (!e || e->len == 0) return set_error(VXG_ERR_INVALID_ARGUMENT, "Ends array must have at least one element");
+        if (!ptype_is_unsigned(e->ptype))
+            return set_error(VXG_ERR_INVALID_ARGUMENT, "Ends array must be an unsigned integer type");
+        const void* pe;
+        VXG_TRY(view_primitive(*e, &pe));
+        return launch_runend_bool(pe, width(*e), e->len, a.meta.runendbool.offset, a.meta.runendbool.start != 0,
+                                  a.len, bits, off, ctx_->c.err_word, s_);
+    }
+    case VXG_ENC_CONSTANT:  // constant/canonical.rs:26-33: new_set / new_unset
+        if (!a.meta.constant.is_null && a.meta.constant.scalar[0])
+            return launch_copy_bits(bits, off, nullptr, 0, a.len, true, s_);
+        return VXG_OK;
+    case VXG_ENC_SPARSE: {  // sparse/flatten.rs:41-61 canonicalize_sparse_bools
+        const vxg_array* idx = child(a, 0);
+        const vxg_array* val = child(a, 1);
+        if (!idx || !val || idx->len != val->len)
+            return set_error(VXG_ERR_INVALID_ARGUMENT, "Sparse needs indices and values of equal length");
+        if (!a.meta.sparse.fill_is_null && a.meta.sparse.fill[0])
+            VXG_TRY(launch_copy_bits(bits, off, nullptr, 0, a.len, true, s_));
+        if (idx->len == 0) return VXG_OK;
+        void* vb;
+        const uint64_t vbytes = ((val->len + 31) / 32) * 4;
+        VXG_TRY(temp(vbytes, &vb));
+        VXG_TRY(hip_check(hipMemsetAsync(vb, 0, vbytes, s_), "sparse bools memset"));
+        VXG_TRY(bools_into(*val, vb, 0));
+        const void* pi;
+        VXG_TRY(view_primitive(*idx, &pi));
+        return launch_assign_bits_at(bits, off, pi, width(*idx), ptype_is_signed(idx->ptype),
+                                     a.meta.sparse.indices_offset, idx->len, a.len, static_cast<const uint8_t*>(vb), s_);
+    }
+    case VXG_ENC_CHUNKED: {  // chunked/canonical.rs:154-163 pack_bools
+        uint64_t o = 0;
+        for (uint32_t i = 1; i < a.n_children; i++) {
+            VXG_TRY(bools_into(a.children[i], bits, off + o));
+            o += a.children[i].len;
+        }
+        if (o != a.len) return set_error(VXG_ERR_INVALID_ARGUMENT, "Chunked len != sum of chunk lens");
+        return VXG_OK;
+    }
+    default:
+        return set_error(VXG_ERR_NOT_IMPLEMENTED, "bool canonicalize for encoding id " + std::to_string(a.encoding));
+    }
 }
 
 // ---- strings: VarBin, VarBinView, FSST, Dict(strings), Chunked (pack_views) -------------
@@ -1159,6 +1232,10 @@ vxg_status Planner::canonical_size(const vxg_array& a, uint64_t& vb, uint64_t& d
         vb = a.len * width(a);
         return VXG_OK;
     }
+    if (a.dtype == VXG_DTYPE_BOOL) {  // whole 32-bit words
+        vb = ((a.len + 31) / 32) * 4;
+        return VXG_OK;
+    }
     if (a.dtype != VXG_DTYPE_UTF8 && a.dtype != VXG_DTYPE_BINARY)
         return set_error(VXG_ERR_NOT_IMPLEMENTED, "canonical size for this dtype");
     vb = a.len * 16;
@@ -1171,8 +1248,18 @@ vxg_status Planner::canonical(const vxg_array& a, vxg_canonical& out) {
     out.dtype = a.dtype;
     out.ptype = a.ptype;
     if (a.dtype == VXG_DTYPE_UTF8 || a.dtype == VXG_DTYPE_BINARY) return string_canonical(a, out);
+    if (a.dtype == VXG_DTYPE_BOOL) {  // Canonical::Bool: LSB bit buffer + validity
+        out.kind = VXG_ENC_BOOL;
+        out.values_bytes = ((a.len + 31) / 32) * 4;
+        if (!out.values)
+            VXG_TRY(hip_check(hipMalloc(&out.values, out.values_bytes ? out.values_bytes : 4), "bool values alloc"));
+        if (out.values_bytes)
+            VXG_TRY(hip_check(hipMemsetAsync(out.values, 0, out.values_bytes, s_), "bool values memset"));
+        VXG_TRY(bools_into(a, out.values, 0));
+        return validity_into(a, &out.validity);
+    }
     if (a.dtype != VXG_DTYPE_PRIMITIVE)
-        return set_error(VXG_ERR_NOT_IMPLEMENTED, "canonicalize supports primitive and utf8/binary dtypes");
+        return set_error(VXG_ERR_NOT_IMPLEMENTED, "canonicalize supports primitive, bool and utf8/binary dtypes");
     out.kind = VXG_ENC_PRIMITIVE;
     out.values_bytes = a.len * width(a);
     if (!out.values)
@@ -1542,6 +1629,23 @@ vxg_status vxg_runend_decode(vxg_ctx* ctx, unsigned value_width, const void* val
     if (!ptype_is_int(ends_ptype)) return set_error(VXG_ERR_MISMATCHED_TYPES, "RunEnd ends must be integers");
     return launch_runend(int(value_width), values, ptype_width(ends_ptype), ends, n_runs, offset, len, out,
                          ctx->c.err_word, S(stream));
+}
+
+vxg_status vxg_runend_bool_decode(vxg_ctx* ctx, int ends_ptype, const void* ends, uint64_t n_runs, uint64_t offset,
+                                  int start, uint64_t len, void* out_bits, uint64_t out_bit_offset, void* stream) {
+    VXG_TRY(use_device(ctx));
+    if (!ptype_is_unsigned(ends_ptype))
+        return set_error(VXG_ERR_INVALID_ARGUMENT, "Ends array must be an unsigned integer type");
+    if (len && !out_bits) return set_error(VXG_ERR_INVALID_ARGUMENT, "null output");
+    return launch_runend_bool(ends, ptype_width(ends_ptype), n_runs, offset, start != 0, len, out_bits,
+                              out_bit_offset, ctx->c.err_word, S(stream));
+}
+
+vxg_status vxg_bytebool_to_bits(vxg_ctx* ctx, const uint8_t* bytes, uint64_t n, void* out_bits,
+                                uint64_t out_bit_offset, void* stream) {
+    VXG_TRY(use_device(ctx));
+    if (n && (!bytes || !out_bits)) return set_error(VXG_ERR_INVALID_ARGUMENT, "null input/output");
+    return launch_bytebool(bytes, n, out_bits, out_bit_offset, S(stream));
 }
 
 uint64_t vxg_fsst_scratch_bytes(uint64_t n) { return fsst_scratch_bytes(n); }

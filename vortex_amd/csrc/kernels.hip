@@ -780,4 +780,148 @@ vxg_status launch_views_rebase(const uint8_t* src, uint64_t n, uint32_t add, uin
     return hip_check(hipGetLastError(), "views_rebase_kernel");
 }
 
+// ---- Bool canonical: LSB bit buffers (arrow BooleanBuffer) ------------------------------
+// Every bool producer ORs 32-bit words into a zeroed bit buffer at an arbitrary bit position
+// (a chunk of a ChunkedArray starts anywhere); a full word at a 32-aligned position is owned
+// by its producer and stored plainly, ragged ones are split over two words with atomics.
+__device__ __forceinline__ void put_bits(uint32_t* __restrict__ dst, uint64_t pos, uint32_t word, bool full) {
+    const uint64_t w = pos >> 5;
+    const int sh = int(pos & 31);
+    if (full && sh == 0) {
+        dst[w] = word;
+        return;
+    }
+    if (!word) return;
+    atomicOr(dst + w, word << sh);
+    if (sh) {
+        const uint32_t hi = word >> (32 - sh);
+        if (hi) atomicOr(dst + w + 1, hi);
+    }
+}
+
+// RunEndBool (runend-bool/src/compress.rs:46-93): the value flips at every trimmed run end, so
+// a workgroup of 8192 bits finds the run holding its first bit (one wave, 64-ary search), XORs
+// a flip bit at every run end inside its span into LDS (zero-length runs flip twice = not at
+// all, like the reference's empty appends), and turns flips into values with an in-word
+// prefix XOR plus a block XOR-scan of word parities.  Writes are whole words.
+constexpr int kBoolSpan = 32 * kBlock;
+__global__ __launch_bounds__(kBlock) void runend_bool_kernel(const void* __restrict__ ends, int ew, uint64_t n_runs,
+                                                             uint64_t offset, int start, uint64_t len,
+                                                             uint32_t* __restrict__ dst, uint64_t dst_off,
+                                                             uint32_t* __restrict__ err) {
+    __shared__ uint32_t s_flip[kBlock];
+    __shared__ uint32_t s_wpar[kBlock / 64];
+    __shared__ uint64_t s_r0;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const uint64_t j0 = uint64_t(blockIdx.x) * kBoolSpan;
+    const uint64_t jend = len - j0 < uint64_t(kBoolSpan) ? len : j0 + kBoolSpan;
+    s_flip[tid] = 0;
+    if (tid < 64) {
+        const uint64_t r0 = runend_first_gt(ends, ew, offset, n_runs, j0);
+        if (tid == 0) s_r0 = r0;
+        // the trimmed ends must reach len (the reference appends exactly len bits)
+        if (blockIdx.x == 0 && tid == 0 && load_uint(ends, ew, false, n_runs - 1) - offset < len)
+            __hip_atomic_fetch_or(err, kErrRunEnd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    const uint64_t r0 = s_r0;
+    if (r0 >= n_runs) {  // bits past the last run end (flagged above)
+        return;
+    }
+    for (uint64_t r = r0 + tid; r < n_runs; r += kBlock) {
+        const uint64_t e = load_uint(ends, ew, false, r) - offset;
+        if (e >= jend) break;  // ends increase: so do all later ones
+        const uint32_t p = uint32_t(e - j0);  // > 0: ends[r] - offset > j0 for r >= r0
+        atomicXor(&s_flip[p >> 5], 1u << (p & 31));
+    }
+    __syncthreads();
+    const uint32_t f = s_flip[tid];
+    uint32_t x = f;  // inclusive prefix XOR inside the word
+    x ^= x << 1;
+    x ^= x << 2;
+    x ^= x << 4;
+    x ^= x << 8;
+    x ^= x << 16;
+    const unsigned long long bal = __ballot(__popc(f) & 1);
+    const uint32_t below = uint32_t(__popcll(bal & ((1ull << lane) - 1ull)) & 1);
+    if (lane == 0) s_wpar[wave] = uint32_t(__popcll(bal) & 1);
+    __syncthreads();
+    uint32_t carry = below ^ uint32_t(start != 0) ^ uint32_t(r0 & 1);  // value_at_index(r0, start)
+    for (int w = 0; w < wave; w++) carry ^= s_wpar[w];
+    uint32_t word = x ^ (carry ? 0xFFFFFFFFu : 0u);
+    const uint64_t p0 = j0 + uint64_t(tid) * 32;
+    if (p0 >= jend) return;
+    const uint64_t nb = jend - p0;
+    if (nb < 32) word &= (1u << nb) - 1u;
+    put_bits(dst, dst_off + p0, word, nb >= 32);
+}
+
+vxg_status launch_runend_bool(const void* ends, int ew, uint64_t n_runs, uint64_t offset, bool start, uint64_t len,
+                              void* dst, uint64_t dst_off, uint32_t* err, hipStream_t s) {
+    if (len == 0) return VXG_OK;
+    if (n_runs == 0) return set_error(VXG_ERR_INVALID_ARGUMENT, "Ends array must have at least one element");
+    const uint64_t groups = (len + kBoolSpan - 1) / kBoolSpan;
+    if (groups > 0xFFFFFFFFull) return set_error(VXG_ERR_INVALID_ARGUMENT, "RunEndBool too long");
+    hipLaunchKernelGGL(runend_bool_kernel, dim3(unsigned(groups)), dim3(kBlock), 0, s, ends, ew, n_runs, offset,
+                       int(start), len, static_cast<uint32_t*>(dst), dst_off, err);
+    return hip_check(hipGetLastError(), "runend_bool_kernel");
+}
+
+// ByteBool (bytebool/src/array.rs:138-146): 32 bytes -> one word per thread (byte != 0).
+__device__ __forceinline__ uint32_t nonzero_nibble(uint32_t v) {
+    const uint32_t m = (((v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | v) & 0x80808080u;  // bit 7 of each byte != 0
+    const uint32_t b = m >> 7;                                                  // bits 0, 8, 16, 24
+    return (b | (b >> 7) | (b >> 14) | (b >> 21)) & 0xFu;
+}
+
+__global__ __launch_bounds__(kBlock) void bytebool_kernel(const uint8_t* __restrict__ src, uint64_t n,
+                                                          uint32_t* __restrict__ dst, uint64_t dst_off) {
+    const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+    for (uint64_t w = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; w * 32 < n; w += stride) {
+        const uint64_t p0 = w * 32;
+        uint32_t word = 0;
+        if (p0 + 32 <= n && (reinterpret_cast<uintptr_t>(src + p0) & 15) == 0) {
+            const uint4 a = reinterpret_cast<const uint4*>(src + p0)[0];
+            const uint4 b = reinterpret_cast<const uint4*>(src + p0)[1];
+            const uint32_t q[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+            for (int k = 0; k < 8; k++) word |= nonzero_nibble(q[k]) << (4 * k);
+        } else {
+            for (int k = 0; k < 32 && p0 + k < n; k++) word |= uint32_t(src[p0 + k] != 0) << k;
+        }
+        put_bits(dst, dst_off + p0, word, p0 + 32 <= n);
+    }
+}
+
+vxg_status launch_bytebool(const uint8_t* src, uint64_t n, void* dst, uint64_t dst_off, hipStream_t s) {
+    if (n == 0) return VXG_OK;
+    hipLaunchKernelGGL(bytebool_kernel, dim3(grid_for((n + 31) / 32)), dim3(kBlock), 0, s, src, n,
+                       static_cast<uint32_t*>(dst), dst_off);
+    return hip_check(hipGetLastError(), "bytebool_kernel");
+}
+
+// Sparse bools (sparse/flatten.rs:41-61): bit (dst_off + idx - ioff) = values bit i.
+__global__ __launch_bounds__(kBlock) void assign_bits_at_kernel(uint32_t* __restrict__ dst, uint64_t dst_off,
+                                                                const void* idx, int iw, int isg, uint64_t ioff,
+                                                                uint64_t n, uint64_t len,
+                                                                const uint8_t* __restrict__ vals) {
+    const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t p = load_uint(idx, iw, isg != 0, i) - ioff;
+        if (p >= len) continue;
+        const uint64_t q = dst_off + p;
+        const uint32_t bit = 1u << (q & 31);
+        if ((vals[i >> 3] >> (i & 7)) & 1) atomicOr(dst + (q >> 5), bit);
+        else atomicAnd(dst + (q >> 5), ~bit);
+    }
+}
+
+vxg_status launch_assign_bits_at(void* dst, uint64_t dst_off, const void* idx, int iw, bool isg, uint64_t ioff,
+                                 uint64_t n, uint64_t len, const uint8_t* vals, hipStream_t s) {
+    if (n == 0) return VXG_OK;
+    hipLaunchKernelGGL(assign_bits_at_kernel, dim3(grid_for(n)), dim3(kBlock), 0, s, static_cast<uint32_t*>(dst),
+                       dst_off, idx, iw, int(isg), ioff, n, len, vals);
+    return hip_check(hipGetLastError(), "assign_bits_at_kernel");
+}
+
 }  // namespace vxg

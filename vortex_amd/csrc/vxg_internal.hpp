@@ -191,6 +191,12 @@ vxg_status launch_alprd(int float_ptype, const uint16_t* left, const uint16_t* d
                         uint64_t n_exc, void* out, uint32_t* err, hipStream_t s);
 vxg_status launch_copy_bits(void* dst, uint64_t dst_off, const uint8_t* src, uint64_t src_off, uint64_t n,
                             bool set_all, hipStream_t s);
+// Bool producers OR words into a zeroed LSB bit buffer at bit dst_off.
+vxg_status launch_runend_bool(const void* ends, int ew, uint64_t n_runs, uint64_t offset, bool start, uint64_t len,
+                              void* dst, uint64_t dst_off, uint32_t* err, hipStream_t s);
+vxg_status launch_bytebool(const uint8_t* src, uint64_t n, void* dst, uint64_t dst_off, hipStream_t s);
+vxg_status launch_assign_bits_at(void* dst, uint64_t dst_off, const void* idx, int iw, bool isg, uint64_t ioff,
+                                 uint64_t n, uint64_t len, const uint8_t* vals, hipStream_t s);
 vxg_status launch_set_bits_at(void* dst, const void* idx, int iw, bool isg, uint64_t off, uint64_t n,
                               uint64_t len, hipStream_t s);
 vxg_status launch_sum(const void* p, int w, bool sg, uint64_t n, void* out_u64, hipStream_t s);

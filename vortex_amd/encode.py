@@ -220,6 +220,25 @@ def encode_runend(values, bitpack_ends: bool = True, compress_values: bool = Fal
     return A.run_end(e, vals, length=v.size)
 
 
+def runend_bool_encode(mask) -> tuple[np.ndarray, bool]:
+    """runend_bool_encode_slice (encodings/runend-bool/src/compress.rs:16-41): the ends of the
+    alternating runs (u64) and the value of the first run.  No set bit: ([len], false)."""
+    m = np.asarray(mask, dtype=bool)
+    n = m.size
+    if not m.any():
+        return np.array([n], dtype=np.uint64), False
+    flips = np.flatnonzero(m[1:] != m[:-1]) + 1  # where the value changes = run ends
+    return np.concatenate([flips, [n]]).astype(np.uint64), bool(m[0])
+
+
+def encode_runend_bool(mask, bitpack_ends: bool = False, validity=None) -> Array:
+    """RunEndBoolArray::try_new (runend-bool/src/array.rs:36-39) over runend_bool_encode; the
+    ends optionally BitPacked (a compressor cascade on the ends child)."""
+    ends, start = runend_bool_encode(mask)
+    e = encode_bitpacked(ends, allow_patches=False) if bitpack_ends else A.primitive(ends)
+    return A.run_end_bool(e, start, length=int(np.asarray(mask).size), validity=validity)
+
+
 def encode_dict_strings(strings: Sequence[bytes], utf8: bool = True) -> Array:
     """dict_encode_varbin (dict/compress.rs:88-143): values = VarBin of the distinct strings in
     first-appearance order (i32 offsets), codes u64 -> BitPacked (compressors/dict.rs)."""
