@@ -60,7 +60,11 @@ def _validity(a: Array):
     if e == ENC["CONSTANT"]:
         return np.zeros(a.len, dtype=bool) if a.meta["is_null"] else None
     if e == ENC["DICT"]:
-        return None
+        # take(values, codes): values.validity().take(codes) (primitive/compute/take.rs:58-67)
+        vv = _validity(a.children[0])
+        if vv is None:
+            return None
+        return vv[canon(a.children[1])[0].astype(np.int64)]
     if e == ENC["SPARSE"]:
         # primitives: validity only with a null fill; bools: always the indices
         # (sparse/flatten.rs:41-61 vs :72-96)

@@ -729,3 +729,35 @@ def test_plan_with_bool_columns(ctx):
         assert np.array_equal(res[0].numpy(), m) and np.array_equal(res[1].numpy(), m)
         assert np.array_equal(res[2].validity_mask(), ~m)
     plan.close()
+
+
+def test_dict_nullable_values(ctx):
+    """Dict over nullable values: canonical = take(values, codes) with the values' validity
+    taken by the codes (dict/array.rs:68-73, primitive/compute/take.rs:58-67)."""
+    rng = np.random.default_rng(12)
+    n, d = 50_000, 300
+    dv = rng.integers(0, 1 << 30, d).astype(np.uint32)
+    dmask = rng.random(d) > 0.2
+    codes = rng.integers(0, d, n).astype(np.uint64)
+    for values in (A.primitive(dv, validity=dmask), A.primitive(dv, validity=E.encode_runend_bool(dmask))):
+        for c in (A.primitive(codes), E.encode_bitpacked(codes, allow_patches=False)):
+            arr = A.dict_array(values, c)
+            got = A.canonicalize(arr.to(torch_dev()), ctx)
+            want, wvalid = canon(arr)
+            assert got.numpy().tobytes() == want.tobytes()
+            assert np.array_equal(got.validity_mask(), wvalid)
+    # strings: Dict(VarBin with nulls)
+    strs = [None if i % 5 == 0 else b"value-%d" % i * (1 + i % 3) for i in range(d)]
+    heap, offs, valid = E.strings_to_heap(strs)
+    sv = A.varbin(A.primitive(offs.astype(np.int32)), A.primitive(heap), validity=valid)
+    arr = A.dict_array(sv, E.encode_bitpacked(codes, allow_patches=False))
+    got = A.canonicalize(arr.to(torch_dev()), ctx)
+    (rv, rh), rvalid = canon(arr)
+    assert got.numpy()[0].tobytes() == rv.tobytes()
+    assert np.array_equal(got.validity_mask(), rvalid)
+    # chunked dicts with nullable values
+    ch = A.chunked([A.dict_array(A.primitive(dv, validity=dmask), A.primitive(codes[:1234])),
+                    A.dict_array(A.primitive(dv), A.primitive(codes[1234:]))])
+    got = A.canonicalize(ch.to(torch_dev()), ctx)
+    want, wvalid = canon(ch)
+    assert got.numpy().tobytes() == want.tobytes() and np.array_equal(got.validity_mask(), wvalid)

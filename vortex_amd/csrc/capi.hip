@@ -765,8 +765,13 @@ vxg_status Planner::validity_source(const vxg_array& a, const vxg_array** node, 
     case VXG_ENC_DICT: {
         const vxg_array* v = child(a, 0);
         if (!v) return VXG_OK;
+        // take(values, codes) carries values.validity().take(codes) (primitive/compute/take.rs:
+        // 58-67, varbinview/compute.rs:68-76): gathered from the values' bitmap by code
         VXG_TRY(validity_source(*v, node, kind));
-        if (*kind != 0) return set_error(VXG_ERR_NOT_IMPLEMENTED, "nullable dictionary values");
+        if (*kind != 0) {
+            *kind = 6;
+            *node = &a;
+        }
         return VXG_OK;
     }
     case VXG_ENC_SPARSE:
@@ -807,6 +812,19 @@ vxg_status Planner::validity_into(const vxg_array& a, void** bitmap) {
                                 node->meta.boolean.first_byte_bit_offset, a.len, false, s_);
     }
     if (kind == 5) return bools_into(*node, *bitmap, 0);
+    if (kind == 6) {  // Dict with nullable values: bit i = values_valid[codes[i]]
+        const vxg_array* vals = child(a, 0);
+        const vxg_array* codes = child(a, 1);
+        if (!vals || !codes) return set_error(VXG_ERR_INVALID_ARGUMENT, "DictArray needs values and codes");
+        if (!ptype_is_int(codes->ptype)) return set_error(VXG_ERR_MISMATCHED_TYPES, "Dict codes must be integers");
+        void* vbits = nullptr;
+        VXG_TRY(temp(((vals->len + 31) / 32) * 4, &vbits));
+        VXG_TRY(validity_into(*vals, &vbits));
+        const void* pc;
+        VXG_TRY(view_primitive(*codes, &pc));
+        return launch_gather_bits(*bitmap, pc, width(*codes), a.len, static_cast<const uint8_t*>(vbits), vals->len,
+                                  ctx_->c.err_word, s_);
+    }
     if (kind == 3) {  // Sparse with null fill: valid exactly at the indices (flatten.rs:82-93)
         const vxg_array* idx = child(a, 0);
         const void* pi;
@@ -1064,10 +1082,15 @@ vxg_status Planner::strings_into(const vxg_array& a, uint8_t* views, uint8_t* da
         const vxg_array* vn;
         int vk;
         VXG_TRY(validity_source(*values, &vn, &vk));
-        if (vk != 0) return set_error(VXG_ERR_NOT_IMPLEMENTED, "nullable dictionary values");
+        void* vbits = nullptr;  // nullable values: their null rows get zero views before the take
+        if (vk != 0) {
+            VXG_TRY(temp(((values->len + 31) / 32) * 4, &vbits));
+            VXG_TRY(validity_into(*values, &vbits));
+        }
         void* vviews;
         VXG_TRY(temp(16 * values->len, &vviews));
-        VXG_TRY(strings_into(*values, static_cast<uint8_t*>(vviews), data, bufs, bidx, nullptr));
+        VXG_TRY(strings_into(*values, static_cast<uint8_t*>(vviews), data, bufs, bidx,
+                             static_cast<const uint8_t*>(vbits)));
         if (codes->encoding == VXG_ENC_FL_BITPACKED && codes->meta.bitpacked.bit_width <= kDictFusedMaxW) {
             UnpackArgs ua{};
             ua.dict = vviews;

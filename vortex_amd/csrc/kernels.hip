@@ -924,4 +924,33 @@ vxg_status launch_assign_bits_at(void* dst, uint64_t dst_off, const void* idx, i
     return hip_check(hipGetLastError(), "assign_bits_at_kernel");
 }
 
+// Validity of take(values, codes) (primitive/compute/take.rs:58-67 -> Validity::take): bit i =
+// values_valid[codes[i]], 32 rows per thread, whole words into a zeroed bitmap at bit 0.
+__global__ __launch_bounds__(kBlock) void gather_bits_kernel(uint32_t* __restrict__ dst, const void* codes, int cw,
+                                                             uint64_t n, const uint8_t* __restrict__ src,
+                                                             uint64_t n_values, uint32_t* __restrict__ err) {
+    const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+    for (uint64_t w = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; w * 32 < n; w += stride) {
+        uint32_t word = 0;
+        bool oob = false;
+        for (int k = 0; k < 32; k++) {
+            const uint64_t i = w * 32 + k;
+            if (i >= n) break;
+            const uint64_t c = load_uint(codes, cw, false, i);
+            oob |= c >= n_values;
+            word |= (c < n_values ? uint32_t((src[c >> 3] >> (c & 7)) & 1) : 0u) << k;
+        }
+        if (oob) __hip_atomic_fetch_or(err, kErrTakeOOB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        dst[w] = word;
+    }
+}
+
+vxg_status launch_gather_bits(void* dst, const void* codes, int cw, uint64_t n, const uint8_t* src, uint64_t n_values,
+                              uint32_t* err, hipStream_t s) {
+    if (n == 0) return VXG_OK;
+    hipLaunchKernelGGL(gather_bits_kernel, dim3(grid_for((n + 31) / 32)), dim3(kBlock), 0, s,
+                       static_cast<uint32_t*>(dst), codes, cw, n, src, n_values, err);
+    return hip_check(hipGetLastError(), "gather_bits_kernel");
+}
+
 }  // namespace vxg

@@ -197,6 +197,8 @@ vxg_status launch_runend_bool(const void* ends, int ew, uint64_t n_runs, uint64_
 vxg_status launch_bytebool(const uint8_t* src, uint64_t n, void* dst, uint64_t dst_off, hipStream_t s);
 vxg_status launch_assign_bits_at(void* dst, uint64_t dst_off, const void* idx, int iw, bool isg, uint64_t ioff,
                                  uint64_t n, uint64_t len, const uint8_t* vals, hipStream_t s);
+vxg_status launch_gather_bits(void* dst, const void* codes, int cw, uint64_t n, const uint8_t* src, uint64_t n_values,
+                              uint32_t* err, hipStream_t s);
 vxg_status launch_set_bits_at(void* dst, const void* idx, int iw, bool isg, uint64_t off, uint64_t n,
                               uint64_t len, hipStream_t s);
 vxg_status launch_sum(const void* p, int w, bool sg, uint64_t n, void* out_u64, hipStream_t s);
