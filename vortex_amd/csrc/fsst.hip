@@ -178,29 +178,31 @@ __device__ __forceinline__ void scan_tile_sums(const int64_t* s_ts, int64_t* ws,
 }
 
 // Chunk of workgroup g in a launch: workgroup-uniform binary search on the kernarg table's
-// first_*, or the wave-wide count over a recorded plan's device table (returned by value:
-// the fields the kernel uses land in scalar registers).
-template <bool SCAN>
-__device__ __forceinline__ FsstChunk fsst_chunk_of(const FsstTable& tab, uint64_t g) {
-    if (tab.ext)
+// first_*, or (EXT: a recorded plan's device table of any length) the wave-wide count.  EXT is
+// a template parameter so the kernarg path keeps its scalar-load code unchanged.
+template <bool SCAN, bool EXT>
+__device__ __forceinline__ const FsstChunk& fsst_chunk_of(const FsstTable& tab, uint64_t g) {
+    if constexpr (EXT) {
         return tab.ext[ext_chunk_index(tab.ext, tab.n, g,
                                        [](const FsstChunk& d) { return SCAN ? d.first_scan : d.first_tile; })];
-    uint32_t lo = 0, hi = tab.n;
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if ((SCAN ? tab.c[mid].first_scan : tab.c[mid].first_tile) <= g) lo = mid; else hi = mid;
+    } else {
+        uint32_t lo = 0, hi = tab.n;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if ((SCAN ? tab.c[mid].first_scan : tab.c[mid].first_tile) <= g) lo = mid; else hi = mid;
+        }
+        return tab.c[lo];
     }
-    return tab.c[lo];
 }
 
 // Any length column: wave w sums tile 4r + w in round r (4 consecutive lengths per lane).
-template <class LenAcc>
+template <class LenAcc, bool EXT>
 __global__ __launch_bounds__(kTile) void fsst_tile_scan(FsstTable tab, int64_t* __restrict__ tile_prefix_all,
                                                         int64_t* __restrict__ block_totals_all) {
     __shared__ int64_t s_ts[kScanTiles];
     __shared__ int64_t ws[kTile / 64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const FsstChunk c = fsst_chunk_of<true>(tab, blockIdx.x);
+    const FsstChunk& c = fsst_chunk_of<true, EXT>(tab, blockIdx.x);
     const LenAcc lens(c.lens);
     const uint64_t n = c.n, n_tiles = (n + kTile - 1) / kTile, sb = blockIdx.x - c.first_scan;
     int64_t* const tile_prefix = tile_prefix_all + c.first_tile;
@@ -252,13 +254,13 @@ __device__ __forceinline__ void fl32_tile_rows(const Vec16<32>* p, int t, uint64
     (row(std::integral_constant<int, Rs>{}), ...);
 }
 
-template <int W>
+template <int W, bool EXT>
 __global__ __launch_bounds__(kTile) void fsst_tile_scan_fl32(FsstTable tab, int64_t* __restrict__ tile_prefix_all,
                                                              int64_t* __restrict__ block_totals_all) {
     __shared__ int64_t s_ts[kScanTiles];
     __shared__ int64_t ws[kTile / 64];
     const int tid = threadIdx.x, t = tid & 7;
-    const FsstChunk c = fsst_chunk_of<true>(tab, blockIdx.x);
+    const FsstChunk& c = fsst_chunk_of<true, EXT>(tab, blockIdx.x);
     const uint8_t* __restrict__ packed = static_cast<const uint8_t*>(c.lens.p);
     const uint32_t shift = c.lens.shift, reference = uint32_t(c.lens.reference);
     const bool sgn = c.lens.sgn;
@@ -288,7 +290,7 @@ __global__ __launch_bounds__(kTile) void fsst_tile_scan_fl32(FsstTable tab, int6
     scan_tile_sums(s_ts, ws, n_tiles, sb, tile_prefix, block_totals);
 }
 
-template <class OffAcc, class LenAcc>
+template <class OffAcc, class LenAcc, bool EXT>
 __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t total_tiles,
                                                      const int64_t* __restrict__ tile_prefix_all,
                                                      const int64_t* __restrict__ block_totals_all,
@@ -306,7 +308,7 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
     uint8_t* const s_heap = reinterpret_cast<uint8_t*>(s_heap32);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 
-    const FsstChunk ch = fsst_chunk_of<false>(tab, blockIdx.x);
+    const FsstChunk& ch = fsst_chunk_of<false, EXT>(tab, blockIdx.x);
     const uint64_t* __restrict__ symbols = ch.symbols;
     const uint8_t* __restrict__ sym_lens = ch.sym_lens;
     const unsigned n_symbols = ch.n_symbols;
@@ -597,8 +599,9 @@ template <int... Ws>
 void launch_tile_scan_fl32(int W, dim3 grid, hipStream_t s, const FsstTable& t, int64_t* tiles, int64_t* blocks,
                            std::integer_sequence<int, Ws...>) {
     using Fn = void (*)(FsstTable, int64_t*, int64_t*);
-    static constexpr Fn table[] = {&fsst_tile_scan_fl32<Ws>...};
-    hipLaunchKernelGGL(table[W], grid, dim3(kTile), 0, s, t, tiles, blocks);
+    static constexpr Fn table[] = {&fsst_tile_scan_fl32<Ws, false>...};
+    static constexpr Fn table_ext[] = {&fsst_tile_scan_fl32<Ws, true>...};
+    hipLaunchKernelGGL((t.ext ? table_ext : table)[W], grid, dim3(kTile), 0, s, t, tiles, blocks);
 }
 
 // accessor = plain width 1/2/4/8 or packed T = 32/64
@@ -669,10 +672,16 @@ vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint
                 ok = with_acc(std::get<1>(key), [&](auto* la) {
                     using OA = std::remove_pointer_t<decltype(oa)>;
                     using LA = std::remove_pointer_t<decltype(la)>;
-                    if (std::get<2>(key) < 0)
-                        hipLaunchKernelGGL((fsst_tile_scan<LA>), dim3(unsigned(scans)), dim3(kTile), 0, s, tab, tp, bt);
-                    hipLaunchKernelGGL((fsst_decode<OA, LA>), dim3(unsigned(tiles)), dim3(kTile), 0, s, tab, tiles, tp, bt,
-                                       err);
+                    auto go = [&](auto ext) {
+                        constexpr bool X = decltype(ext)::value;
+                        if (std::get<2>(key) < 0)
+                            hipLaunchKernelGGL((fsst_tile_scan<LA, X>), dim3(unsigned(scans)), dim3(kTile), 0, s, tab,
+                                               tp, bt);
+                        hipLaunchKernelGGL((fsst_decode<OA, LA, X>), dim3(unsigned(tiles)), dim3(kTile), 0, s, tab,
+                                           tiles, tp, bt, err);
+                    };
+                    if (tab.ext) go(std::true_type{});
+                    else go(std::false_type{});
                 });
             });
             if (!ok) return set_error(VXG_ERR_MISMATCHED_TYPES, "FSST accessor");
