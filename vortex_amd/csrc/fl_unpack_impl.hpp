@@ -344,22 +344,10 @@ __device__ __forceinline__ void stage_dict(uint8_t* s_dict, const void* dict, ui
 // S = 1: 8 threads per block, 32 blocks per workgroup (large launches).  S = 4 (T = 32/64):
 // each wave takes one quarter of the rows of 8 blocks -> 8 blocks per workgroup and 4x the
 // threads, for launches too small to fill 256 CUs (the quarter is wave-uniform, no divergence).
-template <int T, int W, Epi EPI, int VW, bool LDSD = false, int S = 1>
-__global__ __launch_bounds__(256) void fl_unpack_kernel(ChunkTable tab) {
+template <int T, int W, Epi EPI, int VW, bool LDSD, int S>
+__device__ __forceinline__ void unpack_chunk(const ChunkDev& c, uint64_t g, uint32_t* err) {
     using O = typename EpiOut<T, EPI, VW>::type;
     constexpr int BPG = 32 / S;  // blocks per workgroup
-    const uint64_t g = blockIdx.x;
-    ChunkDev c;  // this workgroup's chunk (scalar registers)
-    if (tab.ext) {
-        c = tab.ext[ext_chunk_index(tab.ext, tab.n, g, [](const ChunkDev& d) { return d.first_group; })];
-    } else {
-        uint32_t lo = 0, hi = tab.n;
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (tab.c[mid].first_group <= g) lo = mid; else hi = mid;
-        }
-        c = tab.c[lo];
-    }
     const uint64_t blk = (g - c.first_group) * BPG + ((threadIdx.x >> 3) % BPG);
     const int t = int(threadIdx.x & 7);
     EpiParams ep;
@@ -369,8 +357,8 @@ __global__ __launch_bounds__(256) void fl_unpack_kernel(ChunkTable tab) {
     ep.alp_b = c.alp_b;
     ep.dict = c.dict;
     ep.dict_len = c.dict_len;
-    ep.err = tab.err;
-    if constexpr (LDSD) {  // the whole workgroup is in chunk `lo`
+    ep.err = err;
+    if constexpr (LDSD) {  // the whole workgroup is in this chunk
         __shared__ __attribute__((aligned(16))) uint8_t s_dict[kDictLdsBytes];
         stage_dict<VW>(s_dict, c.dict, c.dict_len);
         ep.dict = s_dict;
@@ -397,10 +385,30 @@ __global__ __launch_bounds__(256) void fl_unpack_kernel(ChunkTable tab) {
     }
 }
 
+// EXT: the chunk table is a recorded plan's device table (any length; one wave-wide count
+// finds the chunk) instead of the kernel argument -- a separate instantiation, so the kernarg
+// path keeps its scalar-load code (a runtime branch cost C1 1 %).
+template <int T, int W, Epi EPI, int VW, bool LDSD = false, int S = 1, bool EXT = false>
+__global__ __launch_bounds__(256) void fl_unpack_kernel(ChunkTable tab) {
+    const uint64_t g = blockIdx.x;
+    if constexpr (EXT) {
+        const ChunkDev& c =
+            tab.ext[ext_chunk_index(tab.ext, tab.n, g, [](const ChunkDev& d) { return d.first_group; })];
+        unpack_chunk<T, W, EPI, VW, LDSD, S>(c, g, tab.err);
+    } else {
+        uint32_t lo = 0, hi = tab.n;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (tab.c[mid].first_group <= g) lo = mid; else hi = mid;
+        }
+        unpack_chunk<T, W, EPI, VW, LDSD, S>(tab.c[lo], g, tab.err);
+    }
+}
+
 // A launch with fewer 32-block workgroups than this uses the row split (S = 4).
 constexpr uint64_t kSplitBelowGroups = 512;
 
-template <int T, int W, Epi EPI, int VW, bool LDSD, int S>
+template <int T, int W, Epi EPI, int VW, bool LDSD, int S, bool EXT = false>
 vxg_status launch_s(ChunkTable tab, hipStream_t s) {
     // first workgroup of each chunk at this launch's blocks per workgroup (a device table's
     // host mirror is completed here and uploaded when the plan is finalised)
@@ -412,7 +420,7 @@ vxg_status launch_s(ChunkTable tab, hipStream_t s) {
     }
     if (groups == 0) return VXG_OK;
     if (groups > 0xFFFFFFFFull) return set_error(VXG_ERR_INVALID_ARGUMENT, "array too long for one launch");
-    hipLaunchKernelGGL((fl_unpack_kernel<T, W, EPI, VW, LDSD, S>), dim3(unsigned(groups)), dim3(256), 0, s, tab);
+    hipLaunchKernelGGL((fl_unpack_kernel<T, W, EPI, VW, LDSD, S, EXT>), dim3(unsigned(groups)), dim3(256), 0, s, tab);
     return hip_check(hipGetLastError(), "fl_unpack_kernel launch");
 }
 
@@ -429,6 +437,13 @@ vxg_status launch_one(const ChunkTable& tab, uint64_t groups32, hipStream_t s) {
         for (uint32_t k = 0; k < tab.n; k++)
             lds = lds && cs[k].dict_len * VW <= uint64_t(kDictLdsBytes) &&
                   (reinterpret_cast<uintptr_t>(cs[k].dict) & 15) == 0;
+    }
+    if (tab.ext) {  // device table (plans): one variant, row split where it exists
+        constexpr int SX = kSplit ? 4 : 1;
+        if constexpr (EPI == Epi::Dict) {
+            if (lds) return launch_s<T, W, EPI, VW, true, SX, true>(tab, s);
+        }
+        return launch_s<T, W, EPI, VW, false, SX, true>(tab, s);
     }
     if constexpr (kSplit) {
         if (split) return lds ? launch_s<T, W, EPI, VW, true, 4>(tab, s) : launch_s<T, W, EPI, VW, false, 4>(tab, s);
