@@ -761,3 +761,77 @@ def test_dict_nullable_values(ctx):
     got = A.canonicalize(ch.to(torch_dev()), ctx)
     want, wvalid = canon(ch)
     assert got.numpy().tobytes() == want.tobytes() and np.array_equal(got.validity_mask(), wvalid)
+
+
+# ------------------------------------------------------------------ compute::take on compressed arrays
+def _take_case(ctx, arr, idx):
+    got = A.take(arr.to(torch_dev()), idx, ctx)
+    vals, valid = canon(arr)
+    ii = np.asarray(idx).astype(np.int64)
+    want = np.ascontiguousarray(vals[ii])
+    assert got.numpy().tobytes() == want.tobytes()
+    if valid is None:
+        assert got.validity is None or got.validity_mask().all()
+    else:
+        assert np.array_equal(got.validity_mask(), valid[ii])
+
+
+@pytest.mark.parametrize("T,W", [(8, 3), (16, 11), (32, 7), (32, 31), (64, 1), (64, 24), (64, 63)])
+def test_take_bitpacked(ctx, T, W):
+    """bitpacking/compute/take.rs:21-125: unpack_single of the taken positions only (few
+    indices) and the canonicalize-then-take path (many indices, take.rs:23-31)."""
+    rng = np.random.default_rng(T * 100 + W)
+    n = 70_001
+    dt = {8: np.uint8, 16: np.uint16, 32: np.uint32, 64: np.uint64}[T]
+    vals = (rng.integers(0, 1 << 62, n, dtype=np.uint64) & np.uint64((1 << W) - 1 if W < 64 else (1 << 64) - 1)).astype(dt)
+    arr = E.encode_bitpacked(vals, bit_width=W, allow_patches=False)
+    for k in (0, 1, 17, 5000, 40_000):
+        _take_case(ctx, arr, rng.integers(0, n, k).astype(np.uint32))
+    _take_case(ctx, arr, np.array([0, n - 1, 1023, 1024, 1025], np.int64))
+
+
+def test_take_cascades(ctx):
+    rng = np.random.default_rng(77)
+    n = 100_000
+    idx = rng.integers(0, n, 3000).astype(np.uint64)
+    # patches (inner): a few wide outliers
+    v = rng.integers(0, 1 << 9, n).astype(np.uint32)
+    v[rng.choice(n, 300, replace=False)] = rng.integers(1 << 20, 1 << 31, 300).astype(np.uint32)
+    bp = E.encode_bitpacked(v, allow_patches=True)
+    assert bp.meta["has_patches"]
+    _take_case(ctx, bp, idx)
+    _take_case(ctx, bp, np.sort(rng.choice(n, 500, replace=False)).astype(np.int32))
+    # sliced offset
+    _take_case(ctx, E.encode_bitpacked(v[:5000] & 511, bit_width=9, allow_patches=False, offset=300),
+               rng.integers(0, 5000 - 300, 200).astype(np.uint16))
+    # FoR / ZigZag / ALP (+ patches) / Dict
+    s = rng.integers(-(1 << 40), 1 << 40, n).astype(np.int64)
+    _take_case(ctx, E.encode_for_bitpacked(s), idx)
+    _take_case(ctx, E.encode_zigzag(rng.integers(-5000, 5000, n).astype(np.int32)), idx)
+    prices = np.round(rng.uniform(1, 100_000, n) * 100) / 100
+    prices[rng.choice(n, 100, replace=False)] = rng.uniform(0, 1, 100) * np.pi
+    _take_case(ctx, E.encode_alp(prices), idx)
+    _take_case(ctx, E.encode_alp(np.round(rng.uniform(0, 100, n), 1).astype(np.float32)), idx)
+    dv = rng.integers(0, 1 << 40, 300).astype(np.uint64)
+    _take_case(ctx, A.dict_array(A.primitive(dv), E.encode_bitpacked(rng.integers(0, 300, n).astype(np.uint64),
+                                                                     allow_patches=False)), idx)
+    # anything else: canonicalize + gather (chunked, runend)
+    _take_case(ctx, A.chunked([E.encode_bitpacked(v[:40_000] & 511, bit_width=9, allow_patches=False),
+                               A.primitive(v[40_000:])]), idx)
+    _take_case(ctx, E.encode_runend(np.repeat(np.arange(1000, dtype=np.int32), 100)), idx)
+
+
+def test_take_validity_and_errors(ctx):
+    rng = np.random.default_rng(78)
+    n = 50_000
+    v = rng.integers(0, 1 << 12, n).astype(np.uint32)
+    m = rng.random(n) > 0.3
+    idx = rng.integers(0, n, 2000).astype(np.int64)
+    _take_case(ctx, E.encode_bitpacked(v, bit_width=12, allow_patches=False, validity=m), idx)
+    _take_case(ctx, A.primitive(v, validity=E.encode_runend_bool(m)), idx)
+    _take_case(ctx, E.encode_bitpacked(v, bit_width=12, allow_patches=False), np.zeros(0, np.uint32))
+    # out-of-bounds index -> OutOfBounds at the next sync (compute/take.rs bounds)
+    with pytest.raises(V.VortexGpuError) as ei:
+        A.take(E.encode_bitpacked(v, bit_width=12, allow_patches=False).to(torch_dev()),
+               np.array([1, n], np.uint32), ctx)
+    assert ei.value.kind == "OutOfBounds"

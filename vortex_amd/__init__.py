@@ -6,8 +6,8 @@ package is the host-side mirror of the reference's array/encoding API for that p
 `encode` (the reference encoders, used to build inputs) and `canonicalize` (the C-ABI call).
 """
 from ._lib import ENC, PTYPE, PTYPES, VortexGpuError, gpu_lib, enc_lib  # noqa: F401
-from .arrays import Array, Canonical, Context, Plan, canonicalize  # noqa: F401
+from .arrays import Array, Canonical, Context, Plan, canonicalize, take  # noqa: F401
 from . import arrays, encode  # noqa: F401
 
-__all__ = ["Array", "Canonical", "Context", "Plan", "canonicalize", "arrays", "encode", "ENC", "PTYPE",
+__all__ = ["Array", "Canonical", "Context", "Plan", "canonicalize", "take", "arrays", "encode", "ENC", "PTYPE",
            "PTYPES", "VortexGpuError", "gpu_lib", "enc_lib"]

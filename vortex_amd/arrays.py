@@ -570,6 +570,42 @@ def canonicalize(a: Array, ctx: Context, out_values=None, sync: bool = True) -> 
     return res
 
 
+def take(a: Array, indices, ctx: Context, sync: bool = True) -> Canonical:
+    """compute::take (vortex-array/src/compute/take.rs:10-34) on the compressed tree
+    (vxg_take_array): BitPacked / FoR / ZigZag / ALP cascades decode only the taken values, Dict
+    takes its codes; `indices` is a device tensor or host array of integers."""
+    import torch
+    keep: list = []
+    node = flatten(a, keep)
+    dev = torch.device("cuda", ctx.device)
+    if isinstance(indices, torch.Tensor):
+        it = indices.to(dev)
+        ip = {torch.uint8: "u8", torch.int8: "i8", torch.int16: "i16", torch.int32: "i32",
+              torch.int64: "i64"}[it.dtype]
+    else:
+        ia = np.ascontiguousarray(indices)
+        ip = PTYPE_OF_NP[ia.dtype]
+        it = torch.from_numpy(ia.view(np.uint8).copy()).to(dev)
+    n = int(it.numel() if isinstance(indices, torch.Tensor) else np.asarray(indices).size)
+    out = _lib.VxgCanonical()
+    w = ptype_width(a.ptype)
+    vals = torch.empty(max(n * w, 16), dtype=torch.uint8, device=dev)
+    out.values = vals.data_ptr()
+    vt = torch.empty(((n + 31) // 32) * 4 + 4, dtype=torch.uint8, device=dev) if a.nullable else None
+    if vt is not None:
+        out.validity = vt.data_ptr()
+    _lib.check(ctx.lib.vxg_take_array(ctx.handle, C.byref(node), PTYPE[ip], C.c_void_p(it.data_ptr()), n,
+                                      C.byref(out), ctx.stream_ptr()))
+    res = Canonical("primitive", n, a.ptype, values=vals[: n * w])
+    if out.validity:
+        if vt is None or out.validity != vt.data_ptr():
+            raise VortexError(7, "engine allocated validity for a non-nullable dtype")
+        res.validity = vt[: (n + 7) // 8]
+    if sync:
+        ctx.sync()
+    return res
+
+
 class Plan:
     """vxg_plan: the launches of canonicalizing `arrays` into preallocated outputs, recorded
     once as a HIP graph and replayed by launch() (one hipGraphLaunch; every kernel runs on

@@ -16,6 +16,7 @@
 #include <tuple>
 #include <vector>
 
+#include "take.hpp"
 #include "vxg_internal.hpp"
 
 struct vxg_ctx {
@@ -222,6 +223,8 @@ class Planner {
     }
 
     vxg_status canonical(const vxg_array& a, vxg_canonical& out);
+    // compute::take on the compressed tree (take.hip): values + validity.take(indices)
+    vxg_status take(const vxg_array& a, const void* idx, int iw, bool isg, uint64_t n, vxg_canonical& out);
     vxg_status canonical_size(const vxg_array& a, uint64_t& vb, uint64_t& db);
     // Data buffers of a string canonical, placed 16-byte aligned in one allocation.
     vxg_status string_layout(const vxg_array& a, std::vector<vxg_data_buffer>& bufs, uint64_t& extent);
@@ -288,6 +291,8 @@ class Planner {
     vxg_status decode_alprd(const vxg_array& a, void* dst);
     vxg_status decode_sparse_values(const vxg_array& a, void* dst);
 
+    vxg_status take_values(const vxg_array& a, const void* idx, int iw, bool isg, uint64_t n, void* dst);
+    vxg_status take_patches(const vxg_array& sp, TakePatches& p);
     vxg_status validity_into(const vxg_array& a, void** bitmap);
     // OR the values of a Bool-dtype array into the zeroed bit buffer `bits` at bit `off`.
     vxg_status bools_into(const vxg_array& a, void* bits, uint64_t off);
@@ -855,6 +860,137 @@ vxg_status Planner::validity_into(const vxg_array& a, void** bitmap) {
         off += c.len;
     }
     return VXG_OK;
+}
+
+// ---- compute::take on compressed arrays (vortex-array/src/compute/take.rs:10-34) ---------
+vxg_status Planner::take_patches(const vxg_array& sp, TakePatches& p) {
+    if (sp.encoding != VXG_ENC_SPARSE) return set_error(VXG_ERR_INVALID_ARGUMENT, "Can't patch with a non-Sparse array");
+    const vxg_array* idx = child(sp, 0);
+    const vxg_array* val = child(sp, 1);
+    if (!idx || !val || idx->len != val->len)
+        return set_error(VXG_ERR_INVALID_ARGUMENT, "Sparse patches need indices and values of equal length");
+    if (!ptype_is_int(idx->ptype)) return set_error(VXG_ERR_MISMATCHED_TYPES, "Sparse indices must be integers");
+    VXG_TRY(view_primitive(*idx, &p.idx));
+    VXG_TRY(view_primitive(*val, &p.values));
+    p.n = idx->len;
+    p.off = sp.meta.sparse.indices_offset;
+    p.iw = width(*idx);
+    p.isg = ptype_is_signed(idx->ptype);
+    return VXG_OK;
+}
+
+vxg_status Planner::take_values(const vxg_array& a, const void* idx, int iw, bool isg, uint64_t n, void* dst) {
+    if (n == 0) return VXG_OK;
+    auto via_canonical = [&]() -> vxg_status {  // canonicalize, then take the primitive
+        const void* pv;
+        VXG_TRY(view_primitive(a, &pv));
+        return launch_take(width(a), pv, a.len, iw, idx, n, dst, ctx_->c.err_word, s_);
+    };
+    const vxg_array* bp = nullptr;
+    Epi epi = Epi::Plain;
+    EpiParams ep{};
+    TakePatches outer;
+    auto fl_child = [&](const vxg_array* c) -> const vxg_array* {  // FoR(BitPacked) or BitPacked
+        if (c && c->encoding == VXG_ENC_FL_FOR && child(*c, 0) && child(*c, 0)->encoding == VXG_ENC_FL_BITPACKED) {
+            ep.reference = c->meta.for_.reference;
+            ep.shift = c->meta.for_.shift;
+            return child(*c, 0);
+        }
+        return c && c->encoding == VXG_ENC_FL_BITPACKED ? c : nullptr;
+    };
+    switch (a.encoding) {
+    case VXG_ENC_FL_BITPACKED: bp = &a; break;  // bitpacking/compute/take.rs:21-125
+    case VXG_ENC_FL_FOR:                          // for/compute.rs:39-48: take the child, keep the FoR
+        bp = fl_child(&a);
+        epi = Epi::For;
+        break;
+    case VXG_ENC_ZIGZAG:  // zigzag/compute.rs: take the encoded child, decode
+        bp = fl_child(child(a, 0));
+        epi = Epi::ForZigZag;
+        break;
+    case VXG_ENC_ALP: {  // alp/compute.rs: take the encoded child and the patches
+        const bool f32 = a.ptype == VXG_F32;
+        const unsigned e = a.meta.alp.e, f = a.meta.alp.f;
+        if ((f32 && (e > 10 || f > 10)) || (!f32 && (a.ptype != VXG_F64 || e > 23 || f > 23))) return via_canonical();
+        bp = fl_child(child(a, 0));
+        epi = f32 ? Epi::AlpF32 : Epi::AlpF64;
+        ep.alp_a = f32 ? double(kF10f[f]) : kF10d[f];
+        ep.alp_b = f32 ? double(kIF10f[e]) : kIF10d[e];
+        if (bp && a.meta.alp.has_patches) {
+            if (!child(a, 1)) return set_error(VXG_ERR_INVALID_ARGUMENT, "ALPArray: patches child missing");
+            VXG_TRY(take_patches(*child(a, 1), outer));
+        }
+        break;
+    }
+    case VXG_ENC_DICT: {  // dict/compute.rs:44-52: take the codes, then the values at them
+        const vxg_array* values = child(a, 0);
+        const vxg_array* codes = child(a, 1);
+        if (!values || !codes || values->dtype != VXG_DTYPE_PRIMITIVE || !ptype_is_int(codes->ptype))
+            return via_canonical();
+        void* tc;
+        VXG_TRY(temp(n * width(*codes), &tc));
+        VXG_TRY(take_values(*codes, idx, iw, isg, n, tc));
+        const void* pv;
+        VXG_TRY(view_primitive(*values, &pv));
+        return launch_take(width(*values), pv, values->len, width(*codes), tc, n, dst, ctx_->c.err_word, s_);
+    }
+    default: return via_canonical();
+    }
+    const int T = bp ? 8 * width(*bp) : 0;
+    const bool t_ok = bp && (epi == Epi::AlpF32 ? T == 32 : epi == Epi::AlpF64 ? T == 64 : T == 8 * width(a));
+    // bitpacking/compute/take.rs:23-31: many indices -> canonicalize and take the primitive
+    if (!t_ok || bp->len != a.len || n * 8 > a.len) return via_canonical();
+    const vxg_buffer* pb = buf(*bp, 0);
+    const unsigned W = bp->meta.bitpacked.bit_width, off = bp->meta.bitpacked.offset;
+    if (off > 1023) return set_error(VXG_ERR_INVALID_ARGUMENT, "Offset must be less than full block, i.e. 1024");
+    if (W > unsigned(T)) return set_error(VXG_ERR_INVALID_ARGUMENT, "Unsupported bit width");
+    const uint64_t nblk = (bp->len + off + 1023) / 1024, have = pb ? pb->len : 0;
+    if (W > 0 && have != nblk * 128ull * W)  // bitpacking/mod.rs:80-88
+        return set_error(VXG_ERR_INVALID_ARGUMENT, "Expected " + std::to_string(nblk * 128ull * W) +
+                                                       " packed bytes, got " + std::to_string(have));
+    TakePacked t{};
+    t.packed = pb ? static_cast<const uint8_t*>(pb->ptr) : nullptr;
+    t.W = W;
+    t.offset = off;
+    t.len = a.len;
+    t.idx = idx;
+    t.iw = iw;
+    t.isg = isg;
+    t.n = n;
+    t.out = dst;
+    t.ep = ep;
+    t.outer = outer;
+    t.err = ctx_->c.err_word;
+    if (bp->meta.bitpacked.has_patches) {  // take.rs:127-200: patches of the taken positions
+        if (!child(*bp, 0)) return set_error(VXG_ERR_INVALID_ARGUMENT, "BitPacked patches child missing");
+        VXG_TRY(take_patches(*child(*bp, 0), t.inner));
+    }
+    return launch_take_packed(T, epi, t, s_);
+}
+
+vxg_status Planner::take(const vxg_array& a, const void* idx, int iw, bool isg, uint64_t n, vxg_canonical& out) {
+    if (a.dtype != VXG_DTYPE_PRIMITIVE) return set_error(VXG_ERR_NOT_IMPLEMENTED, "take supports primitive arrays");
+    out.kind = VXG_ENC_PRIMITIVE;
+    out.len = n;
+    out.dtype = a.dtype;
+    out.ptype = a.ptype;
+    out.values_bytes = n * width(a);
+    if (!out.values)
+        VXG_TRY(hip_check(hipMalloc(&out.values, out.values_bytes ? out.values_bytes : 16), "take values alloc"));
+    VXG_TRY(take_values(a, idx, iw, isg, n, out.values));
+    const vxg_array* node;
+    int kind;
+    VXG_TRY(validity_source(a, &node, &kind));
+    if (kind == 0) {  // validity.take of NonNullable / AllValid: no nulls
+        out.validity = nullptr;
+        return VXG_OK;
+    }
+    void* src = nullptr;  // the array's validity, then taken at the indices
+    VXG_TRY(temp(((a.len + 31) / 32) * 4, &src));
+    VXG_TRY(validity_into(a, &src));
+    const uint64_t bytes = ((n + 31) / 32) * 4;
+    if (!out.validity) VXG_TRY(hip_check(hipMalloc(&out.validity, bytes ? bytes : 4), "take validity alloc"));
+    return launch_gather_bits(out.validity, idx, iw, n, static_cast<const uint8_t*>(src), a.len, ctx_->c.err_word, s_);
 }
 
 // ---- bools: canonical BoolArray = LSB bit buffer (bool/mod.rs), from every Bool encoding ----
@@ -1652,6 +1788,15 @@ vxg_status vxg_runend_decode(vxg_ctx* ctx, unsigned value_width, const void* val
     if (!ptype_is_int(ends_ptype)) return set_error(VXG_ERR_MISMATCHED_TYPES, "RunEnd ends must be integers");
     return launch_runend(int(value_width), values, ptype_width(ends_ptype), ends, n_runs, offset, len, out,
                          ctx->c.err_word, S(stream));
+}
+
+vxg_status vxg_take_array(vxg_ctx* ctx, const vxg_array* a, int indices_ptype, const void* indices,
+                          uint64_t n_indices, vxg_canonical* out, void* stream) {
+    VXG_TRY(use_device(ctx));
+    if (!a || !out || (n_indices && !indices)) return set_error(VXG_ERR_INVALID_ARGUMENT, "null array/indices/out");
+    if (!ptype_is_int(indices_ptype)) return set_error(VXG_ERR_INVALID_ARGUMENT, "take indices must be integers");
+    Planner p(ctx, S(stream));
+    return p.take(*a, indices, ptype_width(indices_ptype), ptype_is_signed(indices_ptype), n_indices, *out);
 }
 
 vxg_status vxg_runend_bool_decode(vxg_ctx* ctx, int ends_ptype, const void* ends, uint64_t n_runs, uint64_t offset,
