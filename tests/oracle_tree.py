@@ -298,3 +298,38 @@ def view_bytes(views: np.ndarray, heap, i: int):
     off = int(np.frombuffer(v[12:16].tobytes(), dtype=np.uint32)[0])
     buf = heap[bi] if isinstance(heap, list) else heap
     return buf[off: off + n].tobytes()
+
+
+def filter_canon(a: Array, predicate: Array):
+    """compute::filter (compute/filter.rs:23-52) on the CPU: canonical of the selected rows.
+
+    Primitive / Bool: `filter_primitive_slice` (primitive/compute/filter.rs:32-48) and
+    bool/compute/filter.rs:15-60 keep the set rows in order; validity.filter the same way.
+    Strings: VarBin's filter (varbin/compute/filter.rs:135-200, by index; the by-slice path
+    builds the same bytes) appends each selected value to a VarBinBuilder — a null row as an
+    empty value — and the result canonicalizes through varbin/flatten.rs (one heap, views by
+    vxo_make_views).  FSST's filter (fsst/compute.rs:147-160) filters codes and lengths, whose
+    canonical is the same single heap of the selected strings."""
+    mask = canon_bool(predicate).astype(bool)
+    if predicate.nullable:
+        raise ValueError("predicate must be non-nullable bool")
+    if len(mask) != a.len:
+        raise ValueError("predicate length mismatch")
+    if a.dtype in (DTYPE["PRIMITIVE"], DTYPE["BOOL"]):
+        vals, valid = canon(a) if a.dtype == DTYPE["PRIMITIVE"] else (canon_bool(a), _validity(a))
+        return np.ascontiguousarray(vals[mask]), (None if valid is None else valid[mask])
+    (views, heap), valid = canon(a)
+    idx = np.nonzero(mask)[0]
+    fvalid = None if valid is None else valid[mask]
+    strs = []
+    for j, i in enumerate(idx):
+        strs.append(b"" if (fvalid is not None and not fvalid[j]) else view_bytes(views, heap, int(i)))
+    offs = np.zeros(len(strs) + 1, dtype=np.int64)
+    if strs:
+        offs[1:] = np.cumsum([len(s) for s in strs])
+    new_heap = np.frombuffer(b"".join(strs), dtype=np.uint8).copy()
+    vbits = None if fvalid is None else np.packbits(fvalid, bitorder="little")
+    out = np.zeros((len(strs), 16), dtype=np.uint8)
+    O.lib().vxo_make_views(O.p(new_heap), O.p(offs), len(strs), O.p(vbits) if vbits is not None else None, 0,
+                           O.p(out))
+    return (out, new_heap), fvalid

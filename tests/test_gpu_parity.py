@@ -835,3 +835,112 @@ def test_take_validity_and_errors(ctx):
         A.take(E.encode_bitpacked(v, bit_width=12, allow_patches=False).to(torch_dev()),
                np.array([1, n], np.uint32), ctx)
     assert ei.value.kind == "OutOfBounds"
+
+
+# ------------------------------------------------------------------ compute::filter (stream compaction)
+def _filter_case(ctx, arr, pred):
+    from oracle_tree import filter_canon
+    got = A.filter(arr.to(torch_dev()), pred.to(torch_dev()), ctx)
+    want, wvalid = filter_canon(arr, pred)
+    if arr.dtype == A.DTYPE["PRIMITIVE"]:
+        assert got.len == len(want) and got.numpy().tobytes() == want.tobytes()
+    elif arr.dtype == A.DTYPE["BOOL"]:
+        assert got.len == len(want) and np.array_equal(got.numpy(), want)
+        nb = (got.len + 7) // 8
+        assert got.values.cpu().numpy()[:nb].tobytes() == np.packbits(want, bitorder="little").tobytes()
+    else:
+        wv, wh = want
+        gv, gh = got.numpy()
+        assert got.len == len(wv) and gv.tobytes() == wv.tobytes()  # same views byte for byte
+        assert gh.tobytes() == wh.tobytes() and got.data_buffers == [(0, len(wh))]
+    if wvalid is None:
+        assert got.validity is None
+    else:
+        assert np.array_equal(got.validity_mask(), wvalid)
+    return got
+
+
+def _preds(rng, n):
+    yield A.bool_array(rng.random(n) < 0.5)
+    yield A.bool_array(rng.random(n) < 0.01)
+    yield A.bool_array(np.ones(n, bool))
+    yield A.bool_array(np.zeros(n, bool))
+    m = np.zeros(n, bool)
+    m[:: 4097] = True
+    yield E.encode_runend_bool(m | (np.arange(n) % 9000 < 3000))
+    yield A.constant_bool(True, n)
+
+
+@pytest.mark.parametrize("n", [0, 1, 63, 64, 4095, 4097, 70_001])
+def test_filter_primitive_sizes(ctx, n):
+    """primitive/compute/filter.rs:15-50: selected rows in order, at tile edges (64, 4096)."""
+    rng = np.random.default_rng(n + 5)
+    v = rng.integers(0, 1 << 30, n).astype(np.uint32)
+    for pred in _preds(rng, n):
+        _filter_case(ctx, A.primitive(v), pred)
+
+
+def test_filter_compressed_cascades(ctx):
+    """filter.rs:41-49 fallback (canonicalize, then filter) on every primitive encoding."""
+    rng = np.random.default_rng(91)
+    n = 100_000
+    pred = A.bool_array(rng.random(n) < 0.3)
+    v = rng.integers(0, 1 << 9, n).astype(np.uint32)
+    v[rng.choice(n, 300, replace=False)] = rng.integers(1 << 20, 1 << 31, 300).astype(np.uint32)
+    _filter_case(ctx, E.encode_bitpacked(v, allow_patches=True), pred)
+    _filter_case(ctx, E.encode_for_bitpacked(rng.integers(-(1 << 40), 1 << 40, n).astype(np.int64)), pred)
+    _filter_case(ctx, E.encode_zigzag(rng.integers(-5000, 5000, n).astype(np.int16)), pred)
+    prices = np.round(rng.uniform(1, 100_000, n) * 100) / 100
+    _filter_case(ctx, E.encode_alp(prices), pred)
+    _filter_case(ctx, E.encode_dict(rng.integers(0, 50, n).astype(np.uint8) * 3), pred)
+    _filter_case(ctx, E.encode_runend(np.repeat(np.arange(1000, dtype=np.int64), 100)), pred)
+    _filter_case(ctx, E.encode_delta(np.cumsum(rng.integers(0, 5, n)).astype(np.uint64)), pred)
+    _filter_case(ctx, A.chunked([E.encode_bitpacked(v[:40_000] & 511, bit_width=9, allow_patches=False),
+                                 A.primitive(v[40_000:])]), pred)
+    # 16-byte-free widths: u8 / u16 / f32
+    _filter_case(ctx, A.primitive(rng.integers(0, 255, n).astype(np.uint8)), pred)
+    _filter_case(ctx, A.primitive(rng.standard_normal(n).astype(np.float32)), pred)
+
+
+def test_filter_validity_and_bools(ctx):
+    """validity.filter(predicate) and BoolArray filter (bool/compute/filter.rs:15-60)."""
+    rng = np.random.default_rng(92)
+    n = 77_777
+    m = rng.random(n) > 0.3
+    v = rng.integers(0, 1 << 12, n).astype(np.uint32)
+    for pred in _preds(rng, n):
+        _filter_case(ctx, E.encode_bitpacked(v, bit_width=12, allow_patches=False, validity=m), pred)
+        _filter_case(ctx, A.bool_array(rng.random(n) < 0.5, validity=E.encode_runend_bool(m)), pred)
+    _filter_case(ctx, E.encode_runend_bool(rng.random(n) < 0.001), A.bool_array(rng.random(n) < 0.7))
+
+
+def test_filter_strings(ctx):
+    """VarBin / FSST filter (varbin/compute/filter.rs:19-200, fsst/compute.rs:147-160): the
+    canonical of the result is one heap of the selected strings, null rows empty."""
+    rng = np.random.default_rng(93)
+    n = 20_000
+    strs = [None if i % 7 == 3 else (b"comment %d " % i) * (1 + i % 4) for i in range(n)]
+    strs[5] = b""
+    strs[6] = b"x" * 12
+    strs[8] = b"y" * 13
+    heap, offs, valid = E.strings_to_heap(strs)
+    pred = A.bool_array(rng.random(n) < 0.4)
+    _filter_case(ctx, A.varbin(A.primitive(offs.astype(np.int32)), A.primitive(heap), validity=valid), pred)
+    _filter_case(ctx, E.encode_fsst(strs), pred)
+    _filter_case(ctx, E.encode_fsst([s or b"" for s in strs]), A.bool_array(np.ones(n, bool)))
+    _filter_case(ctx, E.encode_dict_strings([b"alpha", b"a-much-longer-value", b"z"] * 1000),
+                 A.bool_array(rng.random(3000) < 0.5))
+    _filter_case(ctx, A.chunked([E.encode_fsst(strs[:9000]), E.encode_fsst(strs[9000:])]), pred)
+    _filter_case(ctx, E.encode_varbinview(strs), pred)
+
+
+def test_filter_errors(ctx):
+    arr = A.primitive(np.arange(100, dtype=np.uint32)).to(torch_dev())
+    with pytest.raises(V.VortexGpuError) as ei:
+        A.filter(arr, A.bool_array(np.ones(99, bool)).to(torch_dev()), ctx)
+    assert ei.value.kind == "InvalidArgument"
+    with pytest.raises(V.VortexGpuError) as ei:
+        A.filter(arr, A.bool_array(np.ones(100, bool), validity=np.ones(100, bool)).to(torch_dev()), ctx)
+    assert ei.value.kind == "InvalidArgument"
+    with pytest.raises(V.VortexGpuError):
+        A.filter(arr, A.primitive(np.ones(100, np.uint8)).to(torch_dev()), ctx)

@@ -429,3 +429,47 @@ def test_bool_encodings_and_compressed_validity():
     # a RunEndBool validity child on a primitive column
     p = A.primitive(np.arange(300, dtype=np.uint32), validity=E.encode_runend_bool(m))
     assert np.array_equal(canon(p)[1], m)
+
+
+# ---------------------------------------------------------------- compute::filter KATs (oracle)
+def test_kat_filter_primitive_nullable():
+    """compute/filter.rs:61-80 test_filter: [0, None, 1, None, 2] by [T, F, T, F, T] -> [0, 1, 2]."""
+    from oracle_tree import filter_canon
+    items = A.primitive(np.array([0, 0, 1, 0, 2], np.int32), validity=np.array([1, 0, 1, 0, 1], bool))
+    pred = A.bool_array(np.array([1, 0, 1, 0, 1], bool))
+    vals, valid = filter_canon(items, pred)
+    assert vals.tolist() == [0, 1, 2] and valid.tolist() == [True, True, True]
+    # primitive/compute/filter.rs:62-75 filter_run_variant_mixed_test
+    arr = A.primitive(np.array([1, 24, 54, 2, 3, 2, 3, 2], np.uint32))
+    vals, _ = filter_canon(arr, A.bool_array(np.array([1, 1, 0, 1, 1, 1, 0, 1], bool)))
+    assert vals.tolist() == [1, 24, 2, 3, 2, 2]
+
+
+def test_kat_filter_bool_and_varbin():
+    """bool/compute/filter.rs:67-78 and varbin/compute/filter.rs:201-280."""
+    from oracle_tree import filter_canon
+    vals, _ = filter_canon(A.bool_array(np.array([1, 1, 0], bool)), A.bool_array(np.array([1, 0, 1], bool)))
+    assert vals.tolist() == [True, False]
+    words = [b"hello", b"world", b"filter", b"filter2", b"filter3"]
+    heap, offs, _ = E.strings_to_heap(words)
+    vb = A.varbin(A.primitive(offs.astype(np.int32)), A.primitive(heap))
+    (views, h), _ = filter_canon(vb, A.bool_array(np.array([1, 0, 1, 0, 1], bool)))
+    assert [view_bytes(views, h, i) for i in range(3)] == [b"hello", b"filter", b"filter3"]
+    # filter_var_bin_slice_null_test: offsets [0,3,6,11,15,19,22], row 1 null
+    data = np.frombuffer(b"onetwothreefourfivesix", np.uint8).copy()
+    vb = A.varbin(A.primitive(np.array([0, 3, 6, 11, 15, 19, 22], np.int32)), A.primitive(data),
+                  validity=np.array([1, 0, 1, 1, 1, 1], bool))
+    (views, h), valid = filter_canon(vb, A.bool_array(np.array([1, 1, 1, 0, 1, 1], bool)))
+    assert valid.tolist() == [True, False, True, True, True]
+    got = [view_bytes(views, h, i) if valid[i] else None for i in range(5)]
+    assert got == [b"one", None, b"three", b"five", b"six"]
+    assert h.tobytes() == b"onethreefivesix" and not views[1].any()  # null rows keep no bytes
+
+
+def test_filter_oracle_rejects_bad_predicates():
+    from oracle_tree import filter_canon
+    arr = A.primitive(np.arange(4, dtype=np.uint32))
+    with pytest.raises(ValueError):
+        filter_canon(arr, A.bool_array(np.ones(3, bool)))
+    with pytest.raises(ValueError):
+        filter_canon(arr, A.bool_array(np.ones(4, bool), validity=np.ones(4, bool)))

@@ -183,6 +183,7 @@ GPU_SIGNATURES = {
     "vxg_runend_bool_decode": (ST, [VP, INT, VP, U64, U64, INT, U64, VP, U64, VP]),
     "vxg_bytebool_to_bits": (ST, [VP, VP, U64, VP, U64, VP]),
     "vxg_take_array": (ST, [VP, VP, INT, VP, U64, VP, VP]),
+    "vxg_filter_array": (ST, [VP, VP, VP, VP, VP]),
     "vxg_fsst_scratch_bytes": (U64, [U64]),
     "vxg_fsst_decode": (ST, [VP, VP, VP, UINT, VP, INT, VP, INT, VP, U64, VP, VP, VP, VP, VP]),
     "vxg_fill": (ST, [VP, UINT, VP, U64, VP, VP]),

@@ -606,6 +606,59 @@ def take(a: Array, indices, ctx: Context, sync: bool = True) -> Canonical:
     return res
 
 
+def filter(a: Array, predicate: Array, ctx: Context) -> Canonical:
+    """compute::filter (vortex-array/src/compute/filter.rs:23-52) on the GPU (vxg_filter_array):
+    the rows of `a` whose bit in `predicate` (a non-nullable Bool array of any Bool encoding) is
+    set, with the filtered validity; strings come back over one new heap of the selected rows.
+    Synchronous, like the reference (the filtered length is read back)."""
+    import torch
+    keep: list = []
+    node = flatten(a, keep)
+    pnode = flatten(predicate, keep)
+    dev = torch.device("cuda", ctx.device)
+    n = a.len
+    out = _lib.VxgCanonical()
+    kind = _kind(a)
+    if kind == "primitive":
+        buf = torch.empty(max(n * ptype_width(a.ptype), 16), dtype=torch.uint8, device=dev)
+        out.values = buf.data_ptr()
+    elif kind == "bool":
+        buf = torch.empty(((n + 31) // 32) * 4 + 4, dtype=torch.uint8, device=dev)
+        out.values = buf.data_ptr()
+    else:
+        buf = torch.empty(max(16 * n, 16), dtype=torch.uint8, device=dev)
+        out.views = buf.data_ptr()
+    vt = torch.empty(((n + 31) // 32) * 4 + 4, dtype=torch.uint8, device=dev) if a.nullable else None
+    if vt is not None:
+        out.validity = vt.data_ptr()
+    table = (_lib.VxgDataBuffer * 1)()
+    out.data_buffers, out.data_buffers_cap = table, 1
+    _lib.check(ctx.lib.vxg_filter_array(ctx.handle, C.byref(node), C.byref(pnode), C.byref(out), ctx.stream_ptr()))
+    k = int(out.len)
+    res = Canonical(kind, k, a.ptype)
+    if kind == "primitive":
+        res.values = buf[: k * ptype_width(a.ptype)]
+    elif kind == "bool":
+        res.values = buf[: ((k + 31) // 32) * 4]
+    else:
+        res.views = buf[: 16 * k]
+        hb = int(out.data_bytes)
+        host = np.empty(hb + 16, dtype=np.uint8)
+        if out.data:  # the engine sized and allocated the new heap: copy it out and release it
+            _lib.check(ctx.lib.vxg_memcpy_d2h(ctx.handle, C.c_void_p(host.ctypes.data), C.c_void_p(out.data), hb,
+                                              ctx.stream_ptr()))
+            ctx.sync()
+            _lib.check(ctx.lib.vxg_free(ctx.handle, C.c_void_p(out.data)))
+        res.data = torch.from_numpy(host).to(dev)[:hb]
+        res.data_buffers = [(0, hb)]
+    if out.validity:
+        if vt is None or out.validity != vt.data_ptr():
+            raise VortexError(7, "engine allocated validity for a non-nullable dtype")
+        res.validity = vt[: (k + 7) // 8]
+    ctx.sync()
+    return res
+
+
 class Plan:
     """vxg_plan: the launches of canonicalizing `arrays` into preallocated outputs, recorded
     once as a HIP graph and replayed by launch() (one hipGraphLaunch; every kernel runs on

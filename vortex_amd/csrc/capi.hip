@@ -16,6 +16,7 @@
 #include <tuple>
 #include <vector>
 
+#include "filter.hpp"
 #include "take.hpp"
 #include "vxg_internal.hpp"
 
@@ -225,6 +226,8 @@ class Planner {
     vxg_status canonical(const vxg_array& a, vxg_canonical& out);
     // compute::take on the compressed tree (take.hip): values + validity.take(indices)
     vxg_status take(const vxg_array& a, const void* idx, int iw, bool isg, uint64_t n, vxg_canonical& out);
+    // compute::filter (filter.hip): the rows whose predicate bit is set + validity.filter
+    vxg_status filter(const vxg_array& a, const vxg_array& pred, vxg_canonical& out);
     vxg_status canonical_size(const vxg_array& a, uint64_t& vb, uint64_t& db);
     // Data buffers of a string canonical, placed 16-byte aligned in one allocation.
     vxg_status string_layout(const vxg_array& a, std::vector<vxg_data_buffer>& bufs, uint64_t& extent);
@@ -991,6 +994,114 @@ vxg_status Planner::take(const vxg_array& a, const void* idx, int iw, bool isg, 
     const uint64_t bytes = ((n + 31) / 32) * 4;
     if (!out.validity) VXG_TRY(hip_check(hipMalloc(&out.validity, bytes ? bytes : 4), "take validity alloc"));
     return launch_gather_bits(out.validity, idx, iw, n, static_cast<const uint8_t*>(src), a.len, ctx_->c.err_word, s_);
+}
+
+// compute::filter (compute/filter.rs:23-52).  The predicate (any Bool encoding) becomes a bit
+// buffer padded to whole u64 words; one sync reads the true count (the filtered length the
+// reference's Array carries); the array is canonicalized into temporaries and compacted.
+// Strings get a new single heap of the selected rows' bytes (VarBin/FSST filter, then
+// varbin/flatten.rs), null rows as empty values.
+vxg_status Planner::filter(const vxg_array& a, const vxg_array& pred, vxg_canonical& out) {
+    if (pred.dtype != VXG_DTYPE_BOOL || pred.nullable)  // filter.rs:27-32
+        return set_error(VXG_ERR_INVALID_ARGUMENT, "predicate must be non-nullable bool");
+    if (pred.len != a.len)  // filter.rs:33-39
+        return set_error(VXG_ERR_INVALID_ARGUMENT, "predicate.len() is " + std::to_string(pred.len) +
+                                                       ", does not equal array.len() of " + std::to_string(a.len));
+    const bool is_str = a.dtype == VXG_DTYPE_UTF8 || a.dtype == VXG_DTYPE_BINARY;
+    if (!is_str && a.dtype != VXG_DTYPE_BOOL && a.dtype != VXG_DTYPE_PRIMITIVE)
+        return set_error(VXG_ERR_NOT_IMPLEMENTED, "filter supports primitive, bool and utf8/binary dtypes");
+    const uint64_t n = a.len, tiles = filter_tiles(n);
+    void* mask;
+    VXG_TRY(temp(((n + 63) / 64) * 8, &mask));
+    VXG_TRY(hip_check(hipMemsetAsync(mask, 0, ((n + 63) / 64) * 8, s_), "filter mask memset"));
+    VXG_TRY(bools_into(pred, mask, 0));
+    void* toff;
+    VXG_TRY(temp((tiles + 1) * 8, &toff));
+    const uint64_t* m = static_cast<const uint64_t*>(mask);
+    uint64_t* to = static_cast<uint64_t*>(toff);
+    VXG_TRY(launch_filter_count(m, n, to, s_));
+    uint64_t k = 0;
+    VXG_TRY(hip_check(hipMemcpyAsync(&k, to + tiles, 8, hipMemcpyDeviceToHost, s_), "filter count readback"));
+    VXG_TRY(hip_check(hipStreamSynchronize(s_), "filter count sync"));
+
+    // canonical source in temporaries
+    vxg_canonical src{};
+    const vxg_array* vnode;
+    int vkind;
+    VXG_TRY(validity_source(a, &vnode, &vkind));
+    if (vkind != 0) VXG_TRY(temp(((n + 31) / 32) * 4, &src.validity));
+    std::vector<vxg_data_buffer> bufs;
+    if (is_str) {
+        uint64_t extent;
+        VXG_TRY(string_layout(a, bufs, extent));
+        VXG_TRY(temp(16 * n, &src.views));
+        VXG_TRY(temp(extent + 16, &src.data));
+        src.data_bytes = extent;
+        src.data_buffers = bufs.data();
+        src.n_data_buffers = src.data_buffers_cap = uint32_t(bufs.size());
+    } else if (a.dtype == VXG_DTYPE_BOOL) {
+        VXG_TRY(temp(((n + 31) / 32) * 4, &src.values));
+    } else {
+        VXG_TRY(temp(n * width(a), &src.values));
+    }
+    VXG_TRY(canonical(a, src));
+
+    out.kind = src.kind;
+    out.len = k;
+    out.dtype = a.dtype;
+    out.ptype = a.ptype;
+    const uint64_t vbits = ((k + 31) / 32) * 4;
+    if (src.validity) {  // validity.filter(predicate)
+        if (!out.validity) VXG_TRY(hip_check(hipMalloc(&out.validity, vbits ? vbits : 4), "filter validity alloc"));
+        VXG_TRY(hip_check(hipMemsetAsync(out.validity, 0, vbits ? vbits : 4, s_), "filter validity memset"));
+        VXG_TRY(launch_filter_bits(m, n, to, static_cast<const uint8_t*>(src.validity), out.validity, s_));
+    } else {
+        out.validity = nullptr;
+    }
+    if (a.dtype == VXG_DTYPE_PRIMITIVE) {
+        out.values_bytes = k * width(a);
+        if (!out.values)
+            VXG_TRY(hip_check(hipMalloc(&out.values, out.values_bytes ? out.values_bytes : 16), "filter values alloc"));
+        return launch_filter_values(m, n, to, src.values, width(a), out.values, s_);
+    }
+    if (a.dtype == VXG_DTYPE_BOOL) {
+        out.values_bytes = vbits;
+        if (!out.values) VXG_TRY(hip_check(hipMalloc(&out.values, vbits ? vbits : 4), "filter bool alloc"));
+        VXG_TRY(hip_check(hipMemsetAsync(out.values, 0, vbits ? vbits : 4, s_), "filter bool memset"));
+        return launch_filter_bits(m, n, to, static_cast<const uint8_t*>(src.values), out.values, s_);
+    }
+    // strings: compact the views, then rebuild one heap of the selected rows
+    if (!out.views) VXG_TRY(hip_check(hipMalloc(&out.views, k ? 16 * k : 16), "filter views alloc"));
+    VXG_TRY(launch_filter_values(m, n, to, src.views, 16, out.views, s_));
+    const uint64_t ktiles = filter_tiles(k);
+    void* hoff;
+    VXG_TRY(temp((ktiles + 1) * 8, &hoff));
+    uint8_t* views = static_cast<uint8_t*>(out.views);
+    const uint8_t* valid = static_cast<const uint8_t*>(out.validity);
+    VXG_TRY(launch_view_heap_sizes(views, k, valid, static_cast<uint64_t*>(hoff), s_));
+    uint64_t heap = 0;
+    VXG_TRY(hip_check(hipMemcpyAsync(&heap, static_cast<uint64_t*>(hoff) + ktiles, 8, hipMemcpyDeviceToHost, s_),
+                      "filter heap readback"));
+    VXG_TRY(hip_check(hipStreamSynchronize(s_), "filter heap sync"));
+    if (heap > 0xFFFFFFFFull) return set_error(VXG_ERR_INVALID_ARGUMENT, "filtered string heap exceeds u32 view offsets");
+    if (out.data && out.data_bytes < heap)
+        return set_error(VXG_ERR_INVALID_ARGUMENT, "caller-provided data holds " + std::to_string(out.data_bytes) +
+                                                       " bytes, the filtered heap needs " + std::to_string(heap));
+    if (!out.data) VXG_TRY(hip_check(hipMalloc(&out.data, heap + 16), "filter heap alloc"));
+    out.data_bytes = heap;
+    out.n_data_buffers = 1;
+    if (out.data_buffers && out.data_buffers_cap >= 1) out.data_buffers[0] = vxg_data_buffer{0, heap};
+    std::vector<const uint8_t*> bases(bufs.size());
+    for (size_t i = 0; i < bufs.size(); ++i) bases[i] = static_cast<const uint8_t*>(src.data) + bufs[i].offset;
+    void* dbases;
+    VXG_TRY(temp(bases.size() * sizeof(void*) + 8, &dbases));
+    if (!bases.empty())
+        VXG_TRY(hip_check(hipMemcpyAsync(dbases, bases.data(), bases.size() * sizeof(void*), hipMemcpyHostToDevice, s_),
+                          "filter buffer table upload"));
+    VXG_TRY(launch_view_heap_build(views, k, valid, static_cast<uint64_t*>(hoff),
+                                   static_cast<const uint8_t* const*>(dbases), uint32_t(bases.size()),
+                                   static_cast<uint8_t*>(out.data), ctx_->c.err_word, s_));
+    return hip_check(hipStreamSynchronize(s_), "filter sync");  // `bases` is read by the upload
 }
 
 // ---- bools: canonical BoolArray = LSB bit buffer (bool/mod.rs), from every Bool encoding ----
@@ -1797,6 +1908,14 @@ vxg_status vxg_take_array(vxg_ctx* ctx, const vxg_array* a, int indices_ptype, c
     if (!ptype_is_int(indices_ptype)) return set_error(VXG_ERR_INVALID_ARGUMENT, "take indices must be integers");
     Planner p(ctx, S(stream));
     return p.take(*a, indices, ptype_width(indices_ptype), ptype_is_signed(indices_ptype), n_indices, *out);
+}
+
+vxg_status vxg_filter_array(vxg_ctx* ctx, const vxg_array* a, const vxg_array* predicate, vxg_canonical* out,
+                            void* stream) {
+    VXG_TRY(use_device(ctx));
+    if (!a || !predicate || !out) return set_error(VXG_ERR_INVALID_ARGUMENT, "null array/predicate/out");
+    Planner p(ctx, S(stream));
+    return p.filter(*a, *predicate, *out);
 }
 
 vxg_status vxg_runend_bool_decode(vxg_ctx* ctx, int ends_ptype, const void* ends, uint64_t n_runs, uint64_t offset,
