@@ -2,20 +2,25 @@
 
 Contract:
   python bench.py --gpus N --steps K --warmup W
-  * one process per GPU (torchrun for N>1; RCCL barrier + MAX over ranks of the timed region);
+  * one process per GPU over RCCL.  Run without torchrun and with N > 1, this script launches
+    `python -m torch.distributed.run --nproc-per-node N ... bench.py` as a CHILD before it
+    touches a GPU and exits with the child's status; every worker asserts WORLD_SIZE == N;
   * a "step" = one vxg_canonicalize (the drop-in C-ABI path) of one array whose buffers are
     already in HBM;
   * headline workload = BASELINE config C1 (FastLanes BitPacked u32, W=7, 64 Mi values) —
     the configuration the north-star target (>=70 % of HBM roofline) is quoted on; chunked
     arrays shard one chunk per GPU, so every rank decodes its own 64 Mi-value chunk
     (weak scaling, no data-path collective);
-  * `value` = decoded bytes written by ALL ranks / max-over-ranks time (GB/s);
+  * `value` = decoded bytes written by ALL ranks / max-over-ranks time (GB/s, whole job);
+    `value_per_gpu` = value / N;
   * `roofline` = algorithmic bytes (packed read + decoded write) per launch / mean kernel
     time from HIP events on the decode stream, against 8.0 TB/s;
   * `cpu_baseline` = the oracle (C restatement of the reference's single-threaded
-    canonicalize) on a bounded sample, rank 0 only;
-  * the other configs (C2 ALP f64, C3 Dict->BitPacked u64 chunk shard, C4 FSST, C5 the TPC-H
-    lineitem scan: 16 chunked columns, this rank's chunk range) are measured the same way and
+    canonicalize) on bounded samples of every config, rank 0 at N = 1 only: median of >= 20
+    repetitions, 1 core, and all cores chunk-parallel for the chunked configs (C3, C5);
+  * the other configs (C2 ALP f64; C3 the fixed 256-chunk Dict->BitPacked u64 table, split
+    over the ranks = strong scaling; C4 FSST; C5 the TPC-H lineitem scan: 16 chunked columns,
+    this rank's chunk range, read from a Vortex file's bytes) are measured the same way and
     reported under "encodings".
 Inputs are rotated across several HBM copies so every step reads from HBM, not from the
 256 MiB Infinity Cache.
@@ -26,6 +31,8 @@ import argparse
 import ctypes as C
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -37,6 +44,7 @@ sys.path.insert(0, str(ROOT))
 
 METRIC = "decoded GB/s/GPU (device-resident) per encoding; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+C3_CHUNKS, C3_CHUNK_VALUES = 256, (128 << 20) // 256  # BASELINE C3: 128 Mi values in 256 chunks
 
 
 def log(*a):
@@ -44,54 +52,37 @@ def log(*a):
 
 
 # ------------------------------------------------------------------------------ inputs
-def make_c1(rng):
-    """C1: 64 Mi u32 uniform in [0,128) -> BitPacked W=7, no patches."""
-    import vortex_amd.encode as E
-    vals = rng.integers(0, 128, 64 << 20, dtype=np.uint32)
-    return E.encode_bitpacked(vals, bit_width=7, allow_patches=False), dict(
-        name="C1", encoding="fastlanes.bitpacked u32 W=7", values=vals.size,
-        read_bytes=vals.size * 7 // 8, write_bytes=vals.nbytes, dtype="u32")
-
-
-def make_c2(rng):
-    """C2: 64 Mi f64 2-decimal prices + 0.1% random full-precision exceptions in the same
-    range (never 2-decimal, so always ALP patches) -> ALP->FoR->BitPacked(u64, W=24)."""
-    import vortex_amd.encode as E
-    n = 64 << 20
+def c2_values(rng, n):
+    """C2 data: 2-decimal prices + 0.1% random full-precision exceptions in the same range
+    (never 2-decimal, so always ALP patches)."""
     vals = np.round(rng.uniform(1, 100000, n) * 100) / 100
     k = n // 1000
     vals[rng.choice(n, k, replace=False)] = rng.uniform(1, 100000, k) + 1e-7
-    arr = E.encode_alp(vals)
-    return arr, dict(name="C2", encoding="vortex.alp(fastlanes.for(fastlanes.bitpacked u64)) f64",
-                     values=n, read_bytes=arr.nbytes(), write_bytes=vals.nbytes, dtype="f64")
+    return vals
 
 
-def make_c3_shard(rng, world: int, rank: int):
-    """C3: Chunked[Dict(codes=BitPacked u64 W=10, values=Primitive u64[1024])] with 512 Ki
-    values per chunk.  BASELINE's config is 256 chunks (128 Mi values) over 8 GPUs = 32 chunks
-    per GPU; to keep per-GPU work fixed as N grows (weak scaling) the global array has 32*N
-    chunks, and this rank decodes the contiguous chunk range vortex_amd.shard.plan_shards gives
-    it (balanced by compressed bytes).  Chunk c is generated from seed c, so every rank agrees
-    on the global array without communicating."""
+def c3_chunk(c: int):
+    """Chunk c of the C3 table (seeded by c so every rank agrees without communicating):
+    Dict(codes = BitPacked u64 W=10, values = 1024 random u64), Zipf(1.1) codes."""
     import vortex_amd.arrays as A
     import vortex_amd.encode as E
+    r = np.random.default_rng(1000 + c)
+    dv = r.integers(0, 2 ** 63, 1024, dtype=np.uint64)
+    codes = (r.zipf(1.1, C3_CHUNK_VALUES) - 1) % 1024
+    return A.dict_array(A.primitive(dv), A.bitpacked(E.bitpack_buffer(codes.astype(np.uint64), 10), "u64", 10,
+                                                     C3_CHUNK_VALUES))
+
+
+def c3_shard(world: int, rank: int) -> range:
     from vortex_amd.shard import plan_shards
-    per_chunk = (128 << 20) // 256
-    n_global = 32 * world
-    packed_bytes = (per_chunk // 1024) * 128 * 10 + 1024 * 8
-    mine = plan_shards([packed_bytes] * n_global, world)[rank]
-    chunks = []
-    for c in mine:
-        r = np.random.default_rng(1000 + c)
-        dv = r.integers(0, 2 ** 63, 1024, dtype=np.uint64)
-        codes = (r.zipf(1.1, per_chunk) - 1) % 1024
-        chunks.append(A.dict_array(A.primitive(dv),
-                                   A.bitpacked(E.bitpack_buffer(codes.astype(np.uint64), 10), "u64", 10, per_chunk)))
-    arr = A.chunked(chunks)
-    return arr, dict(name="C3", encoding="vortex.chunked[vortex.dict(codes=fastlanes.bitpacked u64 W=10)] u64",
-                     values=len(mine) * per_chunk, read_bytes=arr.nbytes() - 8 * (len(mine) + 1),
-                     write_bytes=len(mine) * per_chunk * 8, dtype="u64", chunks_per_gpu=len(mine),
-                     chunk_range=[mine.start, mine.stop], global_chunks=n_global)
+    packed_bytes = (C3_CHUNK_VALUES // 1024) * 128 * 10 + 1024 * 8
+    return plan_shards([packed_bytes] * C3_CHUNKS, world)[rank]
+
+
+def c5_shard(world: int, rank: int) -> range:
+    from tools import lineitem as L
+    from vortex_amd.shard import plan_shards
+    return plan_shards([1] * L.n_chunks(), world)[rank]
 
 
 WORDS = (b"furiously regular deposits sleep carefully final accounts ironic packages blithely "
@@ -100,12 +91,9 @@ WORDS = (b"furiously regular deposits sleep carefully final accounts ironic pack
          b"daring ideas close courts blithe dolphins quiet excuses ruthless warthogs").split()
 
 
-def make_c4(rng):
-    """C4: 6 001 215 synthetic TPC-H l_comment strings (10..43 chars cut from a word stream;
-    dbgen is unavailable offline) -> FSST (codes VarBin i32 offsets FoR/BitPacked, lengths
-    FoR/BitPacked)."""
-    import vortex_amd.encode as E
-    n = 6_001_215
+def c4_heap(rng, n):
+    """n synthetic TPC-H l_comment strings (10..43 chars cut from a word stream; dbgen is
+    unavailable offline) -> (heap u8, offsets i64[n+1])."""
     lens = rng.integers(10, 44, n)
     total = int(lens.sum())
     wl = np.array([len(w) + 1 for w in WORDS])
@@ -120,23 +108,60 @@ def make_c4(rng):
     stream = rows[keep][:total]
     offs = np.zeros(n + 1, np.int64)
     np.cumsum(lens, out=offs[1:])
-    arr = E.encode_fsst_from_heap(stream, offs)
+    return stream, offs
+
+
+def make_c1(rng, world, rank):
+    """C1: 64 Mi u32 uniform in [0,128) -> BitPacked W=7, no patches (one chunk per GPU)."""
+    import vortex_amd.encode as E
+    vals = rng.integers(0, 128, 64 << 20, dtype=np.uint32)
+    return E.encode_bitpacked(vals, bit_width=7, allow_patches=False), dict(
+        name="C1", encoding="fastlanes.bitpacked u32 W=7", values=vals.size,
+        read_bytes=vals.size * 7 // 8, write_bytes=vals.nbytes, dtype="u32")
+
+
+def make_c2(rng, world, rank):
+    """C2: 64 Mi f64 prices -> ALP->FoR->BitPacked(u64, W=24) + Sparse patches (one chunk per GPU)."""
+    import vortex_amd.encode as E
+    n = 64 << 20
+    arr = E.encode_alp(c2_values(rng, n))
+    return arr, dict(name="C2", encoding="vortex.alp(fastlanes.for(fastlanes.bitpacked u64)) f64",
+                     values=n, read_bytes=arr.nbytes(), write_bytes=n * 8, dtype="f64")
+
+
+def make_c3(rng, world, rank):
+    """C3: BASELINE's fixed table, Chunked x256 [Dict(codes=BitPacked u64 W=10, values=Primitive
+    u64[1024])], 512 Ki values per chunk = 128 Mi values.  The table is the same at every N
+    (strong scaling): this rank decodes the contiguous chunk range vortex_amd.shard.plan_shards
+    gives it (balanced by compressed bytes; chunk_offsets, chunked/mod.rs:54-70), all 256 at N=1."""
+    import vortex_amd.arrays as A
+    mine = c3_shard(world, rank)
+    arr = A.chunked([c3_chunk(c) for c in mine])
+    return arr, dict(name="C3", encoding="vortex.chunked[vortex.dict(codes=fastlanes.bitpacked u64 W=10)] u64",
+                     values=len(mine) * C3_CHUNK_VALUES, read_bytes=arr.nbytes() - 8 * (len(mine) + 1),
+                     write_bytes=len(mine) * C3_CHUNK_VALUES * 8, dtype="u64", chunks_per_gpu=len(mine),
+                     chunk_range=[mine.start, mine.stop], global_chunks=C3_CHUNKS, strong_scaling=True)
+
+
+def make_c4(rng, world, rank):
+    """C4: 6 001 215 synthetic l_comment strings -> FSST (codes VarBin i32 offsets FoR/BitPacked,
+    lengths FoR/BitPacked); one column per GPU (replicas)."""
+    import vortex_amd.encode as E
+    n = 6_001_215
+    heap, offs = c4_heap(rng, n)
+    arr = E.encode_fsst_from_heap(heap, offs)
     return arr, dict(name="C4", encoding="vortex.fsst utf8 -> varbinview", values=n,
-                     read_bytes=arr.nbytes(), write_bytes=total + 16 * n, dtype="u8")
+                     read_bytes=arr.nbytes(), write_bytes=int(offs[-1]) + 16 * n, dtype="u8")
 
 
-def make_c5_shard(rng, world: int, rank: int):
+def make_c5(rng, world, rank):
     """C5: bench-vortex's TPC-H lineitem scan -> canonicalize (tools/lineitem.py): SF1's 6 001 215
     rows, 16 columns, each a ChunkedArray of 64 Ki-row chunks compressed with the sampling
     compressor's cascades.  The table is fixed (strong scaling): the 92 chunks are split into
     contiguous ranges, one per rank, and a step canonicalizes every column of this rank's range
-    (struct_to_arrow, canonical.rs:169-187: one canonicalize per field).  The reference reads
-    the table from a Vortex file (vortex-serde); the file reader is out of this round's scope,
-    so the columns start in HBM like the other configs."""
+    (struct_to_arrow, canonical.rs:169-187: one canonicalize per field)."""
     from tools import lineitem as L
-    from vortex_amd.shard import plan_shards
-    nch = L.n_chunks()
-    mine = plan_shards([1] * nch, world)[rank]
+    mine = c5_shard(world, rank)
     cols, plain = L.lineitem_columns(mine)
     rows = sum(len(v) for v in plain["l_orderkey"])
     write = sum(L.canonical_bytes(v) for vs in plain.values() for v in vs)
@@ -144,7 +169,7 @@ def make_c5_shard(rng, world: int, rank: int):
     return [cols[name] for name, _ in L.COLUMNS], dict(
         name="C5", encoding="lineitem scan: 16 x vortex.chunked[<per-column cascades>] -> canonical",
         values=rows, read_bytes=read, write_bytes=write, dtype="mixed", chunks_per_gpu=len(mine),
-        chunk_range=[mine.start, mine.stop], global_chunks=nch, strong_scaling=True)
+        chunk_range=[mine.start, mine.stop], global_chunks=L.n_chunks(), strong_scaling=True)
 
 
 # ------------------------------------------------------------------------------ timing
@@ -169,26 +194,7 @@ class Workload:
             self.cols = []
             for j, arr in enumerate(arrs):
                 nodes = [A.flatten(trees[j], self.keep) for trees in self.copies]
-                vb, db, nb = C.c_uint64(), C.c_uint64(), C.c_uint32()
-                table = (A._lib.VxgDataBuffer * 4096)()
-                chk(ctx.lib.vxg_canonical_layout(ctx.handle, C.byref(nodes[0]), C.byref(vb), C.byref(db), table,
-                                                 4096, C.byref(nb)))
-                out = A._lib.VxgCanonical()
-                if arr.dtype == A.DTYPE["PRIMITIVE"]:
-                    vals = torch.empty(max(vb.value, 16), dtype=torch.uint8, device=dev)
-                    out.values = vals.data_ptr()
-                    self.keep.append(vals)
-                else:
-                    views = torch.empty(max(vb.value, 16), dtype=torch.uint8, device=dev)
-                    data = torch.empty(db.value + 16, dtype=torch.uint8, device=dev)
-                    out.views, out.data, out.data_bytes = views.data_ptr(), data.data_ptr(), db.value
-                    out.data_buffers, out.n_data_buffers, out.data_buffers_cap = table, nb.value, 4096
-                    self.keep += [views, data, table]
-                if arr.nullable:
-                    vt = torch.empty(((arr.len + 31) // 32) * 4 + 4, dtype=torch.uint8, device=dev)
-                    out.validity = vt.data_ptr()
-                    self.keep.append(vt)
-                self.cols.append((nodes, out))
+                self.cols.append((nodes, A.alloc_canonical(ctx, nodes[0], self.keep)[0]))
         self.i = 0
 
     def step(self):
@@ -211,35 +217,37 @@ def chk(st):
     _lib.check(st)
 
 
-def run_workload(wl: Workload, steps: int, warmup: int, dist, rank: int):
-    """Warmup, then exactly `steps` back-to-back steps between barrier + synchronize.  Two HIP
-    events on the decode stream (torch's current stream, the stream vxg_canonicalize is given)
-    bracket the timed steps: (e1 - e0) / steps is the device time per step (per launch for a
-    one-kernel step like C1) without per-step event gaps."""
+def run_workload(wl, steps: int, warmup: int, dist):
+    """Warmup, then exactly `steps` back-to-back steps between barrier + synchronize.  HIP events
+    on the decode stream (torch's current stream, the stream the engine is given) bracket every
+    step: (last - first) / steps is the mean device time per step (per launch for a one-kernel
+    step like C1), and the per-step differences give the median."""
     import torch
     for _ in range(warmup):
         wl.step()
     wl.ctx.sync()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    e0.record()
+    evs[0].record()
     for s in range(steps):
         wl.step()
-    e1.record()
+        evs[s + 1].record()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     wl.ctx.sync()  # surfaces device-side errors (OOB codes, ...)
-    kms = e0.elapsed_time(e1) / steps
+    per = [evs[i].elapsed_time(evs[i + 1]) for i in range(steps)]
+    kmean = evs[0].elapsed_time(evs[-1]) / steps
+    kmed = float(np.median(per))
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    return elapsed, kms, kms
+    return elapsed, kmean, kmed
 
 
 def run_e2e(arr, info, ctx, reps: int = 5):
@@ -303,7 +311,8 @@ def run_e2e(arr, info, ctx, reps: int = 5):
 def pmc_traffic(name: str):
     """Per-launch HBM bytes of the dominant kernel from committed rocprofv3 PMC summaries
     (profiles/pmc_traffic.json, written by tools/pmc_traffic.py: FETCH_SIZE*2 + WRITE_SIZE,
-    KiB -> bytes, gfx950 read correction per MI355X_MICROARCH.md §HBM)."""
+    KiB -> bytes, gfx950 read correction per MI355X_MICROARCH.md §HBM).  Not measured by this
+    run: the PMC passes need their own rocprofv3 runs (see `roofline.traffic_source`)."""
     p = ROOT / "profiles" / "pmc_traffic.json"
     if not p.exists():
         return None
@@ -314,28 +323,153 @@ def pmc_traffic(name: str):
         return None
 
 
-def cpu_baseline(budget_s: float):
-    """Oracle ("port") C1 decode on one host core: vxo_unpack over the full 64 Mi array, in
-    the reference's structure (per-1024 block unpack, single thread), repeated for ~budget."""
+# ------------------------------------------------------------------------------ CPU baseline
+def _cpu_cores() -> int:
+    """Host cores this process may use (the GPU box's share is 16 per GPU; the affinity mask
+    may show the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(n, 16))
+
+
+_POOL_ITEMS: list = []
+
+
+def _pool_decode(idxs):
+    """Worker: canonicalize the given items through the oracle; returns decoded bytes."""
+    from oracle_tree import canon
+    tot = 0
+    for i in idxs:
+        for a in _POOL_ITEMS[i]:
+            v, _ = canon(a)
+            tot += v.nbytes if hasattr(v, "nbytes") else 0
+    return tot
+
+
+def _median_time(fn, reps: int, budget_s: float):
+    ts = []
+    t_start = time.perf_counter()
+    for r in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+        if r >= 4 and time.perf_counter() - t_start > budget_s:
+            break
+    return float(np.median(ts)), len(ts)
+
+
+def cpu_baselines(budget_s: float, reps: int = 20) -> dict:
+    """The oracle ("port": the reference is Rust and cannot be built here) timed on this box's
+    host cores, in the reference's structure (per-block unpack, one materialised buffer per
+    cascade level, serial pack_primitives; fresh outputs like the reference allocates per call),
+    median of `reps` repetitions on a bounded sample of each config.  C1 is also timed with a
+    pre-faulted output.  The chunked configs (C3, C5) are also timed chunk-parallel over all
+    cores (fork pool; each worker canonicalizes whole chunks, outputs stay in the worker).
+    Runs before anything touches the GPU, so the pool forks a GPU-free process."""
+    import multiprocessing as mp
+    sys.path.insert(0, str(ROOT / "tests"))
     from oracle import oracle as O
-    L = O.lib()
+    from oracle_tree import canon
+    import vortex_amd.encode as E
+    from tools import lineitem as L
+    cores = _cpu_cores()
+    per_budget = budget_s / 7
+    out = {"nproc": os.cpu_count(), "cores_all": cores, "reps": reps, "kind": "port"}
+    Lb = O.lib()
+    # C1 full array, 1 core
     rng = np.random.default_rng(42)
     vals = rng.integers(0, 128, 64 << 20, dtype=np.uint32)
     packed = np.zeros((vals.size // 1024) * 128 * 7, np.uint8)
-    L.vxo_bitpack(O.PT["u32"], 7, O.p(vals), vals.size, O.p(packed))
-    reps, t = 0, 0.0
-    while t < budget_s:
-        out = np.empty_like(vals)  # the reference allocates its output per call
-        t0 = time.perf_counter()
-        rc = L.vxo_unpack(O.PT["u32"], 7, 0, vals.size, O.p(packed), packed.size, O.p(out))
-        t += time.perf_counter() - t0
-        reps += 1
-        assert rc == 0
-    assert np.array_equal(out, vals)
-    gbs = reps * vals.nbytes / t / 1e9
-    return {"value": round(gbs, 3), "unit": "GB/s", "cores": 1, "kind": "port",
-            "sample": f"C1 full array (64 Mi u32, W=7) decoded {reps}x by oracle/vx_oracle.c vxo_unpack "
-                      f"(-O3 -march=native), fresh output per call; {t:.1f}s of CPU time"}
+    Lb.vxo_bitpack(O.PT["u32"], 7, O.p(vals), vals.size, O.p(packed))
+    pre = np.empty_like(vals)
+    pre.fill(1)
+
+    def c1(fresh):
+        o = np.empty_like(vals) if fresh else pre
+        assert Lb.vxo_unpack(O.PT["u32"], 7, 0, vals.size, O.p(packed), packed.size, O.p(o)) == 0
+    t_fresh, n1 = _median_time(lambda: c1(True), reps, per_budget)
+    t_pre, _ = _median_time(lambda: c1(False), reps, per_budget)
+    assert np.array_equal(pre, vals)
+    out["C1"] = {"sample": "full C1 (64 Mi u32 W=7)", "1core_GBps": round(vals.nbytes / t_fresh / 1e9, 3),
+                 "1core_prefaulted_GBps": round(vals.nbytes / t_pre / 1e9, 3), "reps": n1}
+    # C2: 8 Mi values of the C2 distribution
+    n2 = 8 << 20
+    a2 = E.encode_alp(c2_values(np.random.default_rng(43), n2))
+    t2, r2 = _median_time(lambda: canon(a2), reps, per_budget)
+    out["C2"] = {"sample": "8 Mi f64 of the C2 distribution, ALP->FoR->BitPacked + patches",
+                 "1core_GBps": round(n2 * 8 / t2 / 1e9, 3), "reps": r2}
+    # C3: 16 of the 256 chunks (8 Mi values)
+    c3 = [[c3_chunk(c)] for c in range(16)]
+    # C4: 1 Mi strings
+    heap, offs = c4_heap(np.random.default_rng(44), 1 << 20)
+    a4 = E.encode_fsst_from_heap(heap, offs)
+    t4, r4 = _median_time(lambda: canon(a4), reps, per_budget)
+    out["C4"] = {"sample": "1 Mi synthetic l_comment strings, FSST",
+                 "1core_GBps": round((int(offs[-1]) + 16 * (1 << 20)) / t4 / 1e9, 3), "reps": r4}
+    # C5: 8 of the 92 lineitem chunks x 16 columns
+    cols, plain = L.lineitem_columns(range(8))
+    c5 = [[cols[name].children[1 + i] for name, _ in L.COLUMNS] for i in range(8)]
+    c5_bytes = sum(L.canonical_bytes(v) for vs in plain.values() for v in vs)
+    c3_bytes = 16 * C3_CHUNK_VALUES * 8
+    global _POOL_ITEMS
+    for key, items, nbytes, sample in (("C3", c3, c3_bytes, "16 of the 256 C3 chunks (8 Mi u64)"),
+                                       ("C5", c5, c5_bytes, "8 of the 92 lineitem chunks x 16 columns")):
+        _POOL_ITEMS = items
+        t1, r1 = _median_time(lambda: _pool_decode(range(len(items))), reps, per_budget)
+        ent = {"sample": sample, "1core_GBps": round(nbytes / t1 / 1e9, 3), "reps": r1}
+        if cores > 1:
+            ctx = mp.get_context("fork")
+            with ctx.Pool(min(cores, len(items))) as pool:
+                parts = [list(range(i, len(items), cores)) for i in range(min(cores, len(items)))]
+                pool.map(_pool_decode, parts)  # warm the workers
+                tp, rp = _median_time(lambda: pool.map(_pool_decode, parts), reps, per_budget)
+            ent.update({"all_core_GBps": round(nbytes / tp / 1e9, 3), "all_core_reps": rp,
+                        "cores": min(cores, len(items))})
+        out[key] = ent
+    _POOL_ITEMS = []
+    return out
+
+
+# ------------------------------------------------------------------------------ launch
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_workers(n: int) -> int:
+    """`--gpus N` without torchrun: start N workers through torch.distributed.run as a child
+    process (nothing here has touched a GPU) and return its exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", str(ROOT / "bench.py")] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    log(f"[bench] launching {n} workers: {' '.join(cmd)}")
+    return subprocess.call(cmd, env=env)
+
+
+def launcher_selftest(world: int, rank: int) -> None:
+    """--launcher-selftest (CPU, gloo): every worker reports its rank and the C3/C5 chunk ranges
+    it would decode; rank 0 gathers them and prints one JSON line."""
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    assert dist.get_world_size() == world and dist.get_rank() == rank
+    mine = [rank, world, c3_shard(world, rank).start, c3_shard(world, rank).stop,
+            c5_shard(world, rank).start, c5_shard(world, rank).stop]
+    parts = [torch.zeros(6, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(parts, torch.tensor(mine, dtype=torch.int64))
+    t = torch.tensor([float(rank)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"selftest": True, "world": world, "max_rank": t.item(),
+                          "ranks": [p.tolist() for p in parts]}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
 
 
 def main():
@@ -345,7 +479,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--workloads", default="c1,c2,c3,c4,c5",
                     help="comma list; c1 is the headline, others go under 'encodings'")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true",
                     help="call vxg_canonicalize per array per step instead of replaying a vxg_plan graph")
@@ -353,19 +487,36 @@ def main():
                     help="diagnostic: with one process, build rank 0's shard of an N-GPU run of C3/C5")
     ap.add_argument("--e2e", action="store_true",
                     help="also measure host->host (H2D + decode + D2H over PCIe); never the headline value")
+    ap.add_argument("--launcher-selftest", action="store_true",
+                    help="CPU check of the multi-process launch (gloo): print every rank's chunk ranges")
     args = ap.parse_args()
 
-    import torch
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_workers(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world and world != 1:
-        log(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.gpus != world:
+        log(f"[bench] error: --gpus {args.gpus} but WORLD_SIZE={world}")
+        sys.exit(2)
+    if args.launcher_selftest:
+        launcher_selftest(world, rank)
+        return
+
+    # the CPU baseline runs first: its fork pool must not inherit an initialised GPU runtime
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        t0 = time.perf_counter()
+        cpu = cpu_baselines(args.cpu_seconds)
+        log(f"[bench] cpu baseline: {time.perf_counter() - t0:.1f}s")
+
+    import torch
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist  # noqa: F811
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        assert dist.get_world_size() == args.gpus
 
     import vortex_amd as V
     ctx = V.Context(local)
@@ -373,13 +524,13 @@ def main():
     # --simulate-world N (diagnostic, single process): rank 0's shard of an N-GPU run of the
     # sharded configs, to read one GPU's share of the N-GPU work before an N-GPU node is used
     shard_world = args.simulate_world if args.simulate_world and world == 1 else world
-    makers = {"c1": make_c1, "c2": make_c2, "c3": lambda r: make_c3_shard(r, shard_world, rank), "c4": make_c4,
-              "c5": lambda r: make_c5_shard(r, shard_world, rank)}
-    copies = {"c1": 4, "c2": 1, "c3": 2, "c4": 1, "c5": 1}
+    makers = {"c1": make_c1, "c2": make_c2, "c3": make_c3, "c4": make_c4, "c5": make_c5}
+    # C1: 8 rotated copies of its 58.7 MB input = 470 MB > the 256 MiB Infinity Cache
+    copies = {"c1": 8, "c2": 1, "c3": 1, "c4": 1, "c5": 1}
     results = {}
     for key in [w.strip() for w in args.workloads.split(",") if w.strip()]:
         t0 = time.perf_counter()
-        arr, info = makers[key](rng)
+        arr, info = makers[key](rng, shard_world, rank)
         e2e = run_e2e(arr, info, ctx) if args.e2e and not isinstance(arr, list) else None
         # one-array steps are one or two back-to-back kernel launches: direct calls overlap the
         # next submission with the running kernel (a graph replay measured 2-6 us slower per
@@ -389,7 +540,7 @@ def main():
         if rank == 0:
             log(f"[bench] {info['name']}: built in {time.perf_counter() - t0:.1f}s; timing...")
         steps = args.steps if key == "c1" else max(3, args.steps // 2)
-        elapsed, kmean, kmed = run_workload(wl, steps, args.warmup if key == "c1" else 2, dist, rank)
+        elapsed, kmean, kmed = run_workload(wl, steps, args.warmup if key == "c1" else 2, dist)
         per_step = elapsed / steps
         algo = info["read_bytes"] + info["write_bytes"]
         total_write = world * info["write_bytes"]
@@ -413,6 +564,8 @@ def main():
             "metric": METRIC,
             "value": round(h["value"], 2),
             "unit": "GB/s",
+            "value_per_gpu": round(h["value"] / world, 2),
+            "value_aggregate": round(h["value"], 2),
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -430,23 +583,41 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": pmc_traffic("fl_unpack_u32_w7") if head_key == "c1" else None,
+                         "traffic_source": "profiles/pmc_traffic.json (committed rocprofv3 --pmc FETCH_SIZE / "
+                                           "WRITE_SIZE passes of this workload; not this run)",
                          "kernel_ms_mean": round(h["kernel_ms_mean"], 5),
+                         "kernel_ms_median": round(h["kernel_ms_median"], 5),
                          "algorithmic_bytes_per_launch": h["algo_bytes"]},
             "encodings": {},
         }
         for k, r in results.items():
             i = r["info"]
-            line["encodings"][i["name"]] = {
+            ent = {
                 "encoding": i["encoding"], "values_per_gpu": i["values"],
+                "scaling": "strong" if i.get("strong_scaling") else "weak",
                 "decoded_GBps_total": round(r["value"], 2),
+                "decoded_GBps_per_gpu": round(r["value"] / world, 2),
                 "decoded_GBps_per_gpu_kernel": round(i["write_bytes"] / (r["kernel_ms_mean"] / 1e3) / 1e9, 1),
                 "hbm_frac_algorithmic": round(r["algo_bytes"] / (r["kernel_ms_mean"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
-                "kernel_ms_mean": round(r["kernel_ms_mean"], 5), "ms_per_step": round(r["ms_per_step"], 5),
+                "kernel_ms_mean": round(r["kernel_ms_mean"], 5), "kernel_ms_median": round(r["kernel_ms_median"], 5),
+                "ms_per_step": round(r["ms_per_step"], 5),
                 "read_bytes": i["read_bytes"], "write_bytes": i["write_bytes"]}
+            for extra in ("chunks_per_gpu", "chunk_range", "global_chunks"):
+                if extra in i:
+                    ent[extra] = i[extra]
+            if cpu is not None and i["name"] in cpu:
+                ent["cpu_baseline"] = cpu[i["name"]]
             if r.get("e2e"):
-                line["encodings"][i["name"]]["host_to_host"] = r["e2e"]
-        if not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+                ent["host_to_host"] = r["e2e"]
+            line["encodings"][i["name"]] = ent
+        if cpu is not None:
+            c1 = cpu["C1"]
+            line["cpu_baseline"] = {
+                "value": c1["1core_GBps"], "unit": "GB/s", "cores": 1, "kind": "port",
+                "sample": f"C1 full array (64 Mi u32, W=7) decoded by oracle/vx_oracle.c vxo_unpack (-O3 "
+                          f"-march=native), fresh output per call, median of {c1['reps']} reps "
+                          f"(pre-faulted output: {c1['1core_prefaulted_GBps']} GB/s); nproc={cpu['nproc']}; "
+                          f"C2-C5 (1 core, and all {cpu['cores_all']} cores for C3/C5) under encodings.*.cpu_baseline"}
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.barrier()

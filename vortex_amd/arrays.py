@@ -659,46 +659,63 @@ def filter(a: Array, predicate: Array, ctx: Context) -> Canonical:
     return res
 
 
+def _kind_of_node(node: _lib.VxgArray) -> str:
+    return {DTYPE["PRIMITIVE"]: "primitive", DTYPE["BOOL"]: "bool"}.get(node.dtype, "varbinview")
+
+
+def alloc_canonical(ctx: Context, node: _lib.VxgArray, keep: list, table_cap: int = 4096):
+    """Caller-allocated canonical output for the flattened array `node` (vxg_canonical_layout:
+    values, or views + data + the per-chunk data-buffer table, and a validity bitmap when the
+    dtype is nullable) -> (VxgCanonical, Canonical of device tensors).  Everything the output
+    references is appended to `keep`."""
+    import torch
+    dev = torch.device("cuda", ctx.device)
+    vb, db, nb = C.c_uint64(), C.c_uint64(), C.c_uint32()
+    table = (_lib.VxgDataBuffer * table_cap)()
+    _lib.check(ctx.lib.vxg_canonical_layout(ctx.handle, C.byref(node), C.byref(vb), C.byref(db), table,
+                                            table_cap, C.byref(nb)))
+    n = int(node.len)
+    res = Canonical(_kind_of_node(node), n, PTYPES[node.ptype])
+    o = _lib.VxgCanonical()
+    if node.dtype in (DTYPE["PRIMITIVE"], DTYPE["BOOL"]):
+        vals = torch.empty(max(vb.value, 16), dtype=torch.uint8, device=dev)
+        o.values = vals.data_ptr()
+        res.values = vals[: vb.value]
+    else:
+        views = torch.empty(max(vb.value, 16), dtype=torch.uint8, device=dev)
+        data = torch.empty(db.value + 16, dtype=torch.uint8, device=dev)
+        o.views, o.data, o.data_bytes = views.data_ptr(), data.data_ptr(), db.value
+        o.data_buffers, o.n_data_buffers, o.data_buffers_cap = table, nb.value, table_cap
+        res.views, res.data = views[: vb.value], data[: db.value]
+        res.data_buffers = [(int(table[k].offset), int(table[k].len)) for k in range(nb.value)]
+        keep.append(table)
+    if node.nullable:
+        vt = torch.empty(((n + 31) // 32) * 4 + 4, dtype=torch.uint8, device=dev)
+        o.validity = vt.data_ptr()
+        res.validity = vt[: (n + 7) // 8]
+    keep.append(res)
+    return o, res
+
+
 class Plan:
     """vxg_plan: the launches of canonicalizing `arrays` into preallocated outputs, recorded
     once as a HIP graph and replayed by launch() (one hipGraphLaunch; every kernel runs on
     every replay).  Outputs are allocated here with vxg_canonical_layout and exposed as
-    Canonical objects; the device arrays must stay alive (and in place) with the plan."""
+    Canonical objects; the device arrays must stay alive (and in place) with the plan.
+    `arrays` are Array trees (device buffers) or already-flattened VxgArray nodes (e.g. the
+    trees a vxg_file reader built over a file's bytes in HBM)."""
 
-    def __init__(self, arrays: Sequence[Array], ctx: Context):
-        import torch
+    def __init__(self, arrays: Sequence, ctx: Context):
         self.ctx = ctx
         self.keep: list = []
-        dev = torch.device("cuda", ctx.device)
         n = len(arrays)
         self.nodes = (_lib.VxgArray * max(n, 1))()
         self.outs = (_lib.VxgCanonical * max(n, 1))()
         self.results = []
         for i, a in enumerate(arrays):
-            self.nodes[i] = flatten(a, self.keep)
-            vb, db, nb = C.c_uint64(), C.c_uint64(), C.c_uint32()
-            table = (_lib.VxgDataBuffer * 4096)()
-            _lib.check(ctx.lib.vxg_canonical_layout(ctx.handle, C.byref(self.nodes[i]), C.byref(vb), C.byref(db),
-                                                    table, 4096, C.byref(nb)))
-            res = Canonical(_kind(a), a.len, a.ptype)
-            o = self.outs[i]
-            if a.dtype in (DTYPE["PRIMITIVE"], DTYPE["BOOL"]):
-                vals = torch.empty(max(vb.value, 16), dtype=torch.uint8, device=dev)
-                o.values = vals.data_ptr()
-                res.values = vals[: vb.value]
-            else:
-                views = torch.empty(max(vb.value, 16), dtype=torch.uint8, device=dev)
-                data = torch.empty(db.value + 16, dtype=torch.uint8, device=dev)
-                o.views, o.data, o.data_bytes = views.data_ptr(), data.data_ptr(), db.value
-                o.data_buffers, o.n_data_buffers, o.data_buffers_cap = table, nb.value, 4096
-                res.views, res.data = views[: vb.value], data[: db.value]
-                res.data_buffers = [(int(table[k].offset), int(table[k].len)) for k in range(nb.value)]
-                self.keep.append(table)
-            if a.nullable:
-                vt = torch.empty(((a.len + 31) // 32) * 4 + 4, dtype=torch.uint8, device=dev)
-                o.validity = vt.data_ptr()
-                res.validity = vt[: (a.len + 7) // 8]
-            self.keep.append(res)
+            self.nodes[i] = a if isinstance(a, _lib.VxgArray) else flatten(a, self.keep)
+            o, res = alloc_canonical(ctx, self.nodes[i], self.keep)
+            self.outs[i] = o
             self.results.append(res)
         h = C.c_void_p()
         _lib.check(ctx.lib.vxg_plan_create(ctx.handle, self.nodes, self.outs, n, C.byref(h)))
