@@ -1,12 +1,14 @@
 // ubench_k1.hip — A/B variants of the FastLanes unpack kernel on the C1 shape
 // (u32, W=7, 64 Mi values), timed interleaved in one process (cdna_hip_programming.md §5.4
-// rule 24).  Build: hipcc --offload-arch=gfx950 -O3 -std=c++20 -I../vortex_amd/csrc
-//                   tools/ubench_k1.hip -o tools/ubench_k1
+// rule 24).  Inputs rotate over 8 copies (470 MB > the 256 MiB Infinity Cache) so every launch
+// reads HBM; `./ubench_k1 flush` also writes a 512 MiB buffer between timed launches.
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++20 tools/ubench_k1.hip -o tools/ubench_k1
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "../vortex_amd/csrc/fl_unpack_impl.hpp"
@@ -21,6 +23,7 @@ using namespace vxg;
 
 constexpr int T = 32, W = 7;
 
+// the engine's K1 path today: 32 blocks per 256-thread workgroup, one block per 8 threads
 template <int NT>
 __global__ __launch_bounds__(256) void k_base(const uint8_t* __restrict__ packed, uint32_t* __restrict__ out,
                                               uint64_t n_blocks) {
@@ -32,39 +35,175 @@ __global__ __launch_bounds__(256) void k_base(const uint8_t* __restrict__ packed
                                           n_blocks * 1024, ep);
 }
 
-// persistent grid-stride: each 8-thread group walks blocks g, g+G, ...
+// persistent + software-pipelined: each 8-thread group walks blocks g, g+G, ...; the next
+// block's packed words are loaded BEFORE the current block's 32 stores are issued, so every
+// wave keeps HBM reads in flight while it writes.
 template <int NT>
-__global__ __launch_bounds__(256) void k_stride(const uint8_t* __restrict__ packed, uint32_t* __restrict__ out,
-                                                uint64_t n_blocks) {
-    const uint64_t gid = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    const uint64_t groups = uint64_t(gridDim.x) * blockDim.x / 8;
-    EpiParams ep{};
-    for (uint64_t blk = gid >> 3; blk < n_blocks; blk += groups)
-        unpack_block<T, W, Epi::Plain, 0, NT>(packed + blk * (128 * W), int(gid & 7), out, int64_t(blk * 1024),
-                                              true, n_blocks * 1024, ep);
-}
-
-// block-major within the workgroup: 256 threads = 32 consecutive blocks, but thread t's slice
-// and block are swapped so a wave's 64 lanes cover 8 slices x 8 blocks (same as base) — kept as
-// the control; plus a 2-blocks-per-group variant that issues both blocks' loads up front.
-template <int NT>
-__global__ __launch_bounds__(256) void k_two(const uint8_t* __restrict__ packed, uint32_t* __restrict__ out,
-                                             uint64_t n_blocks) {
-    const uint64_t gid = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    const uint64_t blk0 = (gid >> 3) * 2;
-    const int t = int(gid & 7);
-    if (blk0 >= n_blocks) return;
-    Vec16<T> p0[W], p1[W];
+__global__ __launch_bounds__(256) void k_pipe(const uint8_t* __restrict__ packed, uint32_t* __restrict__ out,
+                                              uint64_t n_blocks) {
+    const int t = int(threadIdx.x & 7);
+    const uint64_t ngrp = uint64_t(gridDim.x) * 32;
+    uint64_t blk = (uint64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 3;
+    if (blk >= n_blocks) return;
+    Vec16<T> cur[W], nxt[W];
 #pragma unroll
-    for (int w = 0; w < W; w++) p0[w] = load16<T>(packed + blk0 * (128 * W) + 128 * w + 16 * t);
-#pragma unroll
-    for (int w = 0; w < W; w++) p1[w] = load16<T>(packed + (blk0 + 1) * (128 * W) + 128 * w + 16 * t);
+    for (int w = 0; w < W; w++) cur[w] = load16<T>(packed + blk * (128 * W) + 128 * w + 16 * t);
     EpiParams ep{};
     bool oob = false;
-    process_rows<T, W, Epi::Plain, 0, NT, true>(p0, t * 4, out, int64_t(blk0 * 1024), n_blocks * 1024, ep, oob,
-                                          std::make_integer_sequence<int, T>{});
-    process_rows<T, W, Epi::Plain, 0, NT, true>(p1, t * 4, out, int64_t((blk0 + 1) * 1024), n_blocks * 1024, ep, oob,
-                                          std::make_integer_sequence<int, T>{});
+    for (;;) {
+        const uint64_t nb = blk + ngrp;
+        const bool more = nb < n_blocks;
+        if (more) {
+#pragma unroll
+            for (int w = 0; w < W; w++) nxt[w] = load16<T>(packed + nb * (128 * W) + 128 * w + 16 * t);
+        }
+        process_rows<T, W, Epi::Plain, 0, NT, true>(cur, t * 4, out, int64_t(blk * 1024), n_blocks * 1024, ep, oob,
+                                                    std::make_integer_sequence<int, T>{});
+        if (!more) break;
+#pragma unroll
+        for (int w = 0; w < W; w++) cur[w] = nxt[w];
+        blk = nb;
+    }
+}
+
+// row split S=2: 16 threads per block, each takes half of the rows (only the word rows those
+// rows read are loaded) -> 2x the waves, half the stores per wave
+template <int NT, int S>
+__global__ __launch_bounds__(256) void k_split(const uint8_t* __restrict__ packed, uint32_t* __restrict__ out,
+                                               uint64_t n_blocks) {
+    constexpr int BPG = 32 / S;
+    const uint64_t blk = uint64_t(blockIdx.x) * BPG + ((threadIdx.x >> 3) % BPG);
+    const int t = int(threadIdx.x & 7);
+    if (blk >= n_blocks) return;
+    EpiParams ep{};
+    const uint8_t* bp = packed + blk * (128 * W);
+    if constexpr (S == 2) {
+        if ((threadIdx.x >> 7) == 0) unpack_block_part<T, W, Epi::Plain, 0, NT, 2, 0>(bp, t, out, int64_t(blk * 1024), true, n_blocks * 1024, ep);
+        else unpack_block_part<T, W, Epi::Plain, 0, NT, 2, 1>(bp, t, out, int64_t(blk * 1024), true, n_blocks * 1024, ep);
+    } else {
+        switch (threadIdx.x >> 6) {
+        case 0: unpack_block_part<T, W, Epi::Plain, 0, NT, 4, 0>(bp, t, out, int64_t(blk * 1024), true, n_blocks * 1024, ep); break;
+        case 1: unpack_block_part<T, W, Epi::Plain, 0, NT, 4, 1>(bp, t, out, int64_t(blk * 1024), true, n_blocks * 1024, ep); break;
+        case 2: unpack_block_part<T, W, Epi::Plain, 0, NT, 4, 2>(bp, t, out, int64_t(blk * 1024), true, n_blocks * 1024, ep); break;
+        default: unpack_block_part<T, W, Epi::Plain, 0, NT, 4, 3>(bp, t, out, int64_t(blk * 1024), true, n_blocks * 1024, ep); break;
+        }
+    }
+}
+
+
+// transposed stores: each lane group decodes its block's rows phase by phase (a phase = the
+// 8 rows that make up 1 KiB of the block), parks them in LDS, and the wave then writes every
+// block's 1 KiB with ONE fully contiguous 1 KiB store instruction (64 lanes x 16 B).
+template <int NT, int P, int R>
+__device__ __forceinline__ void tr_row(const Vec16<T>* p, int t, uint8_t* lds_j) {
+    constexpr int off = fl_index(R, 0) * 4;
+    if constexpr (off / 1024 == P) {
+        const Vec16<T> v = extract_row<T, W, R>(p);
+        uint4 q;
+        __builtin_memcpy(&q, v.w, 16);
+        *reinterpret_cast<uint4*>(lds_j + (off - 1024 * P) + 16 * t) = q;
+    }
+}
+template <int NT, int P, int... Rs>
+__device__ __forceinline__ void tr_phase(const Vec16<T>* p, int t, uint8_t* lds_w, int j, int lane,
+                                         uint8_t* out_w, std::integer_sequence<int, Rs...>) {
+    (tr_row<NT, P, Rs>(p, t, lds_w + j * 1024), ...);
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int m = 0; m < 8; m++) {
+        uint4 q = *reinterpret_cast<const uint4*>(lds_w + m * 1024 + 16 * lane);
+        store_bytes<16, NT>(out_w + size_t(m) * 4096 + 1024 * P + 16 * lane, &q);
+    }
+    __builtin_amdgcn_wave_barrier();
+}
+template <int NT>
+__global__ __launch_bounds__(256) void k_tr(const uint8_t* __restrict__ packed, uint32_t* __restrict__ out,
+                                            uint64_t n_blocks) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_tr[4 * 8 * 1024];
+    const uint64_t gid = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    const uint64_t blk = gid >> 3;
+    const int t = int(gid & 7), lane = int(threadIdx.x & 63), j = lane >> 3;
+    if (blk >= n_blocks) return;
+    Vec16<T> p[W];
+#pragma unroll
+    for (int w = 0; w < W; w++) p[w] = load16<T>(packed + blk * (128 * W) + 128 * w + 16 * t);
+    uint8_t* lds_w = s_tr + (threadIdx.x >> 6) * 8192;
+    uint8_t* out_w = reinterpret_cast<uint8_t*>(out) + (gid >> 6) * 8 * 4096;
+    tr_phase<NT, 0>(p, t, lds_w, j, lane, out_w, std::make_integer_sequence<int, T>{});
+    tr_phase<NT, 1>(p, t, lds_w, j, lane, out_w, std::make_integer_sequence<int, T>{});
+    tr_phase<NT, 2>(p, t, lds_w, j, lane, out_w, std::make_integer_sequence<int, T>{});
+    tr_phase<NT, 3>(p, t, lds_w, j, lane, out_w, std::make_integer_sequence<int, T>{});
+}
+
+
+// rows in memory order (increasing fl_index offset): each lane group writes its block front to back
+template <int R> struct MemRow {
+    // the R-th row in memory order for T=32: group g = R/4, position p = R%4 -> row q*8+g, q = [0,2,1,3][p]
+    static constexpr int q = (R % 4 == 1) ? 2 : (R % 4 == 2) ? 1 : (R % 4);
+    static constexpr int row = q * 8 + R / 4;
+};
+template <int NT, int... Rs>
+__device__ __forceinline__ void rows_memorder(const Vec16<T>* p, int lane0, uint32_t* out, int64_t base,
+                                              std::integer_sequence<int, Rs...>) {
+    EpiParams ep{};
+    bool oob = false;
+    (process_row<T, W, Epi::Plain, 0, NT, MemRow<Rs>::row, true>(p, lane0, out, base, 1ull << 40, ep, oob), ...);
+}
+// XM: XCD-aware workgroup order (workgroup g runs on XCD g % 8: give each XCD a contiguous range)
+template <int NT, bool MEMORD, bool XM>
+__global__ __launch_bounds__(256) void k_ord(const uint8_t* __restrict__ packed, uint32_t* __restrict__ out,
+                                             uint64_t n_blocks) {
+    uint64_t g = blockIdx.x;
+    if constexpr (XM) g = (g % 8) * (gridDim.x / 8) + g / 8;
+    const uint64_t blk = g * 32 + (threadIdx.x >> 3);
+    const int t = int(threadIdx.x & 7);
+    if (blk >= n_blocks) return;
+    Vec16<T> p[W];
+#pragma unroll
+    for (int w = 0; w < W; w++) p[w] = load16<T>(packed + blk * (128 * W) + 128 * w + 16 * t);
+    if constexpr (MEMORD) {
+        rows_memorder<NT>(p, t * 4, out, int64_t(blk * 1024), std::make_integer_sequence<int, T>{});
+    } else {
+        EpiParams ep{};
+        bool oob = false;
+        process_rows<T, W, Epi::Plain, 0, NT, true>(p, t * 4, out, int64_t(blk * 1024), 1ull << 40, ep, oob,
+                                                    std::make_integer_sequence<int, T>{});
+    }
+}
+// persistent pipelined copy of the same bytes: each wave loads its next 7 KiB while storing
+// the current 32 KiB (1 KiB per instruction)
+template <int NT>
+__global__ __launch_bounds__(256) void k_copy_pipe(const uint4* __restrict__ in, uint4* __restrict__ out,
+                                                   uint64_t n_blocks) {
+    const uint64_t nw = uint64_t(gridDim.x) * 4;
+    uint64_t wave = (uint64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+    const int lane = int(threadIdx.x & 63);
+    const uint64_t n_units = n_blocks / 8;
+    if (wave >= n_units) return;
+    uint4 r[7], nx[7];
+#pragma unroll
+    for (int k = 0; k < 7; k++) r[k] = in[wave * 448 + k * 64 + lane];
+    for (;;) {
+        const uint64_t nwv = wave + nw;
+        const bool more = nwv < n_units;
+        if (more) {
+#pragma unroll
+            for (int k = 0; k < 7; k++) nx[k] = in[nwv * 448 + k * 64 + lane];
+        }
+        uint4 acc = r[0];
+#pragma unroll
+        for (int k = 1; k < 7; k++) { acc.x ^= r[k].x; acc.y ^= r[k].y; }
+        uint4* dst = out + wave * 2048;
+#pragma unroll
+        for (int k = 0; k < 32; k++) {
+            uint4 v = make_uint4(acc.x + k, acc.y, acc.z, acc.w);
+            store_bytes<16, NT>(reinterpret_cast<uint8_t*>(dst + k * 64 + lane), &v);
+        }
+        if (!more) break;
+#pragma unroll
+        for (int k = 0; k < 7; k++) r[k] = nx[k];
+        wave = nwv;
+    }
 }
 
 // Roofline reference with the same bytes: each thread reads 7 x 16 B and writes 32 x 16 B,
@@ -75,7 +214,6 @@ __global__ __launch_bounds__(256) void k_copy(const uint4* __restrict__ in, uint
     const uint64_t wave = gid >> 6;
     const int lane = int(gid & 63);
     if (wave * 8 >= n_blocks) return;
-    // a wave owns 8 blocks: reads 8*128*7 B = 448 uint4, writes 8*4096 B = 2048 uint4
     const uint4* src = in + wave * 448;
     uint4* dst = out + wave * 2048;
     uint4 acc = make_uint4(0, 0, 0, 0);
@@ -98,6 +236,15 @@ __global__ __launch_bounds__(256) void k_copy(const uint4* __restrict__ in, uint
     }
 }
 
+// write-only reference: 268 MB of NT stores, nothing read
+__global__ __launch_bounds__(256) void k_write(uint4* __restrict__ out, uint64_t n16) {
+    using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
+    for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n16; i += uint64_t(gridDim.x) * blockDim.x) {
+        u32x4 v = {unsigned(i), 1u, 2u, 3u};
+        __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(out + i));
+    }
+}
+
 __global__ void fill_rand(uint32_t* p, uint64_t n, uint32_t seed) {
     for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += uint64_t(gridDim.x) * blockDim.x) {
         uint32_t x = uint32_t(i) * 2654435761u ^ seed;
@@ -107,43 +254,64 @@ __global__ void fill_rand(uint32_t* p, uint64_t n, uint32_t seed) {
 }
 
 int main(int argc, char** argv) {
+    const bool flush = argc > 1 && std::strcmp(argv[1], "flush") == 0;
     const uint64_t n_vals = 64ull << 20, n_blocks = n_vals / 1024;
     const uint64_t in_bytes = n_blocks * 128 * W, out_bytes = n_vals * 4;
-    const int copies = 4;
+    const int copies = 8;
     std::vector<uint8_t*> in(copies);
     for (int c = 0; c < copies; c++) {
         CK(hipMalloc(&in[c], in_bytes));
         hipLaunchKernelGGL(fill_rand, dim3(4096), dim3(256), 0, 0, (uint32_t*)in[c], in_bytes / 4, 1234u + c);
     }
     uint32_t *out, *ref;
+    uint8_t* junk = nullptr;
     CK(hipMalloc(&out, out_bytes));
     CK(hipMalloc(&ref, out_bytes));
+    if (flush) CK(hipMalloc(&junk, 512ull << 20));
     CK(hipDeviceSynchronize());
     const unsigned grid_base = unsigned(n_blocks * 8 / 256);
     hipLaunchKernelGGL(k_base<0>, dim3(grid_base), dim3(256), 0, 0, in[0], ref, n_blocks);
     CK(hipDeviceSynchronize());
+    int cus = 256;
+    {
+        hipDeviceProp_t p;
+        CK(hipGetDeviceProperties(&p, 0));
+        cus = p.multiProcessorCount;
+    }
 
     struct Var { const char* name; int id; };
-    std::vector<Var> vars = {{"base", 0}, {"base_nt", 1}, {"stride2048", 2}, {"stride2048_nt", 3}, {"two_blocks", 4},
-                             {"two_blocks_nt", 5}, {"copy_ref", 6}, {"copy_ref_nt", 7}, {"stride4096_nt", 8}};
+    std::vector<Var> vars = {{"base_nt", 1}, {"pipe_nt_x2", 2}, {"pipe_nt_x4", 3}, {"pipe_nt_x8", 4},
+                             {"split2_nt", 5}, {"split4_nt", 6}, {"copy_ref_nt", 7}, {"write_only_nt", 8},
+                             {"base_plain", 11}, {"copy_ref_plain", 12},
+                             {"memord_nt", 13}, {"memord_plain", 14}, {"xcd_nt", 15}, {"xcd_memord_nt", 16},
+                             {"copy_pipe_x4_plain", 17}, {"copy_pipe_x8_plain", 18}, {"copy_pipe_x8_nt", 19}};
     auto launch = [&](int id, const uint8_t* src) {
         switch (id) {
-        case 0: hipLaunchKernelGGL(k_base<0>, dim3(grid_base), dim3(256), 0, 0, src, out, n_blocks); break;
         case 1: hipLaunchKernelGGL(k_base<1>, dim3(grid_base), dim3(256), 0, 0, src, out, n_blocks); break;
-        case 2: hipLaunchKernelGGL(k_stride<0>, dim3(2048), dim3(256), 0, 0, src, out, n_blocks); break;
-        case 3: hipLaunchKernelGGL(k_stride<1>, dim3(2048), dim3(256), 0, 0, src, out, n_blocks); break;
-        case 4: hipLaunchKernelGGL(k_two<0>, dim3(grid_base / 2), dim3(256), 0, 0, src, out, n_blocks); break;
-        case 5: hipLaunchKernelGGL(k_two<1>, dim3(grid_base / 2), dim3(256), 0, 0, src, out, n_blocks); break;
-        case 6: hipLaunchKernelGGL(k_copy<0>, dim3(unsigned(n_blocks / 8 * 64 / 256)), dim3(256), 0, 0, (const uint4*)src, (uint4*)out, n_blocks); break;
+        case 2: hipLaunchKernelGGL(k_pipe<1>, dim3(cus * 2), dim3(256), 0, 0, src, out, n_blocks); break;
+        case 3: hipLaunchKernelGGL(k_pipe<1>, dim3(cus * 4), dim3(256), 0, 0, src, out, n_blocks); break;
+        case 4: hipLaunchKernelGGL(k_pipe<1>, dim3(cus * 8), dim3(256), 0, 0, src, out, n_blocks); break;
+        case 5: hipLaunchKernelGGL((k_split<1, 2>), dim3(unsigned(n_blocks / 16)), dim3(256), 0, 0, src, out, n_blocks); break;
+        case 6: hipLaunchKernelGGL((k_split<1, 4>), dim3(unsigned(n_blocks / 8)), dim3(256), 0, 0, src, out, n_blocks); break;
         case 7: hipLaunchKernelGGL(k_copy<1>, dim3(unsigned(n_blocks / 8 * 64 / 256)), dim3(256), 0, 0, (const uint4*)src, (uint4*)out, n_blocks); break;
-        case 8: hipLaunchKernelGGL(k_stride<1>, dim3(4096), dim3(256), 0, 0, src, out, n_blocks); break;
+        case 9: hipLaunchKernelGGL(k_tr<0>, dim3(grid_base), dim3(256), 0, 0, src, out, n_blocks); break;
+        case 10: hipLaunchKernelGGL(k_tr<1>, dim3(grid_base), dim3(256), 0, 0, src, out, n_blocks); break;
+        case 11: hipLaunchKernelGGL(k_base<0>, dim3(grid_base), dim3(256), 0, 0, src, out, n_blocks); break;
+        case 12: hipLaunchKernelGGL(k_copy<0>, dim3(unsigned(n_blocks / 8 * 64 / 256)), dim3(256), 0, 0, (const uint4*)src, (uint4*)out, n_blocks); break;
+        case 13: hipLaunchKernelGGL((k_ord<1, true, false>), dim3(grid_base), dim3(256), 0, 0, src, out, n_blocks); break;
+        case 14: hipLaunchKernelGGL((k_ord<0, true, false>), dim3(grid_base), dim3(256), 0, 0, src, out, n_blocks); break;
+        case 15: hipLaunchKernelGGL((k_ord<1, false, true>), dim3(grid_base), dim3(256), 0, 0, src, out, n_blocks); break;
+        case 16: hipLaunchKernelGGL((k_ord<1, true, true>), dim3(grid_base), dim3(256), 0, 0, src, out, n_blocks); break;
+        case 17: hipLaunchKernelGGL(k_copy_pipe<0>, dim3(cus * 4), dim3(256), 0, 0, (const uint4*)src, (uint4*)out, n_blocks); break;
+        case 18: hipLaunchKernelGGL(k_copy_pipe<0>, dim3(cus * 8), dim3(256), 0, 0, (const uint4*)src, (uint4*)out, n_blocks); break;
+        case 19: hipLaunchKernelGGL(k_copy_pipe<1>, dim3(cus * 8), dim3(256), 0, 0, (const uint4*)src, (uint4*)out, n_blocks); break;
+        case 8: hipLaunchKernelGGL(k_write, dim3(cus * 8), dim3(256), 0, 0, (uint4*)out, out_bytes / 16); break;
         }
     };
-    // correctness of the decode variants vs base
     std::vector<uint32_t> h_ref(n_vals), h_out(n_vals);
     CK(hipMemcpy(h_ref.data(), ref, out_bytes, hipMemcpyDeviceToHost));
     for (auto& v : vars) {
-        if (v.id >= 6 && v.id <= 7) continue;
+        if (v.id == 7 || v.id == 8 || v.id == 12 || v.id >= 17) continue;
         CK(hipMemset(out, 0, out_bytes));
         launch(v.id, in[0]);
         CK(hipDeviceSynchronize());
@@ -160,6 +328,7 @@ int main(int argc, char** argv) {
         for (size_t vi = 0; vi < vars.size(); vi++) {
             for (int k = 0; k < 3; k++) launch(vars[vi].id, in[(rot++) % copies]);
             for (int k = 0; k < reps; k++) {
+                if (flush) CK(hipMemsetAsync(junk, k & 0xff, 512ull << 20, 0));
                 CK(hipEventRecord(a, 0));
                 launch(vars[vi].id, in[(rot++) % copies]);
                 CK(hipEventRecord(b, 0));
@@ -170,14 +339,15 @@ int main(int argc, char** argv) {
             }
         }
     }
+    printf("copies=%d (%.0f MB of inputs) flush=%d\n", copies, copies * in_bytes / 1e6, int(flush));
     const double bytes = double(in_bytes + out_bytes);
     for (size_t vi = 0; vi < vars.size(); vi++) {
         auto v = t[vi];
         std::sort(v.begin(), v.end());
         const double med = v[v.size() / 2], mn = v[0];
-        printf("%-16s median %8.2f us  min %8.2f us  algo %7.1f GB/s (%.1f%% of 8 TB/s)  decoded %7.1f GB/s\n",
-               vars[vi].name, med * 1e3, mn * 1e3, bytes / (med * 1e-3) / 1e9,
-               100.0 * bytes / (med * 1e-3) / 8e12, out_bytes / (med * 1e-3) / 1e9);
+        const double by = vars[vi].id == 8 ? double(out_bytes) : bytes;
+        printf("%-16s median %8.2f us  min %8.2f us  algo %7.1f GB/s (%.1f%% of 8 TB/s)\n",
+               vars[vi].name, med * 1e3, mn * 1e3, by / (med * 1e-3) / 1e9, 100.0 * by / (med * 1e-3) / 8e12);
     }
     return 0;
 }
