@@ -154,21 +154,130 @@ def make_c4(rng, world, rank):
                      read_bytes=arr.nbytes(), write_bytes=int(offs[-1]) + 16 * n, dtype="u8")
 
 
-def make_c5(rng, world, rank):
-    """C5: bench-vortex's TPC-H lineitem scan -> canonicalize (tools/lineitem.py): SF1's 6 001 215
-    rows, 16 columns, each a ChunkedArray of 64 Ki-row chunks compressed with the sampling
-    compressor's cascades.  The table is fixed (strong scaling): the 92 chunks are split into
-    contiguous ranges, one per rank, and a step canonicalizes every column of this rank's range
-    (struct_to_arrow, canonical.rs:169-187: one canonicalize per field)."""
+def c5_file(dist, rank: int) -> np.ndarray:
+    """BASELINE C5's file: the whole synthetic SF1 lineitem table (tools/lineitem.py: 16 columns,
+    92 chunks of 64 Ki rows, each chunk compressed with the sampling compressor's cascade; the
+    three date columns as vortex.date extension arrays) written the way bench-vortex writes it
+    (LayoutWriter::write_array_columns over a StructArray of ChunkedArrays, tpch/mod.rs:249-307;
+    tools/vxfile.py).  Rank 0 writes it once to /tmp, the others read it after a barrier."""
+    import tempfile
+    from tools import lineitem as L
+    from tools import vxfile as X
+    path = Path(tempfile.gettempdir()) / f"vxg_lineitem_{os.environ.get('MASTER_PORT', 'single')}.vortex"
+    if rank == 0:
+        cols, _ = L.lineitem_columns(range(L.n_chunks()))
+        written = []
+        for name, _ in L.COLUMNS:
+            chunks = cols[name].children[1:]
+            if name in L.DATE_COLUMNS:
+                chunks = [X.date_column(c) for c in chunks]
+            written.append((name, chunks))
+        data = X.write_file(written)
+        del cols, written
+        path.write_bytes(data)
+    if dist is not None:
+        dist.barrier()
+    out = np.fromfile(path, dtype=np.uint8)
+    if dist is not None:
+        dist.barrier()
+    if rank == 0:
+        path.unlink(missing_ok=True)
+    return out
+
+
+def _tree_buffer_bytes(node) -> int:
+    tot = sum(int(node.buffers[i].len) for i in range(node.n_buffers))
+    return tot + sum(_tree_buffer_bytes(node.children[i]) for i in range(node.n_children))
+
+
+class FileWorkload:
+    """C5 "via vortex-serde": the lineitem file's bytes sit in pinned host memory; the engine's
+    reader (vxg_file_*) parses footer, layouts and this rank's chunk messages; each column's
+    message range is copied to HBM once (DeviceColumns); a step = one replay of the vxg_plan
+    that canonicalizes the 16 reader-built ChunkedArray trees (struct_to_arrow,
+    canonical.rs:169-187: one canonicalize per field)."""
+
+    def __init__(self, host, ctx, c0: int, c1: int):
+        import torch
+        import vortex_amd.arrays as A
+        from vortex_amd.file import DeviceColumns, VortexFile
+        self.ctx = ctx
+        self.host = torch.from_numpy(host).pin_memory()
+        t0 = time.perf_counter()
+        self.f = VortexFile(self.host)
+        self.dc = DeviceColumns(self.f, ctx, None, c0, c1)
+        torch.cuda.synchronize()
+        self.setup_s = time.perf_counter() - t0
+        self.plan = A.Plan(self.dc.nodes, ctx)
+        self.read_bytes = sum(_tree_buffer_bytes(n) for n in self.dc.nodes)
+        self.region_bytes = self.dc.nbytes()
+        self.write_bytes = 0
+        for r in self.plan.results:
+            for t in (r.values, r.views, r.data):
+                if t is not None:
+                    self.write_bytes += int(t.numel())
+        self.rows = int(self.dc.nodes[0].len)
+
+    def step(self):
+        self.plan.launch()
+
+    def close(self):
+        self.plan.close()
+        self.f.close()
+
+
+def run_file_e2e(host, ctx, c0: int, c1: int, reps: int = 5) -> dict:
+    """File bytes in (pinned host memory) -> Arrow buffers out (pinned host memory): reader
+    parse (footer + layouts + this range's messages) + one H2D per column range + canonicalize
+    (direct vxg_canonicalize per column) + D2H of every canonical buffer.  Median of `reps`."""
+    import torch
+    import vortex_amd.arrays as A
+    from vortex_amd import _lib
+    from vortex_amd.file import DeviceColumns, VortexFile
+    hostt = torch.from_numpy(host).pin_memory()
+    outs_h, times, parts = None, [], []
+    for r in range(reps + 1):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        f = VortexFile(hostt)
+        dc = DeviceColumns(f, ctx, None, c0, c1)
+        t1 = time.perf_counter()
+        keep: list = []
+        res = []
+        for node in dc.nodes:
+            o, rr = A.alloc_canonical(ctx, node, keep)
+            _lib.check(ctx.lib.vxg_canonicalize(ctx.handle, C.byref(node), C.byref(o), ctx.stream_ptr()))
+            res.append(rr)
+        bufs = [t for rr in res for t in (rr.values, rr.views, rr.data, rr.validity) if t is not None]
+        if outs_h is None:
+            outs_h = [torch.empty(t.numel(), dtype=torch.uint8).pin_memory() for t in bufs]
+        for hbuf, t in zip(outs_h, bufs):
+            hbuf.copy_(t, non_blocking=True)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        ctx.sync()
+        f.close()
+        times.append(t2 - t0)
+        parts.append((t1 - t0, t2 - t1))
+    i = int(np.argsort(times[1:])[len(times[1:]) // 2]) + 1
+    out_bytes = sum(int(h.numel()) for h in outs_h)
+    return dict(e2e_ms=round(times[i] * 1e3, 3), parse_and_h2d_ms=round(parts[i][0] * 1e3, 3),
+                decode_and_d2h_ms=round(parts[i][1] * 1e3, 3), file_bytes=int(host.size),
+                h2d_bytes=int(dc.nbytes()), d2h_bytes=out_bytes,
+                e2e_decoded_GBps=round(out_bytes / times[i] / 1e9, 2))
+
+
+def make_c5(rng, world, rank, dist=None):
+    """C5: bench-vortex's TPC-H lineitem scan -> canonicalize "via vortex-serde": the table is
+    read from a Vortex file's bytes (c5_file) by the engine's reader.  The table is fixed
+    (strong scaling): the 92 chunks are split into contiguous ranges, one per rank, and a step
+    canonicalizes every column of this rank's range."""
     from tools import lineitem as L
     mine = c5_shard(world, rank)
-    cols, plain = L.lineitem_columns(mine)
-    rows = sum(len(v) for v in plain["l_orderkey"])
-    write = sum(L.canonical_bytes(v) for vs in plain.values() for v in vs)
-    read = sum(a.nbytes() for a in cols.values())
-    return [cols[name] for name, _ in L.COLUMNS], dict(
-        name="C5", encoding="lineitem scan: 16 x vortex.chunked[<per-column cascades>] -> canonical",
-        values=rows, read_bytes=read, write_bytes=write, dtype="mixed", chunks_per_gpu=len(mine),
+    host = c5_file(dist, rank)
+    return ("file", host, mine.start, mine.stop), dict(
+        name="C5", encoding="lineitem scan from Vortex file bytes: 16 x vortex.chunked[<per-column cascades>] -> canonical",
+        values=0, read_bytes=0, write_bytes=0, dtype="mixed", chunks_per_gpu=len(mine),
         chunk_range=[mine.start, mine.stop], global_chunks=L.n_chunks(), strong_scaling=True)
 
 
@@ -530,12 +639,19 @@ def main():
     results = {}
     for key in [w.strip() for w in args.workloads.split(",") if w.strip()]:
         t0 = time.perf_counter()
-        arr, info = makers[key](rng, shard_world, rank)
-        e2e = run_e2e(arr, info, ctx) if args.e2e and not isinstance(arr, list) else None
-        # one-array steps are one or two back-to-back kernel launches: direct calls overlap the
-        # next submission with the running kernel (a graph replay measured 2-6 us slower per
-        # step on C1-C4); multi-array steps (C5: 16 columns, ~30 kernels) replay a graph
-        wl = Workload(arr, info, ctx, copies[key], graph=isinstance(arr, list) and not args.no_graph)
+        arr, info = makers[key](rng, shard_world, rank, dist) if key == "c5" else makers[key](rng, shard_world, rank)
+        if isinstance(arr, tuple) and arr[0] == "file":
+            _, host, c0, c1 = arr
+            e2e = run_file_e2e(host, ctx, c0, c1) if args.e2e else None
+            wl = FileWorkload(host, ctx, c0, c1)
+            info.update(values=wl.rows, read_bytes=wl.read_bytes, write_bytes=wl.write_bytes,
+                        h2d_region_bytes=wl.region_bytes, reader_setup_ms=round(wl.setup_s * 1e3, 2))
+        else:
+            e2e = run_e2e(arr, info, ctx) if args.e2e and not isinstance(arr, list) else None
+            # one-array steps are one or two back-to-back kernel launches: direct calls overlap
+            # the next submission with the running kernel (a graph replay measured 2-6 us slower
+            # per step on C1-C4); multi-array steps replay a graph
+            wl = Workload(arr, info, ctx, copies[key], graph=isinstance(arr, list) and not args.no_graph)
         del arr
         if rank == 0:
             log(f"[bench] {info['name']}: built in {time.perf_counter() - t0:.1f}s; timing...")
@@ -602,7 +718,7 @@ def main():
                 "kernel_ms_mean": round(r["kernel_ms_mean"], 5), "kernel_ms_median": round(r["kernel_ms_median"], 5),
                 "ms_per_step": round(r["ms_per_step"], 5),
                 "read_bytes": i["read_bytes"], "write_bytes": i["write_bytes"]}
-            for extra in ("chunks_per_gpu", "chunk_range", "global_chunks"):
+            for extra in ("chunks_per_gpu", "chunk_range", "global_chunks", "h2d_region_bytes", "reader_setup_ms"):
                 if extra in i:
                     ent[extra] = i[extra]
             if cpu is not None and i["name"] in cpu:

@@ -26,6 +26,9 @@ def exported(lib: Path, prefix: str) -> set:
 def test_gpu_lib_exports_match_header():
     decl = declared("vortex_gpu.h", "vxg")
     assert decl == set(L.GPU_SIGNATURES), "ctypes signatures out of sync with vortex_gpu.h"
+    fdecl = declared("vortex_file.h", "vxg")
+    assert fdecl == set(L.FILE_SIGNATURES), "ctypes signatures out of sync with vortex_file.h"
+    decl = decl | fdecl
     assert exported(L.GPU_LIB_PATH, "vxg") == decl
     lib = L.gpu_lib()  # loads (HIP runtime present in the image; no device needed)
     for name in decl:
@@ -48,8 +51,11 @@ def test_struct_layouts_match_c(tmp_path):
                                                  "validity", "n_data_buffers", "data_buffers_cap",
                                                  "data_buffers"]),
               "vxg_data_buffer": (L.VxgDataBuffer, ["offset", "len"]),
-              "vxg_dict_chunk": (L.VxgDictChunk, ["packed", "out", "n_blocks", "dict_len"])}
-    src = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{ROOT}/include/vortex_gpu.h"', "int main(){",
+              "vxg_dict_chunk": (L.VxgDictChunk, ["packed", "out", "n_blocks", "dict_len"]),
+              "vxg_file_column": (L.VxgFileColumn, ["name", "dtype", "is_extension", "n_chunks", "extension_id",
+                                                    "extension_metadata_len", "rows"]),
+              "vxg_file_chunk": (L.VxgFileChunk, ["row_offset", "rows", "message_end", "buffers_begin"])}
+    src = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{ROOT}/include/vortex_gpu.h"', f'#include "{ROOT}/include/vortex_file.h"', "int main(){",
            'printf("vxg_meta %zu\\n", sizeof(vxg_meta));',
            'printf("runendbool.start %zu\\n", offsetof(vxg_meta, runendbool.start));',
            'printf("runendbool.ends_ptype %zu\\n", offsetof(vxg_meta, runendbool.ends_ptype));',

@@ -1,0 +1,90 @@
+"""GPU: BASELINE C5 "via vortex-serde" at reduced size — a lineitem Vortex file's bytes are parsed
+by the engine's reader (vxg_file_*), each column's message range is copied to HBM once, and the
+reader's trees are canonicalized by the HIP engine; every output byte must equal the oracle's
+canonicalize of the arrays that were written (tests/oracle_tree.py), and the plain values."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import vortex_amd as V
+import vortex_amd._lib as L
+import vortex_amd.arrays as A
+from oracle_tree import canon
+from tools import lineitem as LI
+from tools import vxfile as X
+from vortex_amd.file import DeviceColumns, VortexFile, scan
+
+pytestmark = pytest.mark.gpu
+
+
+def _file(rows, chunk_rows):
+    import torch
+    cols, plain = LI.lineitem_columns(range(LI.n_chunks(rows, chunk_rows)), rows=rows, chunk_rows=chunk_rows)
+    written = []
+    for name, _ in LI.COLUMNS:
+        chunks = cols[name].children[1:]
+        if name in ("l_shipdate", "l_commitdate", "l_receiptdate"):
+            chunks = [X.date_column(c) for c in chunks]
+        written.append((name, chunks))
+    data = X.write_file(written)
+    host = torch.from_numpy(np.frombuffer(data, np.uint8).copy()).pin_memory()
+    return VortexFile(host), written, plain
+
+
+def _storage(chunks):
+    return [c.children[0] if c.encoding == X.ENC_EXTENSION else c for c in chunks]
+
+
+def _compare(res, chunks, plain_vals):
+    arr = A.chunked(_storage(chunks))
+    ref, rvalid = canon(arr)
+    if res.kind == "primitive":
+        got = res.numpy()
+        assert got.tobytes() == ref.tobytes()
+        assert got.tobytes() == np.concatenate(plain_vals).astype(got.dtype).tobytes()
+    else:
+        views, _ = res.numpy()
+        rviews, rheap = ref
+        assert views.tobytes() == rviews.tobytes()
+        bufs = res.buffers()
+        assert len(bufs) == len(rheap)
+        for g, r in zip(bufs, rheap):
+            assert g.tobytes() == r.tobytes()
+    assert res.validity_mask() is None and rvalid is None
+
+
+def test_lineitem_file_scan_matches_oracle(ctx):
+    f, written, plain = _file(rows=20_000, chunk_rows=4096)
+    assert f.row_count == 20_000
+    res = scan(f, ctx)
+    assert len(res) == 16
+    for (name, chunks), r in zip(written, res):
+        assert r.len == 20_000, name
+        _compare(r, chunks, plain[name])
+    f.close()
+
+
+def test_lineitem_file_chunk_range_and_plan(ctx):
+    """A rank's chunk range (what bench C5 decodes at N > 1) through a vxg_plan, replayed after
+    the device region was refreshed from the file bytes."""
+    f, written, plain = _file(rows=30_000, chunk_rows=4096)
+    dc = DeviceColumns(f, ctx, None, 2, 6)
+    plan = A.Plan(dc.nodes, ctx)
+    for rep in range(2):
+        dc.refresh()
+        res = plan.launch(sync=True)
+        for (name, chunks), r in zip(written, res):
+            _compare(r, chunks[2:6], plain[name][2:6])
+    plan.close()
+    f.close()
+
+
+def test_file_reader_rejects_uncovered_region(ctx):
+    f, _, _ = _file(rows=5000, chunk_rows=2048)
+    import torch
+    region = torch.empty(64, dtype=torch.uint8, device="cuda")
+    with pytest.raises(L.VortexGpuError) as ei:
+        f.column_tree(0, 0, 2, region.data_ptr(), 0, 64)
+    assert ei.value.kind == "InvalidArgument"
+    f.close()

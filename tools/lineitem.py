@@ -26,6 +26,7 @@ COLUMNS = [("l_orderkey", "i64"), ("l_partkey", "i64"), ("l_suppkey", "i64"), ("
            ("l_returnflag", "utf8"), ("l_linestatus", "utf8"), ("l_shipdate", "i32"), ("l_commitdate", "i32"),
            ("l_receiptdate", "i32"), ("l_shipinstruct", "utf8"), ("l_shipmode", "utf8"), ("l_comment", "utf8")]
 
+DATE_COLUMNS = ("l_shipdate", "l_commitdate", "l_receiptdate")  # Date32 -> vortex.date extension
 RETURNFLAG = [b"A", b"N", b"R"]
 LINESTATUS = [b"F", b"O"]
 SHIPINSTRUCT = [b"DELIVER IN PERSON", b"COLLECT COD", b"NONE", b"TAKE BACK RETURN"]

@@ -189,6 +189,29 @@ GPU_SIGNATURES = {
     "vxg_fill": (ST, [VP, UINT, VP, U64, VP, VP]),
 }
 
+class VxgFileColumn(C.Structure):
+    _fields_ = [("name", C.c_char_p), ("dtype", C.c_uint8), ("ptype", C.c_uint8), ("nullable", C.c_uint8),
+                ("is_extension", C.c_uint8), ("n_chunks", C.c_uint32), ("extension_id", C.c_char_p),
+                ("extension_metadata", C.POINTER(C.c_uint8)), ("extension_metadata_len", C.c_uint64),
+                ("rows", C.c_uint64)]
+
+
+class VxgFileChunk(C.Structure):
+    _fields_ = [("row_offset", C.c_uint64), ("rows", C.c_uint64), ("message_begin", C.c_uint64),
+                ("message_end", C.c_uint64), ("buffers_begin", C.c_uint64)]
+
+
+# include/vortex_file.h (the Vortex file reader, exported by libvortex_gpu.so)
+FILE_SIGNATURES = {
+    "vxg_file_open": (ST, [VP, U64, C.POINTER(VP)]),
+    "vxg_file_close": (ST, [VP]),
+    "vxg_file_info": (ST, [VP, C.POINTER(U64), C.POINTER(U32)]),
+    "vxg_file_column_info": (ST, [VP, U32, C.POINTER(VxgFileColumn)]),
+    "vxg_file_chunk_info": (ST, [VP, U32, U32, C.POINTER(VxgFileChunk)]),
+    "vxg_file_chunk_offsets": (ST, [VP, U32, U32, U32, C.POINTER(U64)]),
+    "vxg_file_column_array": (ST, [VP, U32, U32, U32, VP, U64, U64, VP, C.POINTER(C.POINTER(VxgArray))]),
+}
+
 ENC_SIGNATURES = {
     "vxe_bitpack": (U64, [INT, UINT, VP, U64, VP]),
     "vxe_best_bit_width": (UINT, [INT, VP, U64]),
@@ -231,7 +254,7 @@ _enc = None
 def gpu_lib() -> C.CDLL:
     global _gpu
     if _gpu is None:
-        _gpu = _load(GPU_LIB_PATH, GPU_SIGNATURES)
+        _gpu = _load(GPU_LIB_PATH, {**GPU_SIGNATURES, **FILE_SIGNATURES})
         if _gpu.vxg_abi_version() != ABI_VERSION:
             raise ImportError("libvortex_gpu.so ABI version mismatch")
     return _gpu

@@ -73,7 +73,8 @@ def encode_bitpacked(values, bit_width: Optional[int] = None, allow_patches: boo
             ind = encode_bitpacked(idx, bit_width=iw, allow_patches=False) if iw < 64 else A.primitive(idx)
         else:
             ind = A.primitive(idx)
-        patches = A.sparse(ind, A.primitive(pv), v.size)
+        # gather_patches (bitpacking/compress.rs:138-163): values PrimitiveArray with Validity::AllValid
+        patches = A.sparse(ind, A.primitive(pv, validity="ALL_VALID"), v.size)
     return A.bitpacked(packed, p, bit_width, v.size, offset=offset, patches=patches, validity=validity)
 
 
@@ -137,7 +138,8 @@ def encode_alp(values, cascade: bool = True) -> Array:
     if idx.size:
         iw = max(1, bit_width_of(int(idx.max())))
         ind = encode_bitpacked(idx, bit_width=iw, allow_patches=False) if cascade and iw < 64 else A.primitive(idx)
-        patches = A.sparse(ind, A.primitive(pv), v.size)
+        # alp/compress.rs:38-45: exception values PrimitiveArray with Validity::AllValid
+        patches = A.sparse(ind, A.primitive(pv, validity="ALL_VALID"), v.size)
     child = encode_for_bitpacked(enc, allow_patches=True) if cascade else A.primitive(enc)
     return A.alp(child, e, f, patches)
 
@@ -166,7 +168,8 @@ def encode_alprd(values) -> Array:
     if m:
         ep, ex = ep[:m], ex[:m]
         bw = max(1, bit_width_of(int(ep.max())))
-        exc = A.sparse(encode_bitpacked(ep, bit_width=bw, allow_patches=False), A.primitive(ex), n)
+        # alp_rd/mod.rs:235-236: exceptions with Validity::AllValid
+        exc = A.sparse(encode_bitpacked(ep, bit_width=bw, allow_patches=False), A.primitive(ex, validity="ALL_VALID"), n)
     return A.alp_rd(p, left_a, list(d[: dl.value]), right_a, rbw.value, exc)
 
 
