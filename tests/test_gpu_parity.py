@@ -837,6 +837,38 @@ def test_take_validity_and_errors(ctx):
     assert ei.value.kind == "OutOfBounds"
 
 
+@pytest.mark.parametrize("dt", [np.int8, np.int16, np.int32, np.int64])
+def test_take_negative_index_is_out_of_bounds(ctx, dt):
+    """A negative signed index is a huge usize in the reference (`as usize`): OutOfBounds on
+    every path - unpack_single (few indices), canonicalize-then-take (many indices or other
+    encodings), the Dict codes take, and the validity gather."""
+    rng = np.random.default_rng(5)
+    n = 1000  # longer than 255 so a zero-extended i8 -1 would be a valid row
+    v = rng.integers(0, 1 << 12, n).astype(np.uint32)
+    m = rng.random(n) > 0.3
+    trees = [E.encode_bitpacked(v, bit_width=12, allow_patches=False),                  # packed path
+             A.primitive(v),                                                             # fallback
+             E.encode_dict(rng.integers(0, 5, n).astype(np.uint32) * 7),                 # Dict codes
+             A.primitive(v, validity=m)]                                                 # validity gather
+    for t in trees:
+        for idx in (np.array([-1], dt), np.array([3, -1, 5] + [1] * 200, dt)):
+            with pytest.raises(V.VortexGpuError) as ei:
+                A.take(t.to(torch_dev()), idx, ctx)
+            assert ei.value.kind == "OutOfBounds", (t.encoding, idx[:3])
+
+
+def test_take_index_dtypes(ctx):
+    import torch
+    v = np.arange(100, dtype=np.uint32)
+    t = A.primitive(v).to(torch_dev())
+    for tdt in ("uint16", "uint32", "uint64"):
+        if hasattr(torch, tdt):
+            idx = torch.tensor([3, 7], dtype=torch.int64).to(getattr(torch, tdt))
+            assert A.take(t, idx, ctx).numpy().tolist() == [3, 7]
+    with pytest.raises(V.VortexGpuError):
+        A.take(t, np.array([1.0]), ctx)
+
+
 # ------------------------------------------------------------------ compute::filter (stream compaction)
 def _filter_case(ctx, arr, pred):
     from oracle_tree import filter_canon

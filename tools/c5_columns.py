@@ -1,0 +1,86 @@
+"""Per-column isolation of BASELINE C5 (the lineitem scan read from Vortex file bytes).
+
+Every column of the file is canonicalized ALONE (one vxg_canonicalize per step on one stream,
+so a rocprofv3 --kernel-trace of this script gives each kernel its own duration), timed with
+HIP events over `reps` back-to-back steps; prints one JSON line per column with its kernel
+time, algorithmic bytes (compressed buffers read + canonical bytes written) and fraction of the
+8 TB/s HBM roofline, then the sum.  Usage:
+  python tools/c5_columns.py [--world N --rank R] [--reps 20]
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--world", type=int, default=1)
+    ap.add_argument("--rank", type=int, default=0)
+    ap.add_argument("--reps", type=int, default=20)
+    args = ap.parse_args()
+    import torch
+    import bench
+    import vortex_amd as V
+    import vortex_amd.arrays as A
+    from vortex_amd import _lib
+    from vortex_amd.file import DeviceColumns, VortexFile
+    mine = bench.c5_shard(args.world, args.rank)
+    host = torch.from_numpy(bench.c5_file(None, 0)).pin_memory()
+    ctx = V.Context(0)
+    f = VortexFile(host)
+    dc = DeviceColumns(f, ctx, None, mine.start, mine.stop)
+    tot_t = tot_p = tot_b = 0.0
+    for col, node in zip(dc.columns, dc.nodes):
+        keep: list = []
+        o, res = A.alloc_canonical(ctx, node, keep)
+
+        def step():
+            _lib.check(ctx.lib.vxg_canonicalize(ctx.handle, C.byref(node), C.byref(o), ctx.stream_ptr()))
+        for _ in range(3):
+            step()
+        ctx.sync()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.reps):
+            step()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / args.reps
+        # the same column as its own vxg_plan (device chunk tables: one launch per kernel group)
+        plan = A.Plan([node], ctx)
+        for _ in range(3):
+            plan.launch()
+        ctx.sync()
+        e0.record()
+        for _ in range(args.reps):
+            plan.launch()
+        e1.record()
+        torch.cuda.synchronize()
+        plan_ms = e0.elapsed_time(e1) / args.reps
+        plan.close()
+        rb = bench._tree_buffer_bytes(node)
+        wb = sum(int(t.numel()) for t in (res.values, res.views, res.data) if t is not None)
+        tot_t += ms
+        tot_p += plan_ms
+        tot_b += rb + wb
+        print(json.dumps({"column": f.columns[col].name, "chunks": len(mine), "ms": round(ms, 4),
+                          "plan_ms": round(plan_ms, 4), "read_bytes": rb, "write_bytes": wb,
+                          "hbm_frac": round((rb + wb) / ms / 1e6 / 8000, 3),
+                          "plan_hbm_frac": round((rb + wb) / plan_ms / 1e6 / 8000, 3)}), flush=True)
+    print(json.dumps({"column": "SUM (sequential)", "ms": round(tot_t, 4), "plan_ms": round(tot_p, 4),
+                      "bytes": tot_b, "hbm_frac": round(tot_b / tot_t / 1e6 / 8000, 3),
+                      "plan_hbm_frac": round(tot_b / tot_p / 1e6 / 8000, 3)}), flush=True)
+    f.close()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

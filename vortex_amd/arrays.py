@@ -580,10 +580,17 @@ def take(a: Array, indices, ctx: Context, sync: bool = True) -> Canonical:
     dev = torch.device("cuda", ctx.device)
     if isinstance(indices, torch.Tensor):
         it = indices.to(dev)
-        ip = {torch.uint8: "u8", torch.int8: "i8", torch.int16: "i16", torch.int32: "i32",
-              torch.int64: "i64"}[it.dtype]
+        tmap = {torch.uint8: "u8", torch.int8: "i8", torch.int16: "i16", torch.int32: "i32", torch.int64: "i64"}
+        for name, p in (("uint16", "u16"), ("uint32", "u32"), ("uint64", "u64")):
+            if hasattr(torch, name):
+                tmap[getattr(torch, name)] = p
+        if it.dtype not in tmap:
+            raise VortexError(3, f"take: indices must be integers, got {it.dtype}")
+        ip = tmap[it.dtype]
     else:
         ia = np.ascontiguousarray(indices)
+        if ia.dtype not in PTYPE_OF_NP or ia.dtype.kind not in "iu":
+            raise VortexError(3, f"take: indices must be integers, got {ia.dtype}")
         ip = PTYPE_OF_NP[ia.dtype]
         it = torch.from_numpy(ia.view(np.uint8).copy()).to(dev)
     n = int(it.numel() if isinstance(indices, torch.Tensor) else np.asarray(indices).size)
@@ -643,13 +650,13 @@ def filter(a: Array, predicate: Array, ctx: Context) -> Canonical:
     else:
         res.views = buf[: 16 * k]
         hb = int(out.data_bytes)
-        host = np.empty(hb + 16, dtype=np.uint8)
-        if out.data:  # the engine sized and allocated the new heap: copy it out and release it
-            _lib.check(ctx.lib.vxg_memcpy_d2h(ctx.handle, C.c_void_p(host.ctypes.data), C.c_void_p(out.data), hb,
+        heap = torch.empty(hb + 16, dtype=torch.uint8, device=dev)
+        if out.data:  # the engine sized and allocated the new heap: move it into a torch buffer (D2D)
+            _lib.check(ctx.lib.vxg_memcpy_d2d(ctx.handle, C.c_void_p(heap.data_ptr()), C.c_void_p(out.data), hb,
                                               ctx.stream_ptr()))
             ctx.sync()
             _lib.check(ctx.lib.vxg_free(ctx.handle, C.c_void_p(out.data)))
-        res.data = torch.from_numpy(host).to(dev)[:hb]
+        res.data = heap[:hb]
         res.data_buffers = [(0, hb)]
     if out.validity:
         if vt is None or out.validity != vt.data_ptr():

@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -62,6 +63,16 @@ vxg_status hip_check(hipError_t e, const char* what) {
                      std::string(what) + ": " + hipGetErrorString(e));
 }
 
+// K14 (dict_rows.hip) for 8/16-byte dictionary values; VXG_DICT_ROWS=0 selects K1's Dict
+// epilogue instead (A/B measurements).
+static bool dict_rows_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("VXG_DICT_ROWS");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 // K1 dispatch over the instantiation units.
 vxg_status launch_fl_unpack(int T, int W, Epi epi, int vw, const ChunkTable& t, uint64_t g, hipStream_t s) {
     if (W < 0 || W > T) return set_error(VXG_ERR_INVALID_ARGUMENT, "bit width out of range");
@@ -81,6 +92,7 @@ vxg_status launch_fl_unpack(int T, int W, Epi epi, int vw, const ChunkTable& t, 
         return fl_alp(T, W, epi, t, g, s);
     case Epi::Dict:
         if (W > kDictFusedMaxW) return VXG_ERR_NOT_IMPLEMENTED;
+        if ((vw == 8 || vw == 16) && dict_rows_enabled()) return launch_dict_rows(T, W, vw, t, s);
         switch (vw) {
         case 1: return fl_dict_1(T, W, t, g, s);
         case 2: return fl_dict_2(T, W, t, g, s);
@@ -462,7 +474,7 @@ vxg_status Planner::decode_dict_primitive(const vxg_array& a, void* dst) {
     }
     const void* pc;
     VXG_TRY(view_primitive(*codes, &pc));
-    return launch_take(vw, pv, values->len, width(*codes), pc, a.len, dst, ctx_->c.err_word, s_);
+    return launch_take(vw, pv, values->len, width(*codes), false, pc, a.len, dst, ctx_->c.err_word, s_);
 }
 
 // Chunks whose whole decode is one K1 launch (+ patch scatters): BitPacked, FoR/ZigZag/ALP over
@@ -830,7 +842,7 @@ vxg_status Planner::validity_into(const vxg_array& a, void** bitmap) {
         VXG_TRY(validity_into(*vals, &vbits));
         const void* pc;
         VXG_TRY(view_primitive(*codes, &pc));
-        return launch_gather_bits(*bitmap, pc, width(*codes), a.len, static_cast<const uint8_t*>(vbits), vals->len,
+        return launch_gather_bits(*bitmap, pc, width(*codes), false, a.len, static_cast<const uint8_t*>(vbits), vals->len,
                                   ctx_->c.err_word, s_);
     }
     if (kind == 3) {  // Sparse with null fill: valid exactly at the indices (flatten.rs:82-93)
@@ -887,7 +899,7 @@ vxg_status Planner::take_values(const vxg_array& a, const void* idx, int iw, boo
     auto via_canonical = [&]() -> vxg_status {  // canonicalize, then take the primitive
         const void* pv;
         VXG_TRY(view_primitive(a, &pv));
-        return launch_take(width(a), pv, a.len, iw, idx, n, dst, ctx_->c.err_word, s_);
+        return launch_take(width(a), pv, a.len, iw, isg, idx, n, dst, ctx_->c.err_word, s_);
     };
     const vxg_array* bp = nullptr;
     Epi epi = Epi::Plain;
@@ -935,7 +947,7 @@ vxg_status Planner::take_values(const vxg_array& a, const void* idx, int iw, boo
         VXG_TRY(take_values(*codes, idx, iw, isg, n, tc));
         const void* pv;
         VXG_TRY(view_primitive(*values, &pv));
-        return launch_take(width(*values), pv, values->len, width(*codes), tc, n, dst, ctx_->c.err_word, s_);
+        return launch_take(width(*values), pv, values->len, width(*codes), false, tc, n, dst, ctx_->c.err_word, s_);
     }
     default: return via_canonical();
     }
@@ -993,7 +1005,8 @@ vxg_status Planner::take(const vxg_array& a, const void* idx, int iw, bool isg, 
     VXG_TRY(validity_into(a, &src));
     const uint64_t bytes = ((n + 31) / 32) * 4;
     if (!out.validity) VXG_TRY(hip_check(hipMalloc(&out.validity, bytes ? bytes : 4), "take validity alloc"));
-    return launch_gather_bits(out.validity, idx, iw, n, static_cast<const uint8_t*>(src), a.len, ctx_->c.err_word, s_);
+    return launch_gather_bits(out.validity, idx, iw, isg, n, static_cast<const uint8_t*>(src), a.len, ctx_->c.err_word,
+                              s_);
 }
 
 // compute::filter (compute/filter.rs:23-52).  The predicate (any Bool encoding) becomes a bit
@@ -1346,7 +1359,7 @@ vxg_status Planner::strings_into(const vxg_array& a, uint8_t* views, uint8_t* da
         }
         const void* pc;
         VXG_TRY(view_primitive(*codes, &pc));
-        return launch_take(16, vviews, values->len, width(*codes), pc, a.len, views, ctx_->c.err_word, s_);
+        return launch_take(16, vviews, values->len, width(*codes), false, pc, a.len, views, ctx_->c.err_word, s_);
     }
     case VXG_ENC_CHUNKED: {
         // pack_views (chunked/canonical.rs:194-236): each chunk's views go to its slice of the
@@ -1603,6 +1616,11 @@ vxg_status vxg_memcpy_h2d(vxg_ctx* ctx, void* dst, const void* src, uint64_t byt
 vxg_status vxg_memcpy_d2h(vxg_ctx* ctx, void* dst, const void* src, uint64_t bytes, void* stream) {
     VXG_TRY(use_device(ctx));
     return hip_check(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, S(stream)), "d2h");
+}
+
+vxg_status vxg_memcpy_d2d(vxg_ctx* ctx, void* dst, const void* src, uint64_t bytes, void* stream) {
+    VXG_TRY(use_device(ctx));
+    return hip_check(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, S(stream)), "d2d");
 }
 
 vxg_status vxg_stream_sync(vxg_ctx* ctx, void* stream) {
@@ -1876,7 +1894,7 @@ vxg_status vxg_take(vxg_ctx* ctx, unsigned value_width, const void* values, uint
                     const void* codes, uint64_t n, void* out, void* stream) {
     VXG_TRY(use_device(ctx));
     if (!ptype_is_unsigned(codes_ptype)) return set_error(VXG_ERR_MISMATCHED_TYPES, "take indices must be unsigned");
-    return launch_take(int(value_width), values, n_values, ptype_width(codes_ptype), codes, n, out,
+    return launch_take(int(value_width), values, n_values, ptype_width(codes_ptype), ptype_is_signed(codes_ptype), codes, n, out,
                        ctx->c.err_word, S(stream));
 }
 
@@ -1914,8 +1932,14 @@ vxg_status vxg_filter_array(vxg_ctx* ctx, const vxg_array* a, const vxg_array* p
                             void* stream) {
     VXG_TRY(use_device(ctx));
     if (!a || !predicate || !out) return set_error(VXG_ERR_INVALID_ARGUMENT, "null array/predicate/out");
-    Planner p(ctx, S(stream));
-    return p.filter(*a, *predicate, *out);
+    vxg_status st;
+    {
+        Planner p(ctx, S(stream));
+        st = p.filter(*a, *predicate, *out);
+    }
+    if (st != VXG_OK) return st;
+    // synchronous like the reference's compute::filter: every output is complete on return
+    return hip_check(hipStreamSynchronize(S(stream)), "filter sync");
 }
 
 vxg_status vxg_runend_bool_decode(vxg_ctx* ctx, int ends_ptype, const void* ends, uint64_t n_runs, uint64_t offset,

@@ -254,14 +254,19 @@ static vxg_status take_c(int vw, const void* values, uint64_t nv, const void* co
     return hip_check(hipGetLastError(), "take_kernel");
 }
 
-vxg_status launch_take(int value_width, const void* values, uint64_t n_values, int code_width,
+// Signed indices are sign-extended: a negative index becomes a huge usize and is OutOfBounds,
+// as the reference's `as usize` conversion makes it (primitive/compute/take.rs:58-67).
+vxg_status launch_take(int value_width, const void* values, uint64_t n_values, int code_width, bool code_signed,
                        const void* codes, uint64_t n, void* out, uint32_t* err, hipStream_t s) {
     if (n == 0) return VXG_OK;
-    switch (code_width) {
+    switch (code_width * (code_signed ? -1 : 1)) {
     case 1: return take_c<uint8_t>(value_width, values, n_values, codes, n, out, err, s);
     case 2: return take_c<uint16_t>(value_width, values, n_values, codes, n, out, err, s);
     case 4: return take_c<uint32_t>(value_width, values, n_values, codes, n, out, err, s);
-    case 8: return take_c<uint64_t>(value_width, values, n_values, codes, n, out, err, s);
+    case 8: case -8: return take_c<uint64_t>(value_width, values, n_values, codes, n, out, err, s);
+    case -1: return take_c<int8_t>(value_width, values, n_values, codes, n, out, err, s);
+    case -2: return take_c<int16_t>(value_width, values, n_values, codes, n, out, err, s);
+    case -4: return take_c<int32_t>(value_width, values, n_values, codes, n, out, err, s);
     default: return VXG_ERR_INVALID_ARGUMENT;
     }
 }
@@ -927,7 +932,7 @@ vxg_status launch_assign_bits_at(void* dst, uint64_t dst_off, const void* idx, i
 // Validity of take(values, codes) (primitive/compute/take.rs:58-67 -> Validity::take): bit i =
 // values_valid[codes[i]], 32 rows per thread, whole words into a zeroed bitmap at bit 0.
 __global__ __launch_bounds__(kBlock) void gather_bits_kernel(uint32_t* __restrict__ dst, const void* codes, int cw,
-                                                             uint64_t n, const uint8_t* __restrict__ src,
+                                                             bool csg, uint64_t n, const uint8_t* __restrict__ src,
                                                              uint64_t n_values, uint32_t* __restrict__ err) {
     const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
     for (uint64_t w = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; w * 32 < n; w += stride) {
@@ -936,7 +941,7 @@ __global__ __launch_bounds__(kBlock) void gather_bits_kernel(uint32_t* __restric
         for (int k = 0; k < 32; k++) {
             const uint64_t i = w * 32 + k;
             if (i >= n) break;
-            const uint64_t c = load_uint(codes, cw, false, i);
+            const uint64_t c = load_uint(codes, cw, csg, i);  // negative -> huge -> out of bounds
             oob |= c >= n_values;
             word |= (c < n_values ? uint32_t((src[c >> 3] >> (c & 7)) & 1) : 0u) << k;
         }
@@ -945,11 +950,11 @@ __global__ __launch_bounds__(kBlock) void gather_bits_kernel(uint32_t* __restric
     }
 }
 
-vxg_status launch_gather_bits(void* dst, const void* codes, int cw, uint64_t n, const uint8_t* src, uint64_t n_values,
-                              uint32_t* err, hipStream_t s) {
+vxg_status launch_gather_bits(void* dst, const void* codes, int cw, bool csg, uint64_t n, const uint8_t* src,
+                              uint64_t n_values, uint32_t* err, hipStream_t s) {
     if (n == 0) return VXG_OK;
     hipLaunchKernelGGL(gather_bits_kernel, dim3(grid_for((n + 31) / 32)), dim3(kBlock), 0, s,
-                       static_cast<uint32_t*>(dst), codes, cw, n, src, n_values, err);
+                       static_cast<uint32_t*>(dst), codes, cw, csg, n, src, n_values, err);
     return hip_check(hipGetLastError(), "gather_bits_kernel");
 }
 

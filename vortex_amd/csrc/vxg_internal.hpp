@@ -183,7 +183,7 @@ vxg_status launch_for(int width, const void* in, uint64_t n, uint64_t ref, unsig
 vxg_status launch_zigzag(int width, const void* in, uint64_t n, void* out, hipStream_t s);
 vxg_status launch_alp(int float_ptype, const void* enc, uint64_t n, double a, double b, void* out,
                       hipStream_t s);
-vxg_status launch_take(int value_width, const void* values, uint64_t n_values, int code_width,
+vxg_status launch_take(int value_width, const void* values, uint64_t n_values, int code_width, bool code_signed,
                        const void* codes, uint64_t n, void* out, uint32_t* err, hipStream_t s);
 vxg_status launch_alprd(int float_ptype, const uint16_t* left, const uint16_t* dict, unsigned dict_len,
                         unsigned right_bw, const void* right, uint64_t n, const void* exc_pos,
@@ -197,8 +197,8 @@ vxg_status launch_runend_bool(const void* ends, int ew, uint64_t n_runs, uint64_
 vxg_status launch_bytebool(const uint8_t* src, uint64_t n, void* dst, uint64_t dst_off, hipStream_t s);
 vxg_status launch_assign_bits_at(void* dst, uint64_t dst_off, const void* idx, int iw, bool isg, uint64_t ioff,
                                  uint64_t n, uint64_t len, const uint8_t* vals, hipStream_t s);
-vxg_status launch_gather_bits(void* dst, const void* codes, int cw, uint64_t n, const uint8_t* src, uint64_t n_values,
-                              uint32_t* err, hipStream_t s);
+vxg_status launch_gather_bits(void* dst, const void* codes, int cw, bool csg, uint64_t n, const uint8_t* src,
+                              uint64_t n_values, uint32_t* err, hipStream_t s);
 vxg_status launch_set_bits_at(void* dst, const void* idx, int iw, bool isg, uint64_t off, uint64_t n,
                               uint64_t len, hipStream_t s);
 vxg_status launch_sum(const void* p, int w, bool sg, uint64_t n, void* out_u64, hipStream_t s);
@@ -208,6 +208,8 @@ vxg_status fl_plain_16(int W, Epi epi, const ChunkTable& t, uint64_t g, hipStrea
 vxg_status fl_plain_32(int W, Epi epi, const ChunkTable& t, uint64_t g, hipStream_t s);
 vxg_status fl_plain_64(int W, Epi epi, const ChunkTable& t, uint64_t g, hipStream_t s);
 vxg_status fl_alp(int T, int W, Epi epi, const ChunkTable& t, uint64_t g, hipStream_t s);
+// K14: Dict(codes=BitPacked) with 8/16-byte values, thread per output (dict_rows.hip)
+vxg_status launch_dict_rows(int T, int W, int vw, const ChunkTable& tab, hipStream_t s);
 #define VXG_DECL_DICT(VW) vxg_status fl_dict_##VW(int T, int W, const ChunkTable& t, uint64_t g, hipStream_t s);
 VXG_DECL_DICT(1)
 VXG_DECL_DICT(2)
