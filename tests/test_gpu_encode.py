@@ -1,0 +1,222 @@
+"""GPU encoders (vortex_amd/gpu_encode.py, C ABI vxg_bitpack / vxg_for_bitpack / vxg_for_encode /
+vxg_gather_patches / vxg_compute_int_stats / vxg_alp_encode) against the host encoders
+(vortex_amd/encode.py over libvortex_enc.so), byte for byte: the same tree, the same metadata,
+the same packed buffers, the same patches — and decode(encode(x)) == x through the GPU decoder.
+The host encoders are themselves pinned to the reference's ALP / bit-packing known answers
+(tests/test_oracle.py, tests/golden/kat.json), which are replayed here on the GPU path.
+"""
+import json
+import struct
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import vortex_amd as V
+import vortex_amd.arrays as A
+import vortex_amd.encode as E
+import vortex_amd.gpu_encode as G
+
+pytestmark = pytest.mark.gpu
+
+GOLD = Path(__file__).resolve().parent / "golden"
+KATS = {k["name"]: k for k in json.loads((GOLD / "kat.json").read_text())}
+UT = {8: np.uint8, 16: np.uint16, 32: np.uint32, 64: np.uint64}
+ST = {8: np.int8, 16: np.int16, 32: np.int32, 64: np.int64}
+SIZES = [0, 1, 1023, 1024, 1025, 5000]
+
+
+def dev(a: np.ndarray):
+    import torch
+    a = np.ascontiguousarray(a)
+    t = torch.empty(max(a.nbytes, 16), dtype=torch.uint8, device="cuda:0")
+    if a.nbytes:
+        t[: a.nbytes].copy_(torch.from_numpy(a.view(np.uint8).reshape(-1).copy()))
+    return t[: a.nbytes]
+
+
+def host_bytes(b) -> bytes:
+    if hasattr(b, "cpu"):
+        return b.cpu().numpy().tobytes()
+    return np.ascontiguousarray(b).view(np.uint8).tobytes()
+
+
+def assert_same_tree(g: A.Array, h: A.Array, path="root"):
+    assert (g.encoding, g.len, g.dtype, g.ptype, g.nullable, g.validity) == \
+        (h.encoding, h.len, h.dtype, h.ptype, h.nullable, h.validity), path
+    assert g.meta == h.meta, path
+    assert len(g.buffers) == len(h.buffers), path
+    for i, (gb, hb) in enumerate(zip(g.buffers, h.buffers)):
+        assert host_bytes(gb) == host_bytes(hb), f"{path}.buffer[{i}]"
+    assert len(g.children) == len(h.children), path
+    for i, (gc, hc) in enumerate(zip(g.children, h.children)):
+        assert_same_tree(gc, hc, f"{path}.child[{i}]")
+
+
+def roundtrip(arr: A.Array, ctx, vals: np.ndarray):
+    import torch
+    res = V.canonicalize(arr.to(torch.device("cuda", 0)), ctx)
+    assert res.numpy().tobytes() == np.ascontiguousarray(vals).tobytes()
+
+
+# ------------------------------------------------------------------ statistics
+@pytest.mark.parametrize("T", [8, 16, 32, 64])
+@pytest.mark.parametrize("signed", [False, True])
+def test_int_stats(ctx, T, signed):
+    rng = np.random.default_rng(T + signed)
+    dt = (ST if signed else UT)[T]
+    for n in [1, 1000, 70_000]:
+        v = rng.integers(np.iinfo(dt).min, np.iinfo(dt).max, n, dtype=dt, endpoint=True)
+        v[::7] &= dt(0x70)
+        st = G.int_stats(ctx, dev(v), A.PTYPE_OF_NP[np.dtype(dt)])
+        assert (st.n, st.min, st.max) == (n, int(v.min()), int(v.max()))
+        u = v.view(UT[T]).astype(np.uint64)
+        tz = [T if x == 0 else (int(x) & -int(x)).bit_length() - 1 for x in u]
+        assert st.trailing_zeros == min(tz)
+        bw = np.array([int(x).bit_length() for x in u])
+        assert st.bit_width_freq == np.bincount(bw, minlength=T + 1).tolist()
+
+
+# ------------------------------------------------------------------ K15 pack
+@pytest.mark.parametrize("T", [8, 16, 32, 64])
+def test_bitpack_every_width(ctx, T):
+    rng = np.random.default_rng(100 + T)
+    dt = UT[T]
+    for W in range(0, T):
+        for n in SIZES:
+            v = (rng.integers(0, 2**63, n, dtype=np.uint64) & np.uint64((1 << W) - 1)).astype(dt)
+            g = G.bitpack(ctx, dev(v), f"u{T}", W)
+            assert host_bytes(g) == E.bitpack_buffer(v, W).tobytes(), (T, W, n)
+
+
+@pytest.mark.parametrize("T", [8, 16, 32, 64])
+def test_encode_bitpacked_with_patches(ctx, T):
+    rng = np.random.default_rng(200 + T)
+    dt = UT[T]
+    for n in SIZES + [33_000]:
+        v = rng.integers(0, 1 << min(T - 3, 12), n, dtype=np.uint64).astype(dt)
+        if n:
+            hot = rng.choice(n, max(1, n // 200), replace=False)
+            v[hot] = np.iinfo(dt).max - rng.integers(0, 5, hot.size).astype(dt)
+        for allow in (True, False):
+            if not allow and n and int(v.max()).bit_length() >= T:
+                continue  # the host encoder refuses T-bit packing as well
+            h = E.encode_bitpacked(v, allow_patches=allow)
+            g = G.encode_bitpacked(ctx, dev(v), f"u{T}", allow_patches=allow)
+            assert_same_tree(g, h)
+            roundtrip(g, ctx, v)
+
+
+def test_bitpacked_patch_max_kat(ctx):
+    k = KATS["bitpacked_u64_w1_patch_max"]
+    v = np.array(k["values"], dtype=np.uint64)
+    h = E.encode_bitpacked(v, bit_width=1)
+    g = G.encode_bitpacked(ctx, dev(v), "u64", bit_width=1)
+    assert_same_tree(g, h)
+    roundtrip(g, ctx, v)
+
+
+# ------------------------------------------------------------------ FoR (+ fused pack)
+def _for_cases(rng, dt, n):
+    lo, hi = np.iinfo(dt).min, np.iinfo(dt).max
+    yield rng.integers(lo, hi, n, dtype=dt, endpoint=True)                    # full range
+    yield (rng.integers(-1000, 1000, n) * 8 + 77).astype(dt) if lo < 0 else \
+        (rng.integers(0, 1000, n) * 8 + 77).astype(dt)                          # offset, no shift
+    yield (rng.integers(0, 100, n) * 16).astype(dt)                           # shift 4
+    yield np.full(n, 48, dt)                                                  # one value
+    yield np.zeros(n, dt)                                                     # ConstantArray(0)
+    if lo < 0 and n >= 2:
+        w = np.where(np.arange(n) % 2 == 0, lo, hi - 1).astype(dt)            # signed wrap, shift 1
+        yield w
+
+
+@pytest.mark.parametrize("T", [8, 16, 32, 64])
+@pytest.mark.parametrize("signed", [False, True])
+def test_for_bitpacked(ctx, T, signed):
+    rng = np.random.default_rng(300 + T + signed)
+    dt = (ST if signed else UT)[T]
+    p = A.PTYPE_OF_NP[np.dtype(dt)]
+    for n in [1, 1025, 20_000]:
+        for v in _for_cases(rng, dt, n):
+            for allow in (True, False):
+                h = E.encode_for_bitpacked(v, allow_patches=allow)
+                g = G.encode_for_bitpacked(ctx, dev(v), p, allow_patches=allow)
+                assert_same_tree(g, h)
+                if g.encoding != A.ENC["CONSTANT"]:
+                    roundtrip(g, ctx, v)
+
+
+def test_for_encode_matches_host(ctx):
+    rng = np.random.default_rng(9)
+    for dt in (np.int8, np.int32, np.uint16, np.int64):
+        v = rng.integers(np.iinfo(dt).min // 2, np.iinfo(dt).max // 2, 3000, dtype=dt) * 2
+        enc, ref, shift = E.for_compress(v)
+        g = G.for_encode(ctx, dev(v), A.PTYPE_OF_NP[np.dtype(dt)], ref, shift)
+        assert host_bytes(g) == enc.tobytes()
+
+
+# ------------------------------------------------------------------ ALP
+def _f(bits_hex, ptype):
+    fmt = "<f" if ptype == "f32" else "<d"
+    return np.array([struct.unpack(fmt, bytes.fromhex(h))[0] for h in bits_hex],
+                    dtype=np.float32 if ptype == "f32" else np.float64)
+
+
+def assert_alp_same(ctx, vals, ptype):
+    he, hf, henc, hidx, hpv = E.alp_encode(vals)
+    ge, gf, genc, gidx, gpv, m = G.alp_encode(ctx, dev(vals), ptype)
+    assert (ge, gf) == (he, hf)
+    assert host_bytes(genc) == henc.tobytes()
+    assert m == hidx.size
+    assert host_bytes(gidx) == hidx.tobytes() and host_bytes(gpv) == hpv.tobytes()
+    g = G.encode_alp(ctx, dev(vals), ptype)
+    assert_same_tree(g, E.encode_alp(vals))
+    roundtrip(g, ctx, vals)
+
+
+@pytest.mark.parametrize("name,ptype", [("alp_f32_constant_1025", "f32"), ("alp_f32_nullable", "f32"),
+                                        ("alp_f64_patched", "f64"), ("alp_f32_close_fractional", "f32")])
+def test_alp_kats(ctx, name, ptype):
+    k = KATS[name]
+    vals = _f(k["values_bits"], ptype)
+    ge, gf, genc, _, _, _ = G.alp_encode(ctx, dev(vals), ptype)
+    if "expect_e" in k:
+        assert (ge, gf) == (k["expect_e"], k["expect_f"])
+    if "expect_encoded" in k:
+        assert np.frombuffer(host_bytes(genc), dtype=np.int32 if ptype == "f32" else np.int64).tolist() == \
+            k["expect_encoded"]
+    assert_alp_same(ctx, vals, ptype)
+
+
+def test_alp_reference_doc_example(ctx):
+    import math
+    vals = np.array([1.234, 2.718, math.pi, 4.0])
+    ge, gf, *_ = G.alp_encode(ctx, dev(vals), "f64")
+    assert (ge, gf) == (16, 13)
+    assert_alp_same(ctx, vals, "f64")
+
+
+@pytest.mark.parametrize("n", [1, 31, 33, 1024, 100_000])
+def test_alp_prices_f64(ctx, n):
+    rng = np.random.default_rng(n)
+    vals = np.round(rng.uniform(1, 100000, n) * 100) / 100
+    if n > 10:
+        vals[rng.choice(n, n // 1000 + 1, replace=False)] = rng.standard_normal(n // 1000 + 1) * 1e9
+    assert_alp_same(ctx, vals, "f64")
+
+
+def test_alp_f32_and_specials(ctx):
+    rng = np.random.default_rng(5)
+    vals = (np.round(rng.uniform(-500, 500, 50_000) * 10) / 10).astype(np.float32)
+    assert_alp_same(ctx, vals, "f32")
+    sp = np.round(rng.uniform(0, 100, 4096) * 100) / 100
+    sp[[3, 100, 2000]] = [np.nan, np.inf, -np.inf]
+    sp[[5, 6]] = [1e300, -0.0]
+    assert_alp_same(ctx, sp, "f64")
+
+
+def test_alp_many_exceptions_regrows_capacity(ctx):
+    rng = np.random.default_rng(6)
+    vals = rng.standard_normal(20_000)  # nearly every value is an exception
+    vals[::2] = np.round(vals[::2] * 100) / 100
+    assert_alp_same(ctx, vals, "f64")

@@ -138,6 +138,11 @@ class VxgCanonical(C.Structure):
                 ("data_buffers", C.POINTER(VxgDataBuffer))]
 
 
+class VxgIntStats(C.Structure):
+    _fields_ = [("n", C.c_uint64), ("min_bits", C.c_uint64), ("max_bits", C.c_uint64), ("trailing_zeros", C.c_uint32),
+                ("reserved", C.c_uint32), ("bit_width_freq", C.c_uint64 * 65)]
+
+
 class VxgDictChunk(C.Structure):
     _fields_ = [("packed", C.c_void_p), ("dict_values", C.c_void_p), ("out", C.c_void_p),
                 ("n_blocks", C.c_uint64), ("len", C.c_uint64), ("dict_len", C.c_uint64)]
@@ -188,6 +193,13 @@ GPU_SIGNATURES = {
     "vxg_fsst_scratch_bytes": (U64, [U64]),
     "vxg_fsst_decode": (ST, [VP, VP, VP, UINT, VP, INT, VP, INT, VP, U64, VP, VP, VP, VP, VP]),
     "vxg_fill": (ST, [VP, UINT, VP, U64, VP, VP]),
+    "vxg_compute_int_stats": (ST, [VP, INT, VP, U64, C.POINTER(VxgIntStats), VP]),
+    "vxg_bitpack": (ST, [VP, INT, UINT, VP, U64, VP, U64, VP]),
+    "vxg_for_encode": (ST, [VP, INT, VP, U64, U64, UINT, VP, VP]),
+    "vxg_for_bitpack": (ST, [VP, INT, U64, UINT, UINT, VP, U64, VP, U64, VP]),
+    "vxg_gather_patches": (ST, [VP, INT, UINT, VP, U64, VP, VP, U64, C.POINTER(U64), VP]),
+    "vxg_alp_encode": (ST, [VP, INT, VP, U64, C.POINTER(C.c_uint8), C.POINTER(C.c_uint8), VP, VP, VP, U64,
+                            C.POINTER(U64), VP]),
 }
 
 class VxgFileColumn(C.Structure):

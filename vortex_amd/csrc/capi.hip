@@ -17,6 +17,7 @@
 #include <tuple>
 #include <vector>
 
+#include "encode_gpu.hpp"
 #include "filter.hpp"
 #include "take.hpp"
 #include "vxg_internal.hpp"
@@ -1928,6 +1929,90 @@ vxg_status vxg_take_array(vxg_ctx* ctx, const vxg_array* a, int indices_ptype, c
     if (!ptype_is_int(indices_ptype)) return set_error(VXG_ERR_INVALID_ARGUMENT, "take indices must be integers");
     Planner p(ctx, S(stream));
     return p.take(*a, indices, ptype_width(indices_ptype), ptype_is_signed(indices_ptype), n_indices, *out);
+}
+
+// ---- encoders on the GPU (encode_gpu.hip, fl_pack_impl.hpp) ----------------------------
+vxg_status vxg_compute_int_stats(vxg_ctx* ctx, int ptype, const void* values, uint64_t n, vxg_int_stats* out,
+                                 void* stream) {
+    VXG_TRY(use_device(ctx));
+    if (!out || (n && !values)) return set_error(VXG_ERR_INVALID_ARGUMENT, "null values/out");
+    if (!ptype_is_int(ptype)) return set_error(VXG_ERR_MISMATCHED_TYPES, "integer statistics need an integer ptype");
+    IntStats st{};
+    VXG_TRY(launch_int_stats(ptype_width(ptype), ptype_is_signed(ptype), values, n, &st, S(stream)));
+    std::memset(out, 0, sizeof(*out));
+    out->n = st.n;
+    out->min_bits = st.min_bits;
+    out->max_bits = st.max_bits;
+    out->trailing_zeros = st.trailing_zeros;
+    std::memcpy(out->bit_width_freq, st.bit_width_freq, sizeof(out->bit_width_freq));
+    return VXG_OK;
+}
+
+static vxg_status pack_common(vxg_ctx* ctx, int ptype, bool for_, uint64_t reference, unsigned shift,
+                              unsigned bit_width, const void* values, uint64_t n, void* packed, uint64_t packed_bytes,
+                              void* stream) {
+    VXG_TRY(use_device(ctx));
+    if (!ptype_is_int(ptype)) return set_error(VXG_ERR_MISMATCHED_TYPES, "bitpack needs an integer ptype");
+    const int T = 8 * ptype_width(ptype);
+    if (bit_width >= unsigned(T))  // bitpack_encode (bitpacking/compress.rs:22-30)
+        return set_error(VXG_ERR_INVALID_ARGUMENT,
+                         "Cannot pack -- specified bit width is greater than or equal to raw bit width");
+    const uint64_t want = ((n + 1023) / 1024) * 128ull * bit_width;
+    if (packed_bytes != want)
+        return set_error(VXG_ERR_INVALID_ARGUMENT, "packed buffer must hold " + std::to_string(want) + " bytes");
+    if (bit_width == 0 || n == 0) return VXG_OK;  // bit width 0: an empty buffer (compress.rs:86-88)
+    if (!values || !packed) return set_error(VXG_ERR_INVALID_ARGUMENT, "null values/packed");
+    if (reinterpret_cast<uintptr_t>(packed) & 15) return set_error(VXG_ERR_INVALID_ARGUMENT, "packed must be 16-byte aligned");
+    if (reinterpret_cast<uintptr_t>(values) % uint64_t(ptype_width(ptype)))
+        return set_error(VXG_ERR_INVALID_ARGUMENT, "values must be aligned to the value width");
+    const bool sgn = ptype_is_signed(ptype);
+    switch (T) {
+    case 8: return fl_pack_8(int(bit_width), for_, reference, shift, sgn, values, n, packed, S(stream));
+    case 16: return fl_pack_16(int(bit_width), for_, reference, shift, sgn, values, n, packed, S(stream));
+    case 32: return fl_pack_32(int(bit_width), for_, reference, shift, sgn, values, n, packed, S(stream));
+    default: return fl_pack_64(int(bit_width), for_, reference, shift, sgn, values, n, packed, S(stream));
+    }
+}
+
+vxg_status vxg_bitpack(vxg_ctx* ctx, int ptype, unsigned bit_width, const void* values, uint64_t n, void* packed,
+                       uint64_t packed_bytes, void* stream) {
+    return pack_common(ctx, ptype, false, 0, 0, bit_width, values, n, packed, packed_bytes, stream);
+}
+
+vxg_status vxg_for_bitpack(vxg_ctx* ctx, int ptype, uint64_t reference, unsigned shift, unsigned bit_width,
+                           const void* values, uint64_t n, void* packed, uint64_t packed_bytes, void* stream) {
+    if (shift >= unsigned(8 * ptype_width(ptype))) return set_error(VXG_ERR_INVALID_ARGUMENT, "FoR shift out of range");
+    return pack_common(ctx, ptype, true, reference, shift, bit_width, values, n, packed, packed_bytes, stream);
+}
+
+vxg_status vxg_for_encode(vxg_ctx* ctx, int ptype, const void* values, uint64_t n, uint64_t reference, unsigned shift,
+                          void* out, void* stream) {
+    VXG_TRY(use_device(ctx));
+    if (!ptype_is_int(ptype)) return set_error(VXG_ERR_MISMATCHED_TYPES, "FoR needs an integer ptype");
+    if (shift >= unsigned(8 * ptype_width(ptype))) return set_error(VXG_ERR_INVALID_ARGUMENT, "FoR shift out of range");
+    if (n && (!values || !out)) return set_error(VXG_ERR_INVALID_ARGUMENT, "null values/out");
+    if (n == 0) return VXG_OK;
+    return launch_for_encode(ptype_width(ptype), ptype_is_signed(ptype), values, n, reference, shift, out, S(stream));
+}
+
+vxg_status vxg_gather_patches(vxg_ctx* ctx, int ptype, unsigned bit_width, const void* values, uint64_t n,
+                              uint64_t* indices, void* patch_values, uint64_t cap, uint64_t* n_patches, void* stream) {
+    VXG_TRY(use_device(ctx));
+    if (!n_patches || (n && !values) || (cap && (!indices || !patch_values)))
+        return set_error(VXG_ERR_INVALID_ARGUMENT, "null argument");
+    if (!ptype_is_int(ptype)) return set_error(VXG_ERR_MISMATCHED_TYPES, "patches need an integer ptype");
+    return launch_gather_patches_gpu(ptype_width(ptype), bit_width, values, n, indices, patch_values, cap, n_patches,
+                                     S(stream));
+}
+
+vxg_status vxg_alp_encode(vxg_ctx* ctx, int float_ptype, const void* values, uint64_t n, uint8_t* e, uint8_t* f,
+                          void* encoded, uint64_t* patch_indices, void* patch_values, uint64_t cap,
+                          uint64_t* n_patches, void* stream) {
+    VXG_TRY(use_device(ctx));
+    if (!e || !f || !n_patches || (n && (!values || !encoded)) || (cap && (!patch_indices || !patch_values)))
+        return set_error(VXG_ERR_INVALID_ARGUMENT, "null argument");
+    return launch_alp_encode(float_ptype, values, n, e, f, encoded, patch_indices, patch_values, cap, n_patches,
+                             S(stream));
 }
 
 vxg_status vxg_filter_array(vxg_ctx* ctx, const vxg_array* a, const vxg_array* predicate, vxg_canonical* out,
