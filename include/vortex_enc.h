@@ -84,6 +84,12 @@ void vxe_fsst_train(const uint8_t* heap, const int64_t* offsets, uint64_t n, vxe
 uint64_t vxe_fsst_compress(const vxe_fsst_table* t, const uint8_t* heap, const int64_t* offsets,
                            uint64_t n, uint8_t* codes, uint64_t cap, int32_t* code_offsets);
 
+/* roaring/src/boolean/compress.rs:7-14 roaring_bool_encode: Bitmap of the set positions of an LSB
+ * bit buffer of len bits, run_optimize(), serialize::<Native>() (croaring 2.1.1, not vendored:
+ * its published Native/portable format restated).  Returns the serialized size; bytes are
+ * written only when it is <= cap. */
+uint64_t vxe_roaring_bool_encode(const uint8_t* bits, uint64_t len, uint8_t* out, uint64_t cap);
+
 #ifdef __cplusplus
 }
 #endif

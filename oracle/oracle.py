@@ -39,6 +39,7 @@ _SIG = {
     "vxo_runend_bool_decode": (INT, [INT, VP, SZ, SZ, INT, SZ, VP]),
     "vxo_runend_bool_encode": (SZ, [VP, SZ, VP, VP]),
     "vxo_bytebool_to_bits": (None, [VP, SZ, VP]),
+    "vxo_roaring_bool_decode": (INT, [VP, SZ, SZ, VP]),
     "vxo_fill": (None, [INT, VP, SZ, VP]),
     "vxo_fsst_decompress": (SZ, [VP, VP, VP, SZ, VP]),
     "vxo_fsst_canonicalize": (INT, [VP, VP, VP, INT, VP, INT, VP, SZ, VP, VP, C.POINTER(SZ), VP]),

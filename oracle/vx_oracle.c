@@ -434,6 +434,106 @@ void vxo_bytebool_to_bits(const uint8_t* bytes, size_t n, uint8_t* out_bits) {
     for (size_t i = 0; i < n; i++) put_bit(out_bits, i, bytes[i] != 0);
 }
 
+/* RoaringBool: croaring (2.1.1, not vendored) Native deserialization + to_bitset.  Byte 0 picks
+ * the format: 1 = u32 cardinality + that many u32 values, 2 = the portable format (cookie 12346:
+ * + u32 size, keys/cardinality-1 pairs, u32 offsets; cookie 12347 | (size-1) << 16: run-container
+ * bitset, pairs, offsets when size >= 4).  Containers: run (bit set) = u16 n_runs + (start,
+ * length-1) pairs; cardinality <= 4096 = sorted u16 values; else 1024 u64 bitset words. */
+static uint32_t rd16(const uint8_t* p) { return (uint32_t)p[0] | ((uint32_t)p[1] << 8); }
+static uint32_t rd32(const uint8_t* p) { return rd16(p) | (rd16(p + 2) << 16); }
+
+int vxo_roaring_bool_decode(const uint8_t* buf, size_t n, size_t len, uint8_t* out_bits) {
+    memset(out_bits, 0, (len + 7) / 8);
+    if (n < 1) return -1;
+    uint64_t card_total = 0;
+    if (buf[0] == 1) {
+        if (n < 5) return -1;
+        const uint32_t card = rd32(buf + 1);
+        if (5 + 4 * (uint64_t)card > n) return -1;
+        for (uint32_t i = 0; i < card; i++) {
+            const uint32_t v = rd32(buf + 5 + 4 * (size_t)i);
+            if (v < len) put_bit(out_bits, v, 1);
+        }
+        return 0;
+    }
+    if (buf[0] != 2) return -1;
+    const uint8_t* p = buf + 1;
+    const size_t m = n - 1;
+    if (m < 4) return -1;
+    const uint32_t cookie = rd32(p);
+    size_t size, pos;
+    const uint8_t* runbits = NULL;
+    int has_offsets;
+    if ((cookie & 0xFFFF) == 12347) {
+        size = (cookie >> 16) + 1;
+        runbits = p + 4;
+        pos = 4 + (size + 7) / 8;
+        has_offsets = size >= 4;
+    } else if (cookie == 12346) {
+        if (m < 8) return -1;
+        size = rd32(p + 4);
+        pos = 8;
+        has_offsets = 1;
+    } else {
+        return -1;
+    }
+    if (size > 65536 || pos + 4 * size > m) return -1;
+    const uint8_t* desc = p + pos;
+    pos += 4 * size;
+    const uint8_t* offs = NULL;
+    if (has_offsets) {
+        if (pos + 4 * size > m) return -1;
+        offs = p + pos;
+        pos += 4 * size;
+    }
+    for (size_t k = 1; k < size; k++)
+        if (rd16(desc + 4 * k) <= rd16(desc + 4 * (k - 1))) return -1; /* keys strictly increasing */
+    for (size_t k = 0; k < size; k++) {
+        const uint32_t key = rd16(desc + 4 * k), card = rd16(desc + 4 * k + 2) + 1;
+        const int run = runbits && ((runbits[k / 8] >> (k % 8)) & 1);
+        if (offs) pos = rd32(offs + 4 * k);
+        if (pos > m) return -1;
+        const uint8_t* c = p + pos;
+        const uint64_t base = (uint64_t)key << 16;
+        size_t bytes;
+        if (run) {
+            if (pos + 2 > m) return -1;
+            const uint32_t nr = rd16(c);
+            bytes = 2 + 4 * (size_t)nr;
+            if (pos + bytes > m) return -1;
+            uint64_t cnt = 0;
+            for (uint32_t r = 0; r < nr; r++) {
+                const uint32_t st = rd16(c + 2 + 4 * r), ln = rd16(c + 4 + 4 * r);
+                if (st + ln > 65535) return -1; /* a run past its container */
+                for (uint32_t x = st; x <= st + ln; x++) {
+                    if (base + x < len) put_bit(out_bits, base + x, 1);
+                    cnt++;
+                }
+            }
+            card_total += cnt;
+        } else if (card <= 4096) {
+            bytes = 2 * (size_t)card;
+            if (pos + bytes > m) return -1;
+            for (uint32_t i = 0; i < card; i++) {
+                const uint64_t v = base + rd16(c + 2 * i);
+                if (v < len) put_bit(out_bits, v, 1);
+            }
+            card_total += card;
+        } else {
+            bytes = 8192;
+            if (pos + bytes > m) return -1;
+            for (uint32_t x = 0; x < 65536; x++)
+                if ((c[x >> 3] >> (x & 7)) & 1) {
+                    if (base + x < len) put_bit(out_bits, base + x, 1);
+                    card_total++;
+                }
+        }
+        pos += bytes;
+    }
+    (void)card_total;
+    return 0;
+}
+
 void vxo_fill(int val_width, const void* scalar, size_t n, void* out) {
     for (size_t i = 0; i < n; i++) memcpy((uint8_t*)out + i * val_width, scalar, val_width);
 }

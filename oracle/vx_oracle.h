@@ -109,6 +109,10 @@ int vxo_runend_bool_decode(int ends_ptype, const void* ends, size_t n_runs, size
 size_t vxo_runend_bool_encode(const uint8_t* bits, size_t len, uint64_t* ends, int* start);
 /* bytebool/src/array.rs:138-146 into_canonical: one byte per bool -> bit (byte != 0). */
 void vxo_bytebool_to_bits(const uint8_t* bytes, size_t n, uint8_t* out_bits);
+/* roaring/src/boolean/mod.rs:69-72,127-147: Bitmap::deserialize::<Native> (croaring 2.1.1,
+ * not vendored: restated from its published format) + to_bitset, len bits (positions >= len
+ * dropped).  Returns 0, or -1 for a malformed serialization. */
+int vxo_roaring_bool_decode(const uint8_t* buf, size_t n, size_t len, uint8_t* out_bits);
 
 /* ---- Sparse / Constant canonical (array/sparse/flatten.rs:68-98; constant/canonical.rs) - */
 void vxo_fill(int val_width, const void* scalar, size_t n, void* out);

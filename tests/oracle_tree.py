@@ -221,6 +221,12 @@ def canon_bool(a: Array) -> np.ndarray:
         if rc:
             raise ValueError("runend bool decode failed")
         return np.unpackbits(out, bitorder="little")[:n].astype(bool)
+    if e == ENC["ROARING_BOOL"]:  # roaring/src/boolean/mod.rs:127-147 (croaring Native)
+        raw = np.ascontiguousarray(_buf(a.buffers[0]))
+        out = np.zeros((n + 7) // 8 + 1, np.uint8)
+        if L.vxo_roaring_bool_decode(O.p(raw), raw.size, n, O.p(out)):
+            raise ValueError("malformed croaring Native bitmap")
+        return np.unpackbits(out, bitorder="little")[:n].astype(bool)
     if e == ENC["CONSTANT"]:  # constant/canonical.rs:26-33
         return np.full(n, (not a.meta["is_null"]) and bytes(a.meta["scalar"])[0] != 0, dtype=bool)
     if e == ENC["SPARSE"]:  # sparse/flatten.rs:41-61

@@ -82,7 +82,7 @@ def test_struct_layouts_match_c(tmp_path):
 def test_encoding_ids_match_reference():
     # vortex-array/src/encoding/mod.rs:106-147
     ref = dict(BOOL=2, PRIMITIVE=3, STRUCT=4, VARBIN=5, VARBINVIEW=6, SPARSE=8, CONSTANT=9, CHUNKED=10,
-               ALP=17, BYTE_BOOL=18, DICT=20, FL_BITPACKED=21, FL_DELTA=22, FL_FOR=23, FSST=24, RUN_END=27,
+               ALP=17, BYTE_BOOL=18, DICT=20, FL_BITPACKED=21, FL_DELTA=22, FL_FOR=23, FSST=24, ROARING_BOOL=25, RUN_END=27,
                RUN_END_BOOL=28, ZIGZAG=29, ALP_RD=30)
     assert L.ENC == ref
     hdr = (ROOT / "include" / "vortex_gpu.h").read_text()

@@ -132,6 +132,9 @@ def test_every_encoding_roundtrip(typed, monkeypatch):
         "bool": A.bool_array(rng.random(n) < 0.5, validity=rng.random(n) < 0.9, bit_offset=3),
         "runend_bool": E.encode_runend_bool(np.repeat(rng.random(30) < 0.5, 100), bitpack_ends=True),
         "bytebool": A.byte_bool(rng.random(n) < 0.5),
+        "roaring_bool": E.encode_roaring_bool(rng.random(n) < 0.3),
+        "roaring_validity": A.primitive(rng.integers(0, 9, n).astype(np.int16),
+                                        validity=E.encode_roaring_bool(rng.random(n) < 0.9)),
         "sparse": A.sparse(A.primitive(np.array([3, 70, 999], np.uint64)), A.primitive(np.array([1, 2, 3], np.int32)),
                            1000, fill=-7),
         "constant_null": A.constant(None, 500, "f64"),

@@ -471,8 +471,8 @@ def ref_metadata(a: Array):
     if e == ENC["RUN_END_BOOL"]:
         return {"start": bool(m["start"]), "validity": val, "ends_ptype": PTYPES[m["ends_ptype"]],
                 "num_runs": m["num_runs"], "offset": m["offset"]}
-    if e == ENC["ZIGZAG"]:
-        return None  # unit struct ZigZagMetadata -> serde unit -> flexbuffer null
+    if e == ENC["ZIGZAG"] or e == ENC["ROARING_BOOL"]:
+        return None  # unit structs ZigZagMetadata / RoaringBoolMetadata -> flexbuffer null
     if e == ENC_STRUCT:
         return {"validity": val}
     if e == ENC_EXTENSION:

@@ -17,7 +17,7 @@ ENC_LIB_PATH = _HERE / "libvortex_enc.so"
 # ---- ids mirrored from include/vortex_gpu.h (reference encoding/mod.rs:106-147) ----------
 ENC = dict(BOOL=2, PRIMITIVE=3, STRUCT=4, VARBIN=5, VARBINVIEW=6, SPARSE=8, CONSTANT=9,
            CHUNKED=10, ALP=17, BYTE_BOOL=18, DICT=20, FL_BITPACKED=21, FL_DELTA=22, FL_FOR=23,
-           FSST=24, RUN_END=27, RUN_END_BOOL=28, ZIGZAG=29, ALP_RD=30)
+           FSST=24, ROARING_BOOL=25, RUN_END=27, RUN_END_BOOL=28, ZIGZAG=29, ALP_RD=30)
 PTYPES = ["u8", "u16", "u32", "u64", "i8", "i16", "i32", "i64", "f16", "f32", "f64"]
 PTYPE = {n: i for i, n in enumerate(PTYPES)}
 DTYPE = dict(NULL=0, BOOL=1, PRIMITIVE=2, UTF8=3, BINARY=4)
@@ -227,6 +227,7 @@ FILE_SIGNATURES = {
 
 ENC_SIGNATURES = {
     "vxe_bitpack": (U64, [INT, UINT, VP, U64, VP]),
+    "vxe_roaring_bool_encode": (U64, [VP, U64, VP, U64]),
     "vxe_best_bit_width": (UINT, [INT, VP, U64]),
     "vxe_min_patchless_bit_width": (UINT, [INT, VP, U64]),
     "vxe_gather_patches": (U64, [INT, UINT, VP, U64, VP, VP, U64]),

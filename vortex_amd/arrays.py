@@ -271,6 +271,13 @@ def byte_bool(mask, validity=None) -> Array:
                  [vchild] if vchild is not None else [])
 
 
+def roaring_bool(bitmap, length: int) -> Array:
+    """RoaringBoolArray (encodings/roaring/src/boolean/mod.rs:36-67): DType::Bool(NonNullable),
+    one buffer holding croaring's Native serialization of the set positions, no metadata."""
+    b = np.ascontiguousarray(bitmap).view(np.uint8).reshape(-1)
+    return Array(ENC["ROARING_BOOL"], length, DTYPE["BOOL"], "u8", False, VALIDITY["NON_NULLABLE"], {}, [b])
+
+
 def run_end_bool(ends: Array, start: bool, length: Optional[int] = None, offset: int = 0, validity=None) -> Array:
     """RunEndBoolArray::with_offset_and_size (encodings/runend-bool/src/array.rs:41-80): ends
     strictly increasing unsigned ints (>= 1 element); length defaults to the last end."""

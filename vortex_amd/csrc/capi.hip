@@ -1146,6 +1146,11 @@ vxg_status Planner::bools_into(const vxg_array& a, void* bits, uint64_t off) {
         return launch_runend_bool(pe, width(*e), e->len, a.meta.runendbool.offset, a.meta.runendbool.start != 0,
                                   a.len, bits, off, ctx_->c.err_word, s_);
     }
+    case VXG_ENC_ROARING_BOOL: {  // roaring/src/boolean/mod.rs:127-147 (K16, roaring.hip)
+        const vxg_buffer* b = buf(a, 0);
+        if (!b) return set_error(VXG_ERR_INVALID_ARGUMENT, "RoaringBoolArray without buffer");
+        return launch_roaring_bool(static_cast<const uint8_t*>(b->ptr), b->len, a.len, bits, off, ctx_->c.err_word, s_);
+    }
     case VXG_ENC_CONSTANT:  // constant/canonical.rs:26-33: new_set / new_unset
         if (!a.meta.constant.is_null && a.meta.constant.scalar[0])
             return launch_copy_bits(bits, off, nullptr, 0, a.len, true, s_);
@@ -1638,6 +1643,8 @@ vxg_status vxg_stream_sync(vxg_ctx* ctx, void* stream) {
         if (err & kErrRunEnd) return set_error(VXG_ERR_INVALID_ARGUMENT, "RunEnd ends do not cover the array");
         if (err & kErrFsst)
             return set_error(VXG_ERR_INVALID_ARGUMENT, "FSST codes do not decode to uncompressed_lengths");
+        if (err & kErrRoaring)
+            return set_error(VXG_ERR_INVALID_SERDE, "RoaringBool buffer is not a croaring Native bitmap");
     }
     return VXG_OK;
 }

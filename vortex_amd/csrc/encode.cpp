@@ -607,4 +607,102 @@ uint64_t vxe_fsst_compress(const vxe_fsst_table* t, const uint8_t* heap, const i
     return o;
 }
 
+uint64_t vxe_roaring_bool_encode(const uint8_t* bits, uint64_t len, uint8_t* out, uint64_t cap) {
+    // Containers of 2^16 positions keyed by the high 16 bits; a container starts as an array
+    // (<= 4096 values) or a bitset, and run_optimize turns it into runs when the run form
+    // serializes smaller (array: 2 + 4 r < 2 + 2 card; bitset: 2 + 4 r < 8192).
+    enum Kind { ARRAY, BITSET, RUN };
+    struct Cont {
+        uint16_t key;
+        Kind kind;
+        uint32_t card;
+        std::vector<uint16_t> vals;                      // array values
+        std::vector<std::pair<uint16_t, uint16_t>> runs; // (start, length - 1)
+        uint64_t words[1024];
+        uint64_t bytes() const { return kind == ARRAY ? 2ull * card : kind == BITSET ? 8192 : 2 + 4ull * runs.size(); }
+    };
+    std::vector<Cont> cs;
+    uint64_t card_total = 0;
+    for (uint64_t base = 0; base < len; base += 65536) {
+        const uint64_t end = std::min<uint64_t>(len, base + 65536);
+        Cont c{};
+        c.key = uint16_t(base >> 16);
+        for (uint64_t i = base; i < end; i++) {
+            if (!((bits[i >> 3] >> (i & 7)) & 1)) continue;
+            const uint16_t x = uint16_t(i - base);
+            c.words[x >> 6] |= 1ull << (x & 63);
+            c.vals.push_back(x);
+            if (!c.runs.empty() && uint32_t(c.runs.back().first) + c.runs.back().second + 1 == x)
+                c.runs.back().second++;
+            else
+                c.runs.push_back({x, 0});
+        }
+        c.card = uint32_t(c.vals.size());
+        if (!c.card) continue;
+        card_total += c.card;
+        c.kind = c.card <= 4096 ? ARRAY : BITSET;
+        const uint64_t run_bytes = 2 + 4ull * c.runs.size();
+        if (run_bytes < (c.kind == ARRAY ? 2 + 2ull * c.card : 8192ull)) c.kind = RUN;
+        cs.push_back(std::move(c));
+    }
+    const uint64_t size = cs.size();
+    bool has_run = false;
+    for (auto& c : cs) has_run = has_run || c.kind == RUN;
+    uint64_t header = has_run ? 4 + (size + 7) / 8 + 4 * size + (size >= 4 ? 4 * size : 0) : 8 + 8 * size;
+    uint64_t portable = header;
+    for (auto& c : cs) portable += c.bytes();
+    const uint64_t as_array = 4 * card_total + 4;
+    auto put16 = [&](uint8_t* p, uint32_t v) { p[0] = uint8_t(v); p[1] = uint8_t(v >> 8); };
+    auto put32 = [&](uint8_t* p, uint32_t v) { put16(p, v & 0xFFFF); put16(p + 2, v >> 16); };
+    if (!(portable < as_array)) {  // CROARING_SERIALIZATION_ARRAY_UINT32
+        const uint64_t total = 1 + as_array;
+        if (total > cap) return total;
+        out[0] = 1;
+        put32(out + 1, uint32_t(card_total));
+        uint64_t o = 5;
+        for (auto& c : cs)
+            for (uint16_t x : c.vals) { put32(out + o, (uint32_t(c.key) << 16) | x); o += 4; }
+        return total;
+    }
+    const uint64_t total = 1 + portable;  // CROARING_SERIALIZATION_CONTAINER + portable format
+    if (total > cap) return total;
+    out[0] = 2;
+    uint8_t* p = out + 1;
+    uint64_t o = 0;
+    if (has_run) {
+        put32(p, 12347u | uint32_t((size - 1) << 16));
+        o = 4;
+        std::memset(p + o, 0, (size + 7) / 8);
+        for (uint64_t k = 0; k < size; k++)
+            if (cs[k].kind == RUN) p[o + k / 8] |= uint8_t(1u << (k % 8));
+        o += (size + 7) / 8;
+    } else {
+        put32(p, 12346u);
+        put32(p + 4, uint32_t(size));
+        o = 8;
+    }
+    for (auto& c : cs) {
+        put16(p + o, c.key);
+        put16(p + o + 2, c.card - 1);
+        o += 4;
+    }
+    if (!has_run || size >= 4) {
+        uint32_t start = uint32_t(header);
+        for (auto& c : cs) { put32(p + o, start); o += 4; start += uint32_t(c.bytes()); }
+    }
+    for (auto& c : cs) {
+        if (c.kind == ARRAY) {
+            for (uint16_t x : c.vals) { put16(p + o, x); o += 2; }
+        } else if (c.kind == BITSET) {
+            for (int w = 0; w < 1024; w++)
+                for (int b = 0; b < 8; b++) p[o++] = uint8_t(c.words[w] >> (8 * b));
+        } else {
+            put16(p + o, uint32_t(c.runs.size()));
+            o += 2;
+            for (auto& r : c.runs) { put16(p + o, r.first); put16(p + o + 2, r.second); o += 4; }
+        }
+    }
+    return total;
+}
+
 }  // extern "C"

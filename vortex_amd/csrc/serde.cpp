@@ -773,6 +773,12 @@ struct Builder {
             children(a, {{DType::prim(unsigned_of(dt.ptype), dt.nullable), len}}, o, depth);
             break;
         }
+        case VXG_ENC_ROARING_BOOL: {  // encodings/roaring/src/boolean/mod.rs:25-67 (unit metadata,
+                                      // one buffer: croaring Native bytes, no children)
+            if (dt.kind != DType::Bool) bad("RoaringBool must have a Bool dtype");
+            children(a, {}, o, depth);
+            break;
+        }
         default:
             unsupported("no reader for encoding id " + std::to_string(enc));
         }

@@ -55,7 +55,7 @@ extern const double kF10d[24];
 extern const double kIF10d[24];
 
 // Device error word bits (set by kernels, read by vxg_check via vxg_stream_sync).
-enum : uint32_t { kErrTakeOOB = 1u, kErrPatchOOB = 2u, kErrRunEnd = 4u, kErrFsst = 8u };
+enum : uint32_t { kErrTakeOOB = 1u, kErrPatchOOB = 2u, kErrRunEnd = 4u, kErrFsst = 8u, kErrRoaring = 16u };
 
 struct Ctx {
     int device = 0;
@@ -192,6 +192,9 @@ vxg_status launch_alprd(int float_ptype, const uint16_t* left, const uint16_t* d
 vxg_status launch_copy_bits(void* dst, uint64_t dst_off, const uint8_t* src, uint64_t src_off, uint64_t n,
                             bool set_all, hipStream_t s);
 // Bool producers OR words into a zeroed LSB bit buffer at bit dst_off.
+// K16 (roaring.hip): croaring Native bitmap (n bytes) -> len bits at bit `off`.
+vxg_status launch_roaring_bool(const uint8_t* buf, uint64_t n, uint64_t len, void* bits, uint64_t off, uint32_t* err,
+                               hipStream_t s);
 vxg_status launch_runend_bool(const void* ends, int ew, uint64_t n_runs, uint64_t offset, bool start, uint64_t len,
                               void* dst, uint64_t dst_off, uint32_t* err, hipStream_t s);
 vxg_status launch_bytebool(const uint8_t* src, uint64_t n, void* dst, uint64_t dst_off, hipStream_t s);

@@ -242,6 +242,25 @@ def encode_runend_bool(mask, bitpack_ends: bool = False, validity=None) -> Array
     return A.run_end_bool(e, start, length=int(np.asarray(mask).size), validity=validity)
 
 
+def roaring_bool_encode(mask) -> np.ndarray:
+    """roaring_bool_encode (roaring/src/boolean/compress.rs:7-14): croaring Native bytes."""
+    m = np.asarray(mask, dtype=bool)
+    bits = np.packbits(m, bitorder="little")
+    if bits.size == 0:
+        bits = np.zeros(1, np.uint8)
+    lib = _lib_enc()
+    need = int(lib.vxe_roaring_bool_encode(_p(bits), m.size, None, 0))
+    out = np.zeros(max(need, 1), np.uint8)
+    lib.vxe_roaring_bool_encode(_p(bits), m.size, _p(out), out.size)
+    return out[:need]
+
+
+def encode_roaring_bool(mask) -> Array:
+    """RoaringBoolArray::encode (roaring/src/boolean/mod.rs:74-80)."""
+    m = np.asarray(mask, dtype=bool)
+    return A.roaring_bool(roaring_bool_encode(m), m.size)
+
+
 def encode_dict_strings(strings: Sequence[bytes], utf8: bool = True) -> Array:
     """dict_encode_varbin (dict/compress.rs:88-143): values = VarBin of the distinct strings in
     first-appearance order (i32 offsets), codes u64 -> BitPacked (compressors/dict.rs)."""
