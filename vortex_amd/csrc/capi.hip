@@ -614,7 +614,7 @@ vxg_status Planner::decode_chunked_primitive(const vxg_array& a, void* dst) {
             RunEndChunk& r = cs[tab.n++];
             r = runs[k];
             r.first_group = groups;
-            groups += (r.len + 2047) / 2048;
+            groups += (r.len + kRunEndSpan - 1) / kRunEndSpan;
         }
         VXG_TRY(launch_runend_chunks(w, tab, groups, s_));
     }

@@ -42,6 +42,22 @@ constexpr int kCodeLds = 6 * 1024;    // staged code bytes per tile
 constexpr int kHeapLds = 10 * 1024;   // staged output bytes per tile
 constexpr int kScanTiles = 128;       // tiles per pre-pass workgroup (= 32 FastLanes blocks)
 constexpr int kMaxDw = (kCodeLds / kTile + 3) / 4;  // code dwords per thread in the decode
+
+#ifdef VXG_FSST_STAMPS
+// Phase timing (profiling builds only): thread 0 of every decode workgroup adds the s_memtime
+// ticks of each phase of the staged path to g_fsst_stamps[phase]; [15] counts workgroups.
+__device__ unsigned long long g_fsst_stamps[16];
+#define FSST_STAMP(k)                                                                          \
+    do {                                                                                       \
+        if (threadIdx.x == 0) {                                                                \
+            const unsigned long long t_ = __builtin_amdgcn_s_memtime();                        \
+            atomicAdd(&g_fsst_stamps[k], t_ - st_prev_);                                       \
+            st_prev_ = t_;                                                                     \
+        }                                                                                      \
+    } while (0)
+#else
+#define FSST_STAMP(k) do { } while (0)
+#endif
 static_assert(kMaxDw * 4 * kTile >= kCodeLds, "segments must cover the staged codes");
 
 __device__ __forceinline__ int64_t wave_sum(int64_t x) {
@@ -307,6 +323,10 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
     __shared__ __attribute__((aligned(16))) uint32_t s_heap32[(kHeapLds + 96) / 4];
     uint8_t* const s_heap = reinterpret_cast<uint8_t*>(s_heap32);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#ifdef VXG_FSST_STAMPS
+    unsigned long long st_prev_ = tid == 0 ? __builtin_amdgcn_s_memtime() : 0ull;
+    if (tid == 0) atomicAdd(&g_fsst_stamps[15], 1ull);
+#endif
 
     const FsstChunk& ch = fsst_chunk_of<false, EXT>(tab, blockIdx.x);
     const uint64_t* __restrict__ symbols = ch.symbols;
@@ -362,6 +382,7 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
     if (lane == 0) ws_bad[wave] = bm != 0;
     int t32;
     const int rel32 = block_excl_scan32(bad ? 0 : int(my_len), ws_a, t32);
+    FSST_STAMP(0);  // prologue loads + length scan
     const bool any_bad = (ws_bad[0] | ws_bad[1] | ws_bad[2] | ws_bad[3]) != 0;
     int64_t my_rel = rel32, tile_total = t32;
     if (any_bad) my_rel = block_exclusive_scan<kTile / 64>(my_len, ws64, tile_total);  // uniform branch
@@ -397,6 +418,7 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
             for (int q = tid; q < nz; q += kTile) reinterpret_cast<uint4*>(s_heap32)[q] = make_uint4(0, 0, 0, 0);
         }
         __syncthreads();
+        FSST_STAMP(1);  // code staging + image zeroing
 
         // (c) code-parallel decode over segments of nd dwords (4 code bytes each) per thread,
         // sized so that ~all 256 threads have work.  A wave whose bytes hold no escape (255)
@@ -469,6 +491,7 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
         }
         int dec_total;
         const int seg_rel = block_excl_scan32(int(sum8 >> 3), ws_b, dec_total);
+        FSST_STAMP(2);  // pass 1 + segment scan
         if (tid == 0 && dec_total != ttot)
             __hip_atomic_fetch_or(err, kErrFsst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // pass 2: every code ORs its (zero-padded) bytes into <= 3 dwords of the zeroed image:
@@ -523,6 +546,7 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
             }
         }
         __syncthreads();
+        FSST_STAMP(3);  // pass 2 (image ORs)
         // (d) copy-out of [tile_out0, tile_out0 + ttot): the image sits at the same offset mod 16
         // as its destination, so whole aligned chunks move as ds_read_b128 + 16-byte stores;
         // the ragged first/last chunk byte by byte (shared with the neighbouring tiles)
@@ -542,6 +566,7 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
         if (live)
             views[i] = valid ? lds_view(s_heap32, hshift + int(my_rel), vlen, uint32_t(tile_out0 + my_rel), bidx)
                              : make_uint4(0, 0, 0, 0);
+        FSST_STAMP(4);  // copy-out + views (issue)
     } else {
         // direct path: per-string decode straight into HBM (codes of string i are
         // [offs[i], offs[i+1]); each must decode to exactly lengths[i] bytes)
@@ -694,3 +719,17 @@ vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint
 }
 
 }  // namespace vxg
+
+#ifdef VXG_FSST_STAMPS
+extern "C" vxg_status vxg_debug_fsst_stamps(unsigned long long* out16, int reset) {
+    if (out16) {
+        const vxg_status st = vxg::hip_check(hipMemcpyFromSymbol(out16, HIP_SYMBOL(vxg::g_fsst_stamps), 16 * 8), "stamps");
+        if (st != VXG_OK) return st;
+    }
+    if (reset) {
+        unsigned long long z[16] = {0};
+        return vxg::hip_check(hipMemcpyToSymbol(HIP_SYMBOL(vxg::g_fsst_stamps), z, sizeof z), "stamps reset");
+    }
+    return VXG_OK;
+}
+#endif

@@ -572,12 +572,64 @@ __device__ __forceinline__ uint64_t runend_first_gt(const void* ends, int ew, ui
     return bm ? lo + uint64_t(__ffsll(bm) - 1) : hi;
 }
 
+// First run r in [lo, hi) with ends[r] - offset > j (hi if none), one wave, wave-uniform result.
+__device__ __forceinline__ uint64_t runend_first_gt_in(const void* ends, int ew, uint64_t offset, uint64_t lo,
+                                                       uint64_t hi, uint64_t j) {
+    const int lane = threadIdx.x & 63;
+    while (hi - lo > 64) {
+        const uint64_t step = (hi - lo + 63) / 64;
+        const uint64_t idx = lo + step * uint64_t(lane);
+        const bool gt = idx < hi ? load_uint(ends, ew, false, idx) - offset > j : true;
+        const unsigned long long bm = __ballot(gt);
+        const int k = bm ? __ffsll(bm) - 1 : 64;
+        const uint64_t nlo = k == 0 ? lo : lo + step * uint64_t(k - 1) + 1;
+        const uint64_t nhi = k == 64 ? hi : (lo + step * uint64_t(k) < hi ? lo + step * uint64_t(k) : hi);
+        lo = nlo;
+        hi = nhi;
+    }
+    const uint64_t idx = lo + uint64_t(lane);
+    const bool gt = idx < hi ? load_uint(ends, ew, false, idx) - offset > j : false;
+    const unsigned long long bm = __ballot(gt);
+    return bm ? lo + uint64_t(__ffsll(bm) - 1) : hi;
+}
+
+// The run holding output j: an interpolated guess (j * n_runs / len) probed by one wave at 64
+// points 64 runs apart, then the 64 runs of the bracket -- two dependent loads when the run
+// lengths are near-uniform (the usual case), a 64-ary search of the rest otherwise.
+__device__ __forceinline__ uint64_t runend_locate(const void* ends, int ew, uint64_t offset, uint64_t n_runs,
+                                                  uint64_t len, uint64_t j) {
+    const int lane = threadIdx.x & 63;
+    constexpr uint64_t S = 64;
+    const uint64_t guess = uint64_t(double(j) / double(len) * double(n_runs));
+    const uint64_t base = guess > 32 * S ? guess - 32 * S : 0;
+    if (base >= n_runs) return runend_first_gt_in(ends, ew, offset, 0, n_runs, j);
+    const uint64_t idx = base + S * uint64_t(lane);
+    const bool gt = idx < n_runs ? load_uint(ends, ew, false, idx) - offset > j : true;
+    const unsigned long long bm = __ballot(gt);
+    if (bm & 1ull) return base == 0 ? 0 : runend_first_gt_in(ends, ew, offset, 0, base + 1, j);
+    if (bm == 0) return runend_first_gt_in(ends, ew, offset, base + 63 * S + 1, n_runs, j);
+    const int k = __ffsll(bm) - 1;  // probe k is > j, probe k - 1 is not
+    const uint64_t lo = base + S * uint64_t(k - 1) + 1;
+    const uint64_t hi = base + S * uint64_t(k) < n_runs ? base + S * uint64_t(k) + 1 : n_runs;
+    return runend_first_gt_in(ends, ew, offset, lo, hi, j);
+}
+
+// A workgroup expands outputs [j0, j0 + kRunEndSpan) of one chunk:
+//   * wave 0 locates r0, the run holding j0 (runend_locate); the chunk's last end is checked
+//     to cover the chunk (an independent load);
+//   * every thread loads the ends of 4 runs at once (r0 + t + 256 i): the run after run r starts
+//     at ends[r] - offset, and each start inside the range records its run index (a run head) in
+//     LDS -- repeated while the last start is still inside, so no search for the range's end;
+//   * an inclusive max-scan fills the positions between heads;
+//   * outputs are written coalesced: out[j] = values[run(j)] (non-temporal).
+// Ends are trimmed as the reference does: min(ends[r] - offset, len) (runend/compress.rs:140).
 template <typename V>
 __global__ __launch_bounds__(kBlock) void runend_chunks_kernel(RunEndTable tab) {
-    constexpr int SPAN = 2048, PER = SPAN / kBlock;
+    constexpr int SPAN = int(kRunEndSpan), PER = SPAN / kBlock;
     __shared__ uint32_t s_head[SPAN];
     __shared__ uint32_t s_wmax[kBlock / 64];
-    __shared__ uint64_t s_r[2];
+    __shared__ uint64_t s_r0;
+    __shared__ int s_bad;
     const uint64_t g = blockIdx.x;
     RunEndChunk c;  // this workgroup's chunk: kernarg table (binary search) or a plan's device table
     if (tab.ext) {
@@ -595,26 +647,34 @@ __global__ __launch_bounds__(kBlock) void runend_chunks_kernel(RunEndTable tab) 
     const int ew = int(c.ends_width), tid = threadIdx.x;
     const uint64_t j0 = (g - c.first_group) * SPAN;
     const int jn = int(c.len - j0 < uint64_t(SPAN) ? c.len - j0 : uint64_t(SPAN));
+    const uint64_t jend = j0 + uint64_t(jn);
     if (tid < 64) {
-        const uint64_t r0 = runend_first_gt(c.ends, ew, c.offset, c.n_runs, j0);
-        const uint64_t r1 = runend_first_gt(c.ends, ew, c.offset, c.n_runs, j0 + uint64_t(jn) - 1);
-        if (tid == 0) {
-            s_r[0] = r0;
-            s_r[1] = r1;
-        }
+        const uint64_t r0 = runend_locate(c.ends, ew, c.offset, c.n_runs, c.len, j0);
+        if (tid == 0) s_r0 = r0;
+    } else if (tid == 64) {  // the last run must reach the chunk's end
+        s_bad = c.n_runs == 0 || load_uint(c.ends, ew, false, c.n_runs - 1) - c.offset < c.len;
     }
 #pragma unroll
     for (int k = 0; k < PER; k++) s_head[tid + k * kBlock] = 0;
     __syncthreads();
-    const uint64_t r0 = s_r[0], r1 = s_r[1];
-    if (r1 >= c.n_runs) {  // the ends do not reach the last output of this range
+    if (s_bad) {  // the ends do not reach the end of the array
         if (tid == 0) __hip_atomic_fetch_or(tab.err, kErrRunEnd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
     }
-    // run heads: run r0 + k starts at max(trimmed end of r0 + k - 1, j0)
-    for (uint64_t k = 1 + uint64_t(tid); k <= r1 - r0; k += kBlock) {
-        const uint64_t st = load_uint(c.ends, ew, false, r0 + k - 1) - c.offset;  // > j0 by construction
-        s_head[st - j0] = uint32_t(k);
+    const uint64_t r0 = s_r0;
+    // run heads: run r + 1 starts at ends[r] - offset (> j0 for r >= r0)
+    constexpr int Q = 4;
+    for (uint64_t rb = r0;; rb += uint64_t(Q) * kBlock) {
+        uint64_t st[Q];
+#pragma unroll
+        for (int q = 0; q < Q; q++) {
+            const uint64_t r = rb + uint64_t(q) * kBlock + uint64_t(tid);
+            st[q] = r + 1 < c.n_runs ? load_uint(c.ends, ew, false, r) - c.offset : ~0ull;
+        }
+#pragma unroll
+        for (int q = 0; q < Q; q++)
+            if (st[q] < jend) s_head[st[q] - j0] = uint32_t(rb + uint64_t(q) * kBlock + uint64_t(tid) + 1 - r0);
+        if (!__syncthreads_or(st[Q - 1] < jend)) break;
     }
     __syncthreads();
     // inclusive max-scan of s_head: thread t owns entries [PER t, PER t + PER)

@@ -234,9 +234,10 @@ struct RunEndChunk {
     uint64_t n_runs;
     uint64_t offset;
     uint64_t len;
-    uint64_t first_group;  // first workgroup of this chunk (2048 outputs per workgroup)
+    uint64_t first_group;  // first workgroup of this chunk (kRunEndSpan outputs per workgroup)
     uint32_t ends_width;
 };
+constexpr uint64_t kRunEndSpan = 4096;
 constexpr int kRunEndArgChunks = 48;
 struct RunEndTable {
     RunEndChunk c[kRunEndArgChunks];
