@@ -38,12 +38,11 @@ def main():
     import vortex_amd.arrays as A
     ctx = V.Context(0)
     fn = ctx.lib.vxg_debug_fsst_stamps
-    fn.restype, fn.argtypes = C.c_int, [C.c_void_p, C.c_int]
+    fn.restype, fn.argtypes = C.c_int, [C.c_void_p, C.c_uint64, C.c_int]
     rng = np.random.default_rng(0)
     if a.workload == "c4":
         arr, _ = bench.make_c4(rng, 1, 0)
-        node_arr = arr.to(torch.device("cuda", 0))
-        plan = A.Plan([node_arr], ctx)
+        plan = A.Plan([arr.to(torch.device("cuda", 0))], ctx)
     else:
         from vortex_amd.file import DeviceColumns, VortexFile
         host = torch.from_numpy(bench.c5_file(None, 0)).pin_memory()
@@ -54,20 +53,28 @@ def main():
     for _ in range(3):
         plan.launch()
     ctx.sync()
-    fn(None, 1)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(a.reps):
         plan.launch()
     e1.record()
     torch.cuda.synchronize()
-    buf = (C.c_ulonglong * 16)()
-    fn(buf, 0)
-    wgs = buf[15]
-    out = {"workload": a.workload, "step_ms": round(e0.elapsed_time(e1) / a.reps, 4), "workgroups": wgs // a.reps,
-           "ticks_per_wg": {p: round(buf[i] / max(wgs, 1), 1) for i, p in enumerate(PHASES)}}
-    tot = sum(out["ticks_per_wg"].values())
-    out["share"] = {p: round(v / tot, 3) for p, v in out["ticks_per_wg"].items()}
+    n = 1 << 18
+    rec = np.zeros((n, 8), np.uint64)
+    fn(fn.argtypes[0](rec.ctypes.data), n, 1)  # the last replay's records, then reset
+    plan.launch()
+    ctx.sync()
+    fn(fn.argtypes[0](rec.ctypes.data), n, 0)  # one clean replay
+    r = rec[rec[:, 7] == 1].astype(np.int64)
+    d = np.diff(r[:, :6], axis=1)
+    dur = r[:, 5] - r[:, 0]
+    span = int(r[:, 5].max() - r[:, 0].min())
+    out = {"workload": a.workload, "step_ms_stamped": round(e0.elapsed_time(e1) / a.reps, 4),
+           "staged_workgroups": int(r.shape[0]), "span_ticks": span,
+           "mean_wg_ticks": round(float(dur.mean()), 1), "concurrency": round(float(dur.sum()) / max(span, 1), 1),
+           "phase_mean_ticks": {p: round(float(d[:, k].mean()), 1) for k, p in enumerate(PHASES)},
+           "phase_median_ticks": {p: int(np.median(d[:, k])) for k, p in enumerate(PHASES)}}
+    out["share"] = {p: round(float(d[:, k].sum() / dur.sum()), 3) for k, p in enumerate(PHASES)}
     print(json.dumps(out), flush=True)
 
 

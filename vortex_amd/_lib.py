@@ -22,7 +22,7 @@ PTYPES = ["u8", "u16", "u32", "u64", "i8", "i16", "i32", "i64", "f16", "f32", "f
 PTYPE = {n: i for i, n in enumerate(PTYPES)}
 DTYPE = dict(NULL=0, BOOL=1, PRIMITIVE=2, UTF8=3, BINARY=4)
 VALIDITY = dict(NON_NULLABLE=0, ALL_VALID=1, ALL_INVALID=2, ARRAY=3)
-ABI_VERSION = 4  # VXG_ABI_VERSION
+ABI_VERSION = 5  # VXG_ABI_VERSION
 STATUS = {0: "OK", 1: "OutOfBounds", 2: "ComputeError", 3: "InvalidArgument", 4: "InvalidSerde",
           5: "NotImplemented", 6: "MismatchedTypes", 7: "AssertionFailed", 8: "HipError",
           9: "OutOfMemory"}
@@ -162,6 +162,8 @@ GPU_SIGNATURES = {
     "vxg_last_error": (C.c_char_p, []),
     "vxg_alloc": (ST, [VP, U64, C.POINTER(VP)]),
     "vxg_free": (ST, [VP, VP]),
+    "vxg_host_alloc": (ST, [VP, U64, C.POINTER(VP)]),
+    "vxg_host_free": (ST, [VP, VP]),
     "vxg_memcpy_h2d": (ST, [VP, VP, VP, U64, VP]),
     "vxg_memcpy_d2h": (ST, [VP, VP, VP, U64, VP]),
     "vxg_memcpy_d2d": (ST, [VP, VP, VP, U64, VP]),

@@ -1616,6 +1616,16 @@ vxg_status vxg_free(vxg_ctx* ctx, void* dptr) {
     return hip_check(hipFree(dptr), "hipFree");
 }
 
+vxg_status vxg_host_alloc(vxg_ctx* ctx, uint64_t bytes, void** hptr) {
+    VXG_TRY(use_device(ctx));
+    return hip_check(hipHostMalloc(hptr, bytes ? bytes : 16, hipHostMallocDefault), "hipHostMalloc");
+}
+
+vxg_status vxg_host_free(vxg_ctx* ctx, void* hptr) {
+    VXG_TRY(use_device(ctx));
+    return hip_check(hipHostFree(hptr), "hipHostFree");
+}
+
 vxg_status vxg_memcpy_h2d(vxg_ctx* ctx, void* dst, const void* src, uint64_t bytes, void* stream) {
     VXG_TRY(use_device(ctx));
     return hip_check(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, S(stream)), "h2d");

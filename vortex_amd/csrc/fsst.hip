@@ -44,16 +44,14 @@ constexpr int kScanTiles = 128;       // tiles per pre-pass workgroup (= 32 Fast
 constexpr int kMaxDw = (kCodeLds / kTile + 3) / 4;  // code dwords per thread in the decode
 
 #ifdef VXG_FSST_STAMPS
-// Phase timing (profiling builds only): thread 0 of every decode workgroup adds the s_memtime
-// ticks of each phase of the staged path to g_fsst_stamps[phase]; [15] counts workgroups.
-__device__ unsigned long long g_fsst_stamps[16];
+// Phase timing (profiling builds only): thread 0 of decode workgroup g records s_memtime at the
+// kernel entry and at the end of each phase of the staged path into g_fsst_stamps[g][0..5]
+// (plain vector stores, one 64-byte record per workgroup: no shared counters to contend on).
+constexpr uint32_t kStampWgs = 1u << 18;
+__device__ unsigned long long g_fsst_stamps[kStampWgs][8];
 #define FSST_STAMP(k)                                                                          \
     do {                                                                                       \
-        if (threadIdx.x == 0) {                                                                \
-            const unsigned long long t_ = __builtin_amdgcn_s_memtime();                        \
-            atomicAdd(&g_fsst_stamps[k], t_ - st_prev_);                                       \
-            st_prev_ = t_;                                                                     \
-        }                                                                                      \
+        if (threadIdx.x == 0) st_t_[(k) + 1] = __builtin_amdgcn_s_memtime();                   \
     } while (0)
 #else
 #define FSST_STAMP(k) do { } while (0)
@@ -324,8 +322,8 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
     uint8_t* const s_heap = reinterpret_cast<uint8_t*>(s_heap32);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 #ifdef VXG_FSST_STAMPS
-    unsigned long long st_prev_ = tid == 0 ? __builtin_amdgcn_s_memtime() : 0ull;
-    if (tid == 0) atomicAdd(&g_fsst_stamps[15], 1ull);
+    unsigned long long st_t_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (tid == 0) st_t_[0] = __builtin_amdgcn_s_memtime();
 #endif
 
     const FsstChunk& ch = fsst_chunk_of<false, EXT>(tab, blockIdx.x);
@@ -567,6 +565,13 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
             views[i] = valid ? lds_view(s_heap32, hshift + int(my_rel), vlen, uint32_t(tile_out0 + my_rel), bidx)
                              : make_uint4(0, 0, 0, 0);
         FSST_STAMP(4);  // copy-out + views (issue)
+#ifdef VXG_FSST_STAMPS
+        if (tid == 0 && blockIdx.x < kStampWgs) {
+            st_t_[7] = 1;  // staged path
+#pragma unroll
+            for (int k = 0; k < 8; k++) g_fsst_stamps[blockIdx.x][k] = st_t_[k];
+        }
+#endif
     } else {
         // direct path: per-string decode straight into HBM (codes of string i are
         // [offs[i], offs[i+1]); each must decode to exactly lengths[i] bytes)
@@ -721,14 +726,20 @@ vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint
 }  // namespace vxg
 
 #ifdef VXG_FSST_STAMPS
-extern "C" vxg_status vxg_debug_fsst_stamps(unsigned long long* out16, int reset) {
-    if (out16) {
-        const vxg_status st = vxg::hip_check(hipMemcpyFromSymbol(out16, HIP_SYMBOL(vxg::g_fsst_stamps), 16 * 8), "stamps");
+extern "C" vxg_status vxg_debug_fsst_stamps(unsigned long long* out, uint64_t n_wgs, int reset) {
+    // out: n_wgs records of 8 u64 (n_wgs <= 2^18); reset zeroes the device table
+    if (out && n_wgs) {
+        const uint64_t n = n_wgs < vxg::kStampWgs ? n_wgs : vxg::kStampWgs;
+        const vxg_status st = vxg::hip_check(hipMemcpyFromSymbol(out, HIP_SYMBOL(vxg::g_fsst_stamps), n * 64), "stamps");
         if (st != VXG_OK) return st;
     }
     if (reset) {
-        unsigned long long z[16] = {0};
-        return vxg::hip_check(hipMemcpyToSymbol(HIP_SYMBOL(vxg::g_fsst_stamps), z, sizeof z), "stamps reset");
+        void* p = nullptr;
+        vxg_status st = vxg::hip_check(hipGetSymbolAddress(&p, HIP_SYMBOL(vxg::g_fsst_stamps)), "stamps addr");
+        if (st != VXG_OK) return st;
+        st = vxg::hip_check(hipMemset(p, 0, sizeof(vxg::g_fsst_stamps)), "stamps reset");
+        if (st != VXG_OK) return st;
+        return vxg::hip_check(hipDeviceSynchronize(), "stamps reset sync");
     }
     return VXG_OK;
 }
