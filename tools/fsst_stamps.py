@@ -28,6 +28,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", default="c4")
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--ablate", default="", help="comma list of ablation masks to time (output wrong)")
     a = ap.parse_args()
     if "stamps" not in os.environ.get("VXG_GPU_LIB", ""):
         sys.exit("set VXG_GPU_LIB to the stamps build (make -C vortex_amd/csrc stamps)")
@@ -59,6 +60,24 @@ def main():
         plan.launch()
     e1.record()
     torch.cuda.synchronize()
+    if a.ablate:
+        ab = ctx.lib.vxg_debug_fsst_ablate
+        ab.restype, ab.argtypes = C.c_int, [C.c_uint32]
+        res = {}
+        for mask in [int(x) for x in a.ablate.split(",")]:
+            ab(mask)
+            for _ in range(3):
+                plan.launch()
+            ctx.sync()
+            e0.record()
+            for _ in range(a.reps):
+                plan.launch()
+            e1.record()
+            torch.cuda.synchronize()
+            res[mask] = round(e0.elapsed_time(e1) / a.reps, 4)
+        ab(0)
+        print(json.dumps({"workload": a.workload, "ablation_step_ms": res,
+                          "bits": "1=pass2 2=pass1+scan 4=views 8=copy-out 16=code loads"}), flush=True)
     n = 1 << 18
     rec = np.zeros((n, 8), np.uint64)
     fn(fn.argtypes[0](rec.ctypes.data), n, 1)  # the last replay's records, then reset

@@ -24,6 +24,16 @@ SCALARS = {"uint8_t": "u8", "uint16_t": "u16", "uint32_t": "u32", "uint64_t": "u
            "unsigned long long": "u64"}
 
 
+RUST_KEYWORDS = {"as", "async", "await", "box", "break", "const", "continue", "crate", "dyn", "else", "enum", "extern",
+                 "false", "fn", "for", "if", "impl", "in", "let", "loop", "match", "mod", "move", "mut", "pub", "ref",
+                 "return", "self", "static", "struct", "super", "trait", "true", "type", "unsafe", "use", "where",
+                 "while"}
+
+
+def ident(name: str) -> str:
+    return "r#" + name if name in RUST_KEYWORDS else name
+
+
 def strip_comments(s: str) -> str:
     s = re.sub(r"/\*.*?\*/", " ", s, flags=re.S)
     return re.sub(r"//[^\n]*", " ", s)
@@ -69,7 +79,7 @@ def fields(body: str, known: set, owner: str, extra: list) -> list[str]:
             continue
         ctype, name, n = split_decl(d)
         rt = rust_type(ctype, known)
-        out.append(f"    pub {name}: {'[' + rt + '; ' + n + ']' if n else rt},")
+        out.append(f"    pub {ident(name)}: {'[' + rt + '; ' + n + ']' if n else rt},")
     return out
 
 
@@ -90,7 +100,6 @@ def generate() -> str:
             items.append(f"pub const {m.group(1)}: c_int = {m.group(2)};\n")
         src = re.sub(r"^\s*#[^\n]*", " ", src, flags=re.M)
         src = src.replace('extern "C" {', " ")
-        pos = 0
         toks = re.compile(r"typedef\s+enum\s+(\w+)\s*\{(.*?)\}\s*(\w+)\s*;|"
                           r"enum\s*\{(.*?)\}\s*;|"
                           r"typedef\s+(struct|union)\s+(\w+)\s*\{((?:[^{}]|\{[^{}]*\})*)\}\s*(\w+)\s*;|"
@@ -124,14 +133,17 @@ def generate() -> str:
                 if args.strip() != "void":
                     for a in args.split(","):
                         ctype, an, n = split_decl(a)
-                        ra.append(f"{an}: {rust_type(ctype, known)}")
+                        ra.append(f"{ident(an)}: {rust_type(ctype, known)}")
                 ret_s = "" if rret == "c_void" else f" -> {rret}"
                 fns.append(f"    pub fn {name}({', '.join(ra)}){ret_s};\n")
     head = ("// @generated by tools/gen_ffi_rs.py from include/vortex_gpu.h and include/vortex_file.h.\n"
             "// Do not edit: regenerate with `python tools/gen_ffi_rs.py`.\n"
             "#![allow(non_camel_case_types, non_upper_case_globals, dead_code)]\n\n"
             "use std::os::raw::{c_char, c_int, c_uint, c_void};\n\n")
-    return head + "\n".join(items) + '\n#[link(name = "vortex_gpu")]\nextern "C" {\n' + "".join(fns) + "}\n"
+    body = ""
+    for it in items:  # constants one per line, a blank line around type definitions
+        body += it if it.startswith("pub const") or it.startswith("pub type") else "\n" + it
+    return head + body + '\n#[link(name = "vortex_gpu")]\nextern "C" {\n' + "".join(fns) + "}\n"
 
 
 def main():

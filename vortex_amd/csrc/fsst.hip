@@ -53,8 +53,14 @@ __device__ unsigned long long g_fsst_stamps[kStampWgs][8];
     do {                                                                                       \
         if (threadIdx.x == 0) st_t_[(k) + 1] = __builtin_amdgcn_s_memtime();                   \
     } while (0)
+// Ablation mask (profiling builds only; the output is then WRONG): bit 0 skips pass 2, bit 1
+// skips pass 1 + its scan, bit 2 skips the views, bit 3 skips the heap copy-out, bit 4 skips
+// the code staging loads.  Set with vxg_debug_fsst_ablate.
+__device__ uint32_t g_fsst_abl;
+#define FSST_ABL(bit) (((abl_) >> (bit)) & 1u)
 #else
 #define FSST_STAMP(k) do { } while (0)
+#define FSST_ABL(bit) false
 #endif
 static_assert(kMaxDw * 4 * kTile >= kCodeLds, "segments must cover the staged codes");
 
@@ -324,6 +330,7 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
 #ifdef VXG_FSST_STAMPS
     unsigned long long st_t_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (tid == 0) st_t_[0] = __builtin_amdgcn_s_memtime();
+    const uint32_t abl_ = g_fsst_abl;
 #endif
 
     const FsstChunk& ch = fsst_chunk_of<false, EXT>(tab, blockIdx.x);
@@ -407,6 +414,10 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
             const uint4* a0 = reinterpret_cast<const uint4*>(ga - uintptr_t(cshift));
             const int nchunk = (span + 15) >> 4;
             for (int q = tid; q < nchunk; q += kTile) {
+                if (FSST_ABL(4)) {
+                    *reinterpret_cast<uint4*>(s_codes + 16 * q) = make_uint4(0x01010101u * uint32_t(q & 0x7F), 0, 0, 0);
+                    continue;
+                }
                 const uint4 x = a0[q];
                 uint4 y = make_uint4(0, 0, 0, 0);
                 if (cshift != 0 && 16 * (q + 1) - cshift < span) y = a0[q + 1];
@@ -443,12 +454,15 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
                 slow |= (((x & 0x7F7F7F7Fu) + 0x01010101u) & x & 0x80808080u) != 0;  // a 0xFF byte
             }
         }
-        const bool fast = __ballot(slow) == 0;  // wave-uniform
+        const bool fast = __ballot(slow) == 0 || FSST_ABL(1);  // wave-uniform
         // pass 1: pk[d] byte j = decoded length x 8 of code byte 4d + j (0 for literals and
         // bytes past the tile)
         uint32_t pk[kMaxDw];
         uint32_t sum8 = 0;
-        if (fast) {
+        if (FSST_ABL(1)) {
+#pragma unroll
+            for (int d = 0; d < kMaxDw; d++) pk[d] = 0x18181818u;
+        } else if (fast) {
 #pragma unroll
             for (int d = 0; d < kMaxDw; d++) {
                 pk[d] = 0;
@@ -488,7 +502,13 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
             }
         }
         int dec_total;
-        const int seg_rel = block_excl_scan32(int(sum8 >> 3), ws_b, dec_total);
+        int seg_rel;
+        if (FSST_ABL(1)) {
+            seg_rel = tid * 27;
+            dec_total = ttot;
+        } else {
+            seg_rel = block_excl_scan32(int(sum8 >> 3), ws_b, dec_total);
+        }
         FSST_STAMP(2);  // pass 1 + segment scan
         if (tid == 0 && dec_total != ttot)
             __hip_atomic_fetch_or(err, kErrFsst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -497,7 +517,7 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
         // symbol reads of a dword issued first, no selects.  Codes past the tile (fast path,
         // last segment) OR into the image slack after the tile.  A tile whose codes do not
         // decode to its length sum (corrupt input, flagged above) is not written.
-        if (dec_total == ttot) {
+        if (dec_total == ttot && !FSST_ABL(0)) {
             uint32_t o8 = uint32_t(hshift + seg_rel) << 3;  // bit position in the image
             auto put = [&](uint64_t m, uint32_t L8) {
                 const uint32_t sh = o8 & 24u;
@@ -550,7 +570,7 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
         // the ragged first/last chunk byte by byte (shared with the neighbouring tiles)
         {
             uint8_t* const gbase = heap + (tile_out0 - hshift);
-            const int nchunk = (hshift + ttot + 15) >> 4;
+            const int nchunk = FSST_ABL(3) ? 0 : (hshift + ttot + 15) >> 4;
             for (int q = tid; q < nchunk; q += kTile) {
                 const int lb = 16 * q;
                 if (lb >= hshift && lb + 16 <= hshift + ttot) {
@@ -561,7 +581,9 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
                 }
             }
         }
-        if (live)
+        if (live && FSST_ABL(2))
+            views[i] = make_uint4(0, 0, 0, 0);
+        else if (live)
             views[i] = valid ? lds_view(s_heap32, hshift + int(my_rel), vlen, uint32_t(tile_out0 + my_rel), bidx)
                              : make_uint4(0, 0, 0, 0);
         FSST_STAMP(4);  // copy-out + views (issue)
@@ -726,6 +748,10 @@ vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint
 }  // namespace vxg
 
 #ifdef VXG_FSST_STAMPS
+extern "C" vxg_status vxg_debug_fsst_ablate(uint32_t mask) {
+    return vxg::hip_check(hipMemcpyToSymbol(HIP_SYMBOL(vxg::g_fsst_abl), &mask, sizeof mask), "ablate");
+}
+
 extern "C" vxg_status vxg_debug_fsst_stamps(unsigned long long* out, uint64_t n_wgs, int reset) {
     // out: n_wgs records of 8 u64 (n_wgs <= 2^18); reset zeroes the device table
     if (out && n_wgs) {
