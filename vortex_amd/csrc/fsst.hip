@@ -58,7 +58,9 @@ __device__ unsigned long long g_fsst_stamps[kStampWgs][8];
 // the code staging loads.  Set with vxg_debug_fsst_ablate.
 __device__ uint32_t g_fsst_abl;
 #define FSST_ABL(bit) (((abl_) >> (bit)) & 1u)
+#define FSST_ANY_ABL (abl_ != 0u)
 #else
+#define FSST_ANY_ABL false
 #define FSST_STAMP(k) do { } while (0)
 #define FSST_ABL(bit) false
 #endif
@@ -510,7 +512,7 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
             seg_rel = block_excl_scan32(int(sum8 >> 3), ws_b, dec_total);
         }
         FSST_STAMP(2);  // pass 1 + segment scan
-        if (tid == 0 && dec_total != ttot)
+        if (tid == 0 && dec_total != ttot && !FSST_ANY_ABL)
             __hip_atomic_fetch_or(err, kErrFsst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // pass 2: every code ORs its (zero-padded) bytes into <= 3 dwords of the zeroed image:
         // (w1:w0) = sym << 8(o & 3) and w2 = the bytes shifted past them.  Fast path: all 4
