@@ -111,7 +111,7 @@ fn scalar_bytes(r: &Reader<&[u8]>, dtype: &DType) -> VortexResult<(bool, [u8; 16
         DType::Primitive(p, _) => {
             let w = ptype_width(*p);
             let bytes: [u8; 8] = match p {
-                PType::F32 => (r.as_f64() as f32).to_bits().to_le_bytes().map(|b| b).iter().chain([0u8; 4].iter()).copied().collect::<Vec<_>>().try_into().unwrap_or([0; 8]),
+                PType::F32 => (u64::from((r.as_f64() as f32).to_bits())).to_le_bytes(),
                 PType::F64 => r.as_f64().to_bits().to_le_bytes(),
                 PType::F16 => (vortex_dtype::half::f16::from_f64(r.as_f64()).to_bits() as u64).to_le_bytes(),
                 PType::I8 | PType::I16 | PType::I32 | PType::I64 => r.as_i64().to_le_bytes(),
@@ -135,6 +135,8 @@ pub(crate) fn convert(
     let mut m: ffi::vxg_meta = unsafe { std::mem::zeroed() };
     let mut validity = ffi::VXG_VALIDITY_NON_NULLABLE as u8;
     let c = code as i32;
+    // union field stores (nested places need `unsafe`)
+    #[allow(unused_unsafe)]
     unsafe {
         match c {
             ffi::VXG_ENC_PRIMITIVE | ffi::VXG_ENC_BYTE_BOOL => {
