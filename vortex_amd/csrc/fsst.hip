@@ -349,9 +349,10 @@ __device__ __forceinline__ void fsst_issue_codes(const uint8_t* codes, int64_t c
 // Persistent, software-pipelined decode.  Workgroup b decodes tiles b, b + G, b + 2G, ...
 // (G = gridDim.x).  The dependent global round trips of a tile (code range -> code bytes, and
 // its lengths / symbols / output prefix) are issued while the previous tile of the workgroup is
-// decoded: the next tile's code range and block totals go out before pass 1; after pass 2 its
-// code bytes, lengths, validity and symbol table are requested, and they land while the current
-// tile is copied out.  (An ablation of the one-tile-per-workgroup kernel showed the code-load
+// decoded: the next tile's code range and block totals go out before pass 1; after pass 1 its
+// code bytes, lengths, validity and symbol table are requested, and they land during pass 2 and
+// the copy-out.  Loads are split from the arithmetic on their results (ColRaw issue/finish), so
+// no wait is placed before the data is needed.  (An ablation of the one-tile-per-workgroup kernel showed the code-load
 // round trip alone cost a third of its time: profiles/r02_fsst_ablation_c4.jsonl.)
 //
 // Output offsets: tile_prefix (pre-pass) is the tile's offset inside its 128-tile scan block;
@@ -375,7 +376,7 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
     // the landing area of the raw code chunks before they are shifted into s_codes
     __shared__ __attribute__((aligned(16))) uint32_t s_heap32[(kHeapLds + 96) / 4];
     uint8_t* const s_heap = reinterpret_cast<uint8_t*>(s_heap32);
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, wave = tid >> 6;
     const uint64_t G = gridDim.x;
     if constexpr (EXT) {
         if (tab.n <= kFtLds)
@@ -388,36 +389,43 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
     // running block prefix (uniform): chunk and scan block it has been advanced to, and its sum
     uint32_t rb_chunk = ~0u, rb_sb = 0;
     int64_t rb_sum = 0;
-    // the next tile's early prologue: its code range (threads 0..2) and block totals (wave 0)
-    int64_t x_coff = 0, x_btot = 0;
+    // the next tile's early prologue: its code range (threads 0..2, raw words) and block totals
+    // (wave 0); nothing is computed from them until publish()
+    ColRaw x_craw{0, 0};
+    int64_t x_btot = 0;
     uint32_t x_chunk = 0, x_bt0 = 0, x_nbt = 0;
+    uint64_t x_lt = 0;
+    auto coff_index = [&](const FsstChunk& c, uint64_t lt) -> uint64_t {
+        const uint64_t first = lt * kTile, last = first + kTile < c.n ? first + kTile : c.n;
+        return tid == 0 ? 0 : (tid == 1 ? first : last);
+    };
     auto issue_early = [&](uint64_t gt) {
-        x_chunk = fsst_tile_chunk<EXT>(tab, s_ft, gt);
+        x_chunk = uni32(fsst_tile_chunk<EXT>(tab, s_ft, gt));
         const FsstChunk& c = fsst_chunk_at<EXT>(tab, x_chunk);
-        const uint64_t lt = gt - c.first_tile;
-        const uint32_t sb = uint32_t(lt / kScanTiles);
+        x_lt = gt - c.first_tile;
+        const uint32_t sb = uint32_t(x_lt / kScanTiles);
         x_bt0 = x_chunk == rb_chunk ? rb_sb : 0u;
         x_nbt = sb - x_bt0;
         const OffAcc code_offs(c.offs);
-        const uint64_t n = c.n, first = lt * kTile;
-        const uint64_t last = first + kTile < n ? first + kTile : n;
-        x_coff = tid < 3 ? code_offs(tid == 0 ? 0 : (tid == 1 ? first : last)) : 0;
+        if (tid < 3) x_craw = code_offs.issue(coff_index(c, x_lt));
         x_btot = uint32_t(tid) < x_nbt && tid < 64 ? block_totals_all[c.first_scan + x_bt0 + tid] : 0;
     };
-    // publish it (s_nx; read after the next barrier)
+    // decode and publish it (s_nx; read after the next barrier)
     auto publish = [&]() {
         const FsstChunk& c = fsst_chunk_at<EXT>(tab, x_chunk);
         int64_t bs = wave == 0 ? wave_sum(x_btot) : 0;
         for (uint32_t k = 64; k < x_nbt; k += 64)  // only for G > 64 * 128 (not launched)
             bs += wave == 0 ? wave_sum(tid + k < x_nbt ? block_totals_all[c.first_scan + x_bt0 + k + tid] : 0) : 0;
-        if (tid < 3) s_nx[tid] = x_coff;
+        if (tid < 3) s_nx[tid] = OffAcc(c.offs).finish(x_craw, coff_index(c, x_lt));
         if (tid == 0) s_nx[3] = (x_chunk == rb_chunk ? rb_sum : 0) + bs;
     };
-    // the late prologue of the published tile: code bytes, length, validity, symbols, prefix
+    // the late prologue of the published tile: code bytes, length (raw), validity, symbols,
+    // prefix -- all plain loads, decoded at the top of the tile's iteration
     uint4 raw0, raw1;
-    int64_t p_len, p_tp;
-    uint64_t p_sym;
-    uint32_t p_sl, p_vbyte;
+    ColRaw p_lraw{0, 0};
+    int64_t p_tp = 0;
+    uint64_t p_sym = 0;
+    uint32_t p_sl = 0, p_vbyte = 0;
     auto issue_late = [&](uint64_t gt) {
         const FsstChunk& c = fsst_chunk_at<EXT>(tab, x_chunk);
         rb_chunk = x_chunk;
@@ -425,10 +433,9 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
         rb_sum = uni64(s_nx[3]);
         const int64_t nf = uni64(s_nx[1]), nl = uni64(s_nx[2]);
         fsst_issue_codes(c.codes, nf, nl - nf, raw0, raw1);
-        const LenAcc lens(c.lens);
         const uint64_t lt = gt - c.first_tile;
         const uint64_t n = c.n, i = lt * kTile + tid, ii = i < n ? i : n - 1;
-        p_len = lens(ii);
+        p_lraw = LenAcc(c.lens).issue(ii);
         p_vbyte = c.validity ? c.validity[ii >> 3] : 0xFFu;
         const uint32_t sk = uint32_t(tid) < c.n_symbols ? uint32_t(tid) : 0;
         p_sym = c.symbols[sk];
@@ -461,7 +468,7 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
         const uint64_t ii = live ? i : n - 1;
         const int64_t c_base = uni64(s_nx[0]), cf = uni64(s_nx[1]), cl = uni64(s_nx[2]);
         const int64_t block_prefix = rb_sum;
-        const int64_t len_v = p_len, tp = p_tp;
+        const int64_t len_v = LenAcc(ch.lens).finish(p_lraw, ii), tp = p_tp;
         const uint32_t vbyte = p_vbyte;
         {
             // slot 255 is the escape (length 1, its byte comes from the code stream).  Symbols are
@@ -592,8 +599,10 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
                     }
                 }
             }
+            if (has_next) publish();  // its code range arrived during this tile's scans
             int dec_total;
             const int seg_rel = block_excl_scan32(int(sum8 >> 3), ws_b, dec_total);
+            if (has_next) issue_late(gn);  // lands during pass 2 and the copy-out
             if (tid == 0 && dec_total != ttot)
                 __hip_atomic_fetch_or(err, kErrFsst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             // pass 2: every code ORs its (zero-padded) bytes into <= 3 dwords of the zeroed image:
@@ -647,9 +656,7 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
                     }
                 }
             }
-            if (has_next) publish();
-            __syncthreads();  // image complete; s_nx holds the next tile's code range
-            if (has_next) issue_late(gn);
+            __syncthreads();  // image complete
             // (d) copy-out of [tile_out0, tile_out0 + ttot): the image sits at the same offset mod
             // 16 as its destination, so whole aligned chunks move as ds_read_b128 + 16-byte
             // stores; the ragged first/last chunk byte by byte (shared with the neighbouring tiles)
