@@ -42,7 +42,6 @@ constexpr int kCodeLds = 6 * 1024;    // staged code bytes per tile
 constexpr int kHeapLds = 10 * 1024;   // staged output bytes per tile
 constexpr int kScanTiles = 128;       // tiles per pre-pass workgroup (= 32 FastLanes blocks)
 constexpr int kMaxDw = (kCodeLds / kTile + 3) / 4;  // code dwords per thread in the decode
-
 static_assert(kMaxDw * 4 * kTile >= kCodeLds, "segments must cover the staged codes");
 
 __device__ __forceinline__ int64_t wave_sum(int64_t x) {
@@ -291,74 +290,6 @@ __global__ __launch_bounds__(kTile) void fsst_tile_scan_fl32(FsstTable tab, int6
     scan_tile_sums(s_ts, ws, n_tiles, sb, tile_prefix, block_totals);
 }
 
-// Wave-uniform values held in SGPRs (values read from LDS land in VGPRs otherwise, and every
-// address computed from them with them)
-__device__ __forceinline__ uint32_t uni32(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
-__device__ __forceinline__ int64_t uni64(int64_t x) {
-    const uint64_t u = uint64_t(x);
-    return int64_t(uint64_t(uni32(uint32_t(u))) | (uint64_t(uni32(uint32_t(u >> 32))) << 32));
-}
-
-// Chunk index of tile g: kernarg binary search, or a plan's device table via the LDS copy of
-// its first_tile column (s_ft, n <= kFtLds) / the wave-wide count over the device table.
-constexpr uint32_t kFtLds = 512;
-
-template <bool EXT>
-__device__ __forceinline__ uint32_t fsst_tile_chunk(const FsstTable& tab, const uint32_t* s_ft, uint64_t g) {
-    if constexpr (EXT) {
-        if (tab.n <= kFtLds) {
-            uint32_t lo = 0, hi = tab.n;
-            while (hi - lo > 1) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (uni32(s_ft[mid]) <= g) lo = mid; else hi = mid;
-            }
-            return lo;
-        }
-        return uni32(ext_chunk_index(tab.ext, tab.n, g, [](const FsstChunk& d) { return d.first_tile; }));
-    } else {
-        uint32_t lo = 0, hi = tab.n;
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (tab.c[mid].first_tile <= g) lo = mid; else hi = mid;
-        }
-        return lo;
-    }
-}
-
-template <bool EXT>
-__device__ __forceinline__ const FsstChunk& fsst_chunk_at(const FsstTable& tab, uint32_t k) {
-    if constexpr (EXT) return tab.ext[k];
-    else return tab.c[k];
-}
-
-// Raw (16-byte aligned) code chunks of a tile: chunk q = t, t + 256 of the aligned window that
-// holds code bytes [cabs0, cabs0 + span); nothing for tiles too large to stage.
-__device__ __forceinline__ void fsst_issue_codes(const uint8_t* codes, int64_t cabs0, int64_t span, uint4& r0,
-                                                 uint4& r1) {
-    const int tid = threadIdx.x;
-    r0 = r1 = make_uint4(0, 0, 0, 0);
-    if (span < 0 || span > kCodeLds) return;
-    const uintptr_t ga = reinterpret_cast<uintptr_t>(codes) + uintptr_t(cabs0);
-    const int cshift = int(ga & 15);
-    const int nraw = (cshift + int(span) + 15) >> 4;  // <= kCodeLds / 16 + 2 <= 2 * kTile
-    const uint4* a0 = reinterpret_cast<const uint4*>(ga - uintptr_t(cshift));
-    if (tid < nraw) r0 = a0[tid];
-    if (tid + kTile < nraw) r1 = a0[tid + kTile];
-}
-
-// Persistent, software-pipelined decode.  Workgroup b decodes tiles b, b + G, b + 2G, ...
-// (G = gridDim.x).  The dependent global round trips of a tile (code range -> code bytes, and
-// its lengths / symbols / output prefix) are issued while the previous tile of the workgroup is
-// decoded: the next tile's code range and block totals go out before pass 1; after pass 1 its
-// code bytes, lengths, validity and symbol table are requested, and they land during pass 2 and
-// the copy-out.  Loads are split from the arithmetic on their results (ColRaw issue/finish), so
-// no wait is placed before the data is needed.  (An ablation of the one-tile-per-workgroup kernel showed the code-load
-// round trip alone cost a third of its time: profiles/r02_fsst_ablation_c4.jsonl.)
-//
-// Output offsets: tile_prefix (pre-pass) is the tile's offset inside its 128-tile scan block;
-// the block's offset is the sum of the chunk's preceding block totals, kept as a running sum
-// per workgroup: its consecutive tiles are G tiles apart, so at most G / 128 + 1 new totals are
-// added per tile (one load per lane of wave 0; G <= 4096).
 template <class OffAcc, class LenAcc, bool EXT>
 __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t total_tiles,
                                                      const int64_t* __restrict__ tile_prefix_all,
@@ -369,350 +300,277 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
     __shared__ int ws_a[kTile / 64], ws_b[kTile / 64];
     __shared__ unsigned ws_bad[kTile / 64];
     __shared__ int64_t ws64[kTile / 64];
-    __shared__ int64_t s_nx[4];  // next tile: code_offs(0), code_offs(first), code_offs(last), block prefix
-    __shared__ uint32_t s_ft[EXT ? kFtLds : 1];
+    __shared__ int64_t s_block_prefix;
+    __shared__ int64_t s_coff[3];  // code_offs[0], code_offs[first], code_offs[last]
     __shared__ __attribute__((aligned(16))) uint8_t s_codes[kCodeLds + 48];
-    // + slack: view reads past a string, and ORs of the (<= 3) code bytes past the tile; also
-    // the landing area of the raw code chunks before they are shifted into s_codes
+    // + slack: view reads past a string, and ORs of the (<= 3) code bytes past the tile
     __shared__ __attribute__((aligned(16))) uint32_t s_heap32[(kHeapLds + 96) / 4];
     uint8_t* const s_heap = reinterpret_cast<uint8_t*>(s_heap32);
-    const int tid = threadIdx.x, wave = tid >> 6;
-    const uint64_t G = gridDim.x;
-    if constexpr (EXT) {
-        if (tab.n <= kFtLds)
-            for (uint32_t k = tid; k < tab.n; k += kTile) s_ft[k] = uint32_t(tab.ext[k].first_tile);
-        __syncthreads();
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+
+    const FsstChunk& ch = fsst_chunk_of<false, EXT>(tab, blockIdx.x);
+    const uint64_t* __restrict__ symbols = ch.symbols;
+    const uint8_t* __restrict__ sym_lens = ch.sym_lens;
+    const unsigned n_symbols = ch.n_symbols;
+    const uint8_t* __restrict__ codes = ch.codes;
+    const OffAcc code_offs(ch.offs);
+    const LenAcc lens(ch.lens);
+    const uint64_t n = ch.n;
+    const uint8_t* __restrict__ validity = ch.validity;
+    const int64_t* __restrict__ tile_prefix = tile_prefix_all + ch.first_tile;
+    const int64_t* __restrict__ block_totals = block_totals_all + ch.first_scan;
+    uint8_t* __restrict__ heap = ch.heap;
+    uint4* __restrict__ views = reinterpret_cast<uint4*>(ch.views);
+    const uint32_t bidx = ch.bidx;
+    const uint32_t tile = uint32_t(blockIdx.x - ch.first_tile);
+    {
+        const uint32_t sk = uint32_t(tid) < n_symbols ? uint32_t(tid) : 0;
+        const uint64_t sym_v = symbols[sk];
+        const uint32_t sl = sym_lens[sk];
+        // slot 255 is the escape (length 1, its byte comes from the code stream).  Symbols are
+        // stored zero-padded past their length, so a code can OR all 8 bytes; a length > 8
+        // is corrupt input.
+        const bool has = uint32_t(tid) < n_symbols;
+        if (has && sl > 8) __hip_atomic_fetch_or(err, kErrFsst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_sym[tid] = has ? (sl >= 8 ? sym_v : sym_v & ((1ull << (8 * sl)) - 1)) : 0;
+        s_len[tid] = has ? uint8_t(min(sl, 8u)) : uint8_t(tid == 255 ? 1 : 0);
     }
-    uint64_t g = blockIdx.x;
-    if (g >= total_tiles) return;
+    // Prologue: every global load is unconditional (indices clamped, results selected
+    // afterwards) so they retire under one wait.
+    const uint64_t first = uint64_t(tile) * kTile;
+    const uint64_t i = first + tid;
+    const bool live = i < n;
+    const uint64_t ii = live ? i : n - 1;
+    const uint64_t last = first + kTile < n ? first + kTile : n;
+    const int64_t len_v = lens(ii);
+    if (tid < 3) s_coff[tid] = code_offs(tid == 0 ? 0 : (tid == 1 ? first : last));  // read after a barrier
+    const uint8_t vbyte = validity ? validity[ii >> 3] : uint8_t(0xFF);
+    const int64_t tp = tile_prefix[tile];
+    if (wave == 0) {  // prefix of the preceding scan blocks (<= a few hundred totals), one wave
+        const uint32_t nb = tile / kScanTiles;
+        int64_t acc = 0;
+        for (uint32_t b = lane; b < nb; b += 64) acc += block_totals[b];
+        acc = wave_sum(acc);
+        if (lane == 0) s_block_prefix = acc;
+    }
+    const int64_t my_len = live ? len_v : 0;
 
-    // running block prefix (uniform): chunk and scan block it has been advanced to, and its sum
-    uint32_t rb_chunk = ~0u, rb_sb = 0;
-    int64_t rb_sum = 0;
-    // the next tile's early prologue: its code range (threads 0..2, raw words) and block totals
-    // (wave 0); nothing is computed from them until publish()
-    ColRaw x_craw{0, 0};
-    int64_t x_btot = 0;
-    uint32_t x_chunk = 0, x_bt0 = 0, x_nbt = 0;
-    uint64_t x_lt = 0;
-    auto coff_index = [&](const FsstChunk& c, uint64_t lt) -> uint64_t {
-        const uint64_t first = lt * kTile, last = first + kTile < c.n ? first + kTile : c.n;
-        return tid == 0 ? 0 : (tid == 1 ? first : last);
-    };
-    auto issue_early = [&](uint64_t gt) {
-        x_chunk = uni32(fsst_tile_chunk<EXT>(tab, s_ft, gt));
-        const FsstChunk& c = fsst_chunk_at<EXT>(tab, x_chunk);
-        x_lt = gt - c.first_tile;
-        const uint32_t sb = uint32_t(x_lt / kScanTiles);
-        x_bt0 = x_chunk == rb_chunk ? rb_sb : 0u;
-        x_nbt = sb - x_bt0;
-        const OffAcc code_offs(c.offs);
-        if (tid < 3) x_craw = code_offs.issue(coff_index(c, x_lt));
-        x_btot = uint32_t(tid) < x_nbt && tid < 64 ? block_totals_all[c.first_scan + x_bt0 + tid] : 0;
-    };
-    // decode and publish it (s_nx; read after the next barrier)
-    auto publish = [&]() {
-        const FsstChunk& c = fsst_chunk_at<EXT>(tab, x_chunk);
-        int64_t bs = wave == 0 ? wave_sum(x_btot) : 0;
-        for (uint32_t k = 64; k < x_nbt; k += 64)  // only for G > 64 * 128 (not launched)
-            bs += wave == 0 ? wave_sum(tid + k < x_nbt ? block_totals_all[c.first_scan + x_bt0 + k + tid] : 0) : 0;
-        if (tid < 3) s_nx[tid] = OffAcc(c.offs).finish(x_craw, coff_index(c, x_lt));
-        if (tid == 0) s_nx[3] = (x_chunk == rb_chunk ? rb_sum : 0) + bs;
-    };
-    // the late prologue of the published tile: code bytes, length (raw), validity, symbols,
-    // prefix -- all plain loads, decoded at the top of the tile's iteration
-    uint4 raw0, raw1;
-    ColRaw p_lraw{0, 0};
-    int64_t p_tp = 0;
-    uint64_t p_sym = 0;
-    uint32_t p_sl = 0, p_vbyte = 0;
-    auto issue_late = [&](uint64_t gt) {
-        const FsstChunk& c = fsst_chunk_at<EXT>(tab, x_chunk);
-        rb_chunk = x_chunk;
-        rb_sb = x_bt0 + x_nbt;
-        rb_sum = uni64(s_nx[3]);
-        const int64_t nf = uni64(s_nx[1]), nl = uni64(s_nx[2]);
-        fsst_issue_codes(c.codes, nf, nl - nf, raw0, raw1);
-        const uint64_t lt = gt - c.first_tile;
-        const uint64_t n = c.n, i = lt * kTile + tid, ii = i < n ? i : n - 1;
-        p_lraw = LenAcc(c.lens).issue(ii);
-        p_vbyte = c.validity ? c.validity[ii >> 3] : 0xFFu;
-        const uint32_t sk = uint32_t(tid) < c.n_symbols ? uint32_t(tid) : 0;
-        p_sym = c.symbols[sk];
-        p_sl = c.sym_lens[sk];
-        p_tp = tile_prefix_all[c.first_tile + lt];
-    };
+    // (a) length scan: int32 with DPP when every length is in [0, kHeapLds] (then a staged
+    // tile is possible), int64 otherwise (direct path).
+    const bool bad = my_len < 0 || my_len > kHeapLds;
+    const unsigned long long bm = __ballot(bad);
+    if (lane == 0) ws_bad[wave] = bm != 0;
+    int t32;
+    const int rel32 = block_excl_scan32(bad ? 0 : int(my_len), ws_a, t32);
+    const bool any_bad = (ws_bad[0] | ws_bad[1] | ws_bad[2] | ws_bad[3]) != 0;
+    int64_t my_rel = rel32, tile_total = t32;
+    if (any_bad) my_rel = block_exclusive_scan<kTile / 64>(my_len, ws64, tile_total);  // uniform branch
+    const int64_t tile_out0 = tp + s_block_prefix;
 
-    issue_early(g);
-    publish();
-    __syncthreads();
-    issue_late(g);
+    const int64_t c_base = s_coff[0], cf = s_coff[1], cl = s_coff[2];
+    // code offsets are relative to code_offs[0] (sliced_bytes(), varbin/mod.rs:130-136)
+    const int64_t c0 = cf - c_base, c1 = cl - c_base;
+    const bool valid = live && ((vbyte >> (ii & 7)) & 1);
+    const uint32_t vlen = valid ? uint32_t(my_len) : 0u;
+    const bool stage = !any_bad && (c1 - c0) <= kCodeLds && c1 >= c0 && tile_total <= kHeapLds;
 
-    for (;;) {
-        // a fresh, opaque copy of the thread index per tile: every lane-dependent address and
-        // mask below is recomputed inside the loop instead of being hoisted out of it and held
-        // in VGPRs across the whole loop (which doubled the kernel's VGPRs)
-        int tid_o = int(threadIdx.x);
-        asm volatile("" : "+v"(tid_o));
-        const int tid = tid_o, lane = tid & 63, wave = tid >> 6;
-        const uint32_t ck = rb_chunk;  // the chunk of tile g (issue_late set it)
-        const FsstChunk& ch = fsst_chunk_at<EXT>(tab, ck);
-        const uint8_t* __restrict__ codes = ch.codes;
-        uint8_t* __restrict__ heap = ch.heap;
-        uint4* __restrict__ views = reinterpret_cast<uint4*>(ch.views);
-        const uint32_t bidx = ch.bidx;
-        const uint64_t n = ch.n;
-        const uint64_t first = (g - ch.first_tile) * kTile;
-        const uint64_t i = first + tid;
-        const bool live = i < n;
-        const uint64_t ii = live ? i : n - 1;
-        const int64_t c_base = uni64(s_nx[0]), cf = uni64(s_nx[1]), cl = uni64(s_nx[2]);
-        const int64_t block_prefix = rb_sum;
-        const int64_t len_v = LenAcc(ch.lens).finish(p_lraw, ii), tp = p_tp;
-        const uint32_t vbyte = p_vbyte;
+    if (stage) {
+        // (b) stage the tile's code bytes into LDS shifted so that the tile's first code is
+        // s_codes[0] (two aligned 16-byte loads + a byte funnel per chunk; an aligned chunk that
+        // holds a tile byte never crosses a page, so it is read whole), and zero the image
+        const int64_t cabs0 = c_base + c0;
+        const uintptr_t ga = reinterpret_cast<uintptr_t>(codes) + uintptr_t(cabs0);
+        const int cshift = int(ga & 15);
+        const int hshift = int((reinterpret_cast<uintptr_t>(heap) + tile_out0) & 15);  // image byte hshift = heap[tile_out0]
+        const int span = int(c1 - c0);  // tile codes at s_codes[0, span)
+        const int ttot = int(tile_total);
         {
-            // slot 255 is the escape (length 1, its byte comes from the code stream).  Symbols are
-            // stored zero-padded past their length, so a code can OR all 8 bytes; a length > 8
-            // is corrupt input.
-            const bool has = uint32_t(tid) < ch.n_symbols;
-            if (has && p_sl > 8) __hip_atomic_fetch_or(err, kErrFsst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_sym[tid] = has ? (p_sl >= 8 ? p_sym : p_sym & ((1ull << (8 * p_sl)) - 1)) : 0;
-            s_len[tid] = has ? uint8_t(min(p_sl, 8u)) : uint8_t(tid == 255 ? 1 : 0);
-            // raw code chunks land in the image area until they are shifted into s_codes
-            reinterpret_cast<uint4*>(s_heap32)[tid] = raw0;
-            reinterpret_cast<uint4*>(s_heap32)[tid + kTile] = raw1;
+            const uint4* a0 = reinterpret_cast<const uint4*>(ga - uintptr_t(cshift));
+            const int nchunk = (span + 15) >> 4;
+            for (int q = tid; q < nchunk; q += kTile) {
+                const uint4 x = a0[q];
+                uint4 y = make_uint4(0, 0, 0, 0);
+                if (cshift != 0 && 16 * (q + 1) - cshift < span) y = a0[q + 1];
+                *reinterpret_cast<uint4*>(s_codes + 16 * q) = funnel16(x, y, cshift);
+            }
+            const int nz = (hshift + ttot + 16 + 15) >> 4;
+            for (int q = tid; q < nz; q += kTile) reinterpret_cast<uint4*>(s_heap32)[q] = make_uint4(0, 0, 0, 0);
         }
-        __syncthreads();  // symbol table, raw chunks; s_nx has been read
+        __syncthreads();
 
-        const uint64_t gn = g + G;
-        const bool has_next = gn < total_tiles;
-        if (has_next) issue_early(gn);
-
-        const int64_t my_len = live ? len_v : 0;
-        // (a) length scan: int32 with DPP when every length is in [0, kHeapLds] (then a staged
-        // tile is possible), int64 otherwise (direct path).
-        const bool bad = my_len < 0 || my_len > kHeapLds;
-        const unsigned long long bm = __ballot(bad);
-        if (lane == 0) ws_bad[wave] = bm != 0;
-        int t32;
-        const int rel32 = block_excl_scan32(bad ? 0 : int(my_len), ws_a, t32);
-        const bool any_bad = (ws_bad[0] | ws_bad[1] | ws_bad[2] | ws_bad[3]) != 0;
-        int64_t my_rel = rel32, tile_total = t32;
-        if (any_bad) my_rel = block_exclusive_scan<kTile / 64>(my_len, ws64, tile_total);  // uniform branch
-        const int64_t tile_out0 = tp + block_prefix;
-        // code offsets are relative to code_offs[0] (sliced_bytes(), varbin/mod.rs:130-136)
-        const int64_t c0 = cf - c_base, c1 = cl - c_base;
-        const bool valid = live && ((vbyte >> (ii & 7)) & 1);
-        const uint32_t vlen = valid ? uint32_t(my_len) : 0u;
-        const bool stage = !any_bad && (c1 - c0) <= kCodeLds && c1 >= c0 && tile_total <= kHeapLds;
-
-        if (stage) {
-            // (b) shift the tile's raw code chunks so that its first code is s_codes[0], then
-            // zero the image
-            const int cshift = int((reinterpret_cast<uintptr_t>(codes) + uintptr_t(cf)) & 15);
-            const int hshift = int((reinterpret_cast<uintptr_t>(heap) + tile_out0) & 15);  // image byte hshift = heap[tile_out0]
-            const int span = int(c1 - c0);  // tile codes at s_codes[0, span)
-            const int ttot = int(tile_total);
-            {
-                const int nchunk = (span + 15) >> 4;
-                const uint4* rawl = reinterpret_cast<const uint4*>(s_heap32);
-                const uint4 z = make_uint4(0, 0, 0, 0);
-                uint4 sh0 = z, sh1 = z;
-                if (tid < nchunk) sh0 = funnel16(rawl[tid], cshift ? rawl[tid + 1] : z, cshift);
-                if (tid + kTile < nchunk) sh1 = funnel16(rawl[tid + kTile], cshift ? rawl[tid + kTile + 1] : z, cshift);
-                if (tid < nchunk) *reinterpret_cast<uint4*>(s_codes + 16 * tid) = sh0;
-                if (tid + kTile < nchunk) *reinterpret_cast<uint4*>(s_codes + 16 * (tid + kTile)) = sh1;
+        // (c) code-parallel decode over segments of nd dwords (4 code bytes each) per thread,
+        // sized so that ~all 256 threads have work.  A wave whose bytes hold no escape (255)
+        // and does not start right after one takes the fast path (no escape logic, no
+        // predication); otherwise the general path.  Both pack each code's decoded length x 8
+        // into one byte of a per-dword word (sum = v_sad_u8).
+        const int nd = max(1, ((span + kTile - 1) / kTile + 3) >> 2);
+        const int s0 = tid * 4 * nd;
+        bool slow = false;
+        bool skip0 = false;  // is s_codes[s0] the literal byte of an escape?
+        if (s0 > 0 && s0 < span && s_codes[s0 - 1] == 255) {
+            slow = true;
+            int r = 0;
+            for (int p = s0 - 1; p >= 0 && s_codes[p] == 255; --p) ++r;
+            skip0 = r & 1;
+        }
+        uint32_t wd[kMaxDw];
+#pragma unroll
+        for (int d = 0; d < kMaxDw; d++) {
+            wd[d] = 0;
+            if (d < nd && s0 + 4 * d < span) {
+                wd[d] = *reinterpret_cast<const uint32_t*>(s_codes + s0 + 4 * d);
+                const uint32_t x = wd[d];
+                slow |= (((x & 0x7F7F7F7Fu) + 0x01010101u) & x & 0x80808080u) != 0;  // a 0xFF byte
             }
-            __syncthreads();  // raw chunks consumed: the image area may be zeroed
-            {
-                const int nz = (hshift + ttot + 16 + 15) >> 4;
-                for (int q = tid; q < nz; q += kTile) reinterpret_cast<uint4*>(s_heap32)[q] = make_uint4(0, 0, 0, 0);
-            }
-            __syncthreads();
-
-            // (c) code-parallel decode over segments of nd dwords (4 code bytes each) per thread,
-            // sized so that ~all 256 threads have work.  A wave whose bytes hold no escape (255)
-            // and does not start right after one takes the fast path (no escape logic, no
-            // predication); otherwise the general path.  Both pack each code's decoded length x 8
-            // into one byte of a per-dword word (sum = v_sad_u8).
-            const int nd = max(1, ((span + kTile - 1) / kTile + 3) >> 2);
-            const int s0 = tid * 4 * nd;
-            bool slow = false;
-            bool skip0 = false;  // is s_codes[s0] the literal byte of an escape?
-            if (s0 > 0 && s0 < span && s_codes[s0 - 1] == 255) {
-                slow = true;
-                int r = 0;
-                for (int p = s0 - 1; p >= 0 && s_codes[p] == 255; --p) ++r;
-                skip0 = r & 1;
-            }
-            uint32_t wd[kMaxDw];
+        }
+        const bool fast = __ballot(slow) == 0;  // wave-uniform
+        // pass 1: pk[d] byte j = decoded length x 8 of code byte 4d + j (0 for literals and
+        // bytes past the tile)
+        uint32_t pk[kMaxDw];
+        uint32_t sum8 = 0;
+        if (fast) {
 #pragma unroll
             for (int d = 0; d < kMaxDw; d++) {
-                wd[d] = 0;
+                pk[d] = 0;
                 if (d < nd && s0 + 4 * d < span) {
-                    wd[d] = *reinterpret_cast<const uint32_t*>(s_codes + s0 + 4 * d);
                     const uint32_t x = wd[d];
-                    slow |= (((x & 0x7F7F7F7Fu) + 0x01010101u) & x & 0x80808080u) != 0;  // a 0xFF byte
+                    uint32_t ls[4];
+#pragma unroll
+                    for (int j = 0; j < 4; j++) ls[j] = s_len[(x >> (8 * j)) & 0xFFu];
+                    uint32_t k = 0;
+#pragma unroll
+                    for (int j = 0; j < 4; j++) k |= ls[j] << (8 * j + 3);
+                    const int vb = span - (s0 + 4 * d);  // valid bytes of this dword
+                    if (vb < 4) k &= (1u << (8 * vb)) - 1u;
+                    pk[d] = k;
+                    sum8 = __builtin_amdgcn_sad_u8(k, 0u, sum8);
                 }
             }
-            const bool fast = __ballot(slow) == 0;  // wave-uniform
-            // pass 1: pk[d] byte j = decoded length x 8 of code byte 4d + j (0 for literals and
-            // bytes past the tile)
-            uint32_t pk[kMaxDw];
-            uint32_t sum8 = 0;
+        } else {
+            bool skp = skip0;
+#pragma unroll
+            for (int d = 0; d < kMaxDw; d++) {
+                pk[d] = 0;
+                if (d < nd && s0 + 4 * d < span) {
+                    const uint32_t x = wd[d];
+                    uint32_t k = 0;
+#pragma unroll
+                    for (int j = 0; j < 4; j++) {
+                        const uint32_t c = (x >> (8 * j)) & 0xFFu;
+                        const bool emit = s0 + 4 * d + j < span && !skp;
+                        skp = emit && c == 255;
+                        const uint32_t L = emit ? uint32_t(s_len[c]) : 0u;
+                        k |= L << (8 * j + 3);
+                    }
+                    pk[d] = k;
+                    sum8 = __builtin_amdgcn_sad_u8(k, 0u, sum8);
+                }
+            }
+        }
+        int dec_total;
+        const int seg_rel = block_excl_scan32(int(sum8 >> 3), ws_b, dec_total);
+        if (tid == 0 && dec_total != ttot)
+            __hip_atomic_fetch_or(err, kErrFsst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // pass 2: every code ORs its (zero-padded) bytes into <= 3 dwords of the zeroed image:
+        // (w1:w0) = sym << 8(o & 3) and w2 = the bytes shifted past them.  Fast path: all 4
+        // symbol reads of a dword issued first, no selects.  Codes past the tile (fast path,
+        // last segment) OR into the image slack after the tile.  A tile whose codes do not
+        // decode to its length sum (corrupt input, flagged above) is not written.
+        if (dec_total == ttot) {
+            uint32_t o8 = uint32_t(hshift + seg_rel) << 3;  // bit position in the image
+            auto put = [&](uint64_t m, uint32_t L8) {
+                const uint32_t sh = o8 & 24u;
+                const uint32_t w = o8 >> 5;
+                const uint64_t lo64 = m << sh;
+                const uint32_t hi32 = uint32_t((m >> 32) << sh >> 32);
+                __hip_atomic_fetch_or(&s_heap32[w], uint32_t(lo64), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_or(&s_heap32[w + 1], uint32_t(lo64 >> 32), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_or(&s_heap32[w + 2], hi32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                o8 += L8;
+            };
             if (fast) {
 #pragma unroll
                 for (int d = 0; d < kMaxDw; d++) {
-                    pk[d] = 0;
                     if (d < nd && s0 + 4 * d < span) {
                         const uint32_t x = wd[d];
-                        uint32_t ls[4];
+                        uint64_t sy[4];
 #pragma unroll
-                        for (int j = 0; j < 4; j++) ls[j] = s_len[(x >> (8 * j)) & 0xFFu];
-                        uint32_t k = 0;
+                        for (int j = 0; j < 4; j++) sy[j] = s_sym[(x >> (8 * j)) & 0xFFu];
 #pragma unroll
-                        for (int j = 0; j < 4; j++) k |= ls[j] << (8 * j + 3);
-                        const int vb = span - (s0 + 4 * d);  // valid bytes of this dword
-                        if (vb < 4) k &= (1u << (8 * vb)) - 1u;
-                        pk[d] = k;
-                        sum8 = __builtin_amdgcn_sad_u8(k, 0u, sum8);
+                        for (int j = 0; j < 4; j++) put(sy[j], (pk[d] >> (8 * j)) & 0xFFu);
                     }
                 }
             } else {
-                bool skp = skip0;
 #pragma unroll
                 for (int d = 0; d < kMaxDw; d++) {
-                    pk[d] = 0;
                     if (d < nd && s0 + 4 * d < span) {
                         const uint32_t x = wd[d];
-                        uint32_t k = 0;
+                        const uint32_t after = s_codes[s0 + 4 * d + 4];  // literal of an escape in byte 3
+                        uint64_t sy[4];
+#pragma unroll
+                        for (int j = 0; j < 4; j++) sy[j] = s_sym[(x >> (8 * j)) & 0xFFu];
 #pragma unroll
                         for (int j = 0; j < 4; j++) {
                             const uint32_t c = (x >> (8 * j)) & 0xFFu;
-                            const bool emit = s0 + 4 * d + j < span && !skp;
-                            skp = emit && c == 255;
-                            const uint32_t L = emit ? uint32_t(s_len[c]) : 0u;
-                            k |= L << (8 * j + 3);
-                        }
-                        pk[d] = k;
-                        sum8 = __builtin_amdgcn_sad_u8(k, 0u, sum8);
-                    }
-                }
-            }
-            if (has_next) publish();  // its code range arrived during this tile's scans
-            int dec_total;
-            const int seg_rel = block_excl_scan32(int(sum8 >> 3), ws_b, dec_total);
-            if (has_next) issue_late(gn);  // lands during pass 2 and the copy-out
-            if (tid == 0 && dec_total != ttot)
-                __hip_atomic_fetch_or(err, kErrFsst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            // pass 2: every code ORs its (zero-padded) bytes into <= 3 dwords of the zeroed image:
-            // (w1:w0) = sym << 8(o & 3) and w2 = the bytes shifted past them.  Fast path: all 4
-            // symbol reads of a dword issued first, no selects.  Codes past the tile (fast path,
-            // last segment) OR into the image slack after the tile.  A tile whose codes do not
-            // decode to its length sum (corrupt input, flagged above) is not written.
-            if (dec_total == ttot) {
-                uint32_t o8 = uint32_t(hshift + seg_rel) << 3;  // bit position in the image
-                auto put = [&](uint64_t m, uint32_t L8) {
-                    const uint32_t sh = o8 & 24u;
-                    const uint32_t w = o8 >> 5;
-                    const uint64_t lo64 = m << sh;
-                    const uint32_t hi32 = uint32_t((m >> 32) << sh >> 32);
-                    __hip_atomic_fetch_or(&s_heap32[w], uint32_t(lo64), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    __hip_atomic_fetch_or(&s_heap32[w + 1], uint32_t(lo64 >> 32), __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_WORKGROUP);
-                    __hip_atomic_fetch_or(&s_heap32[w + 2], hi32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    o8 += L8;
-                };
-                if (fast) {
-#pragma unroll
-                    for (int d = 0; d < kMaxDw; d++) {
-                        if (d < nd && s0 + 4 * d < span) {
-                            const uint32_t x = wd[d];
-                            uint64_t sy[4];
-#pragma unroll
-                            for (int j = 0; j < 4; j++) sy[j] = s_sym[(x >> (8 * j)) & 0xFFu];
-#pragma unroll
-                            for (int j = 0; j < 4; j++) put(sy[j], (pk[d] >> (8 * j)) & 0xFFu);
-                        }
-                    }
-                } else {
-#pragma unroll
-                    for (int d = 0; d < kMaxDw; d++) {
-                        if (d < nd && s0 + 4 * d < span) {
-                            const uint32_t x = wd[d];
-                            const uint32_t after = s_codes[s0 + 4 * d + 4];  // literal of an escape in byte 3
-                            uint64_t sy[4];
-#pragma unroll
-                            for (int j = 0; j < 4; j++) sy[j] = s_sym[(x >> (8 * j)) & 0xFFu];
-#pragma unroll
-                            for (int j = 0; j < 4; j++) {
-                                const uint32_t c = (x >> (8 * j)) & 0xFFu;
-                                const uint32_t L8 = (pk[d] >> (8 * j)) & 0xFFu;
-                                const uint64_t lit = j < 3 ? ((x >> (8 * j + 8)) & 0xFFu) : after;
-                                uint64_t m = c == 255 ? lit : sy[j];
-                                put(L8 ? m : 0ull, L8);
-                            }
+                            const uint32_t L8 = (pk[d] >> (8 * j)) & 0xFFu;
+                            const uint64_t lit = j < 3 ? ((x >> (8 * j + 8)) & 0xFFu) : after;
+                            uint64_t m = c == 255 ? lit : sy[j];
+                            put(L8 ? m : 0ull, L8);
                         }
                     }
                 }
             }
-            __syncthreads();  // image complete
-            // (d) copy-out of [tile_out0, tile_out0 + ttot): the image sits at the same offset mod
-            // 16 as its destination, so whole aligned chunks move as ds_read_b128 + 16-byte
-            // stores; the ragged first/last chunk byte by byte (shared with the neighbouring tiles)
-            {
-                uint8_t* const gbase = heap + (tile_out0 - hshift);
-                const int nchunk = (hshift + ttot + 15) >> 4;
-                for (int q = tid; q < nchunk; q += kTile) {
-                    const int lb = 16 * q;
-                    if (lb >= hshift && lb + 16 <= hshift + ttot) {
-                        nt_store(reinterpret_cast<uint4*>(gbase + lb), *reinterpret_cast<const uint4*>(s_heap + lb));
-                    } else {
-                        for (int b = 0; b < 16; b++)
-                            if (lb + b >= hshift && lb + b < hshift + ttot) gbase[lb + b] = s_heap[lb + b];
-                    }
-                }
-            }
-            if (live)
-                views[i] = valid ? lds_view(s_heap32, hshift + int(my_rel), vlen, uint32_t(tile_out0 + my_rel), bidx)
-                                 : make_uint4(0, 0, 0, 0);
-        } else {
-            // direct path: per-string decode straight into HBM (codes of string i are
-            // [offs[i], offs[i+1]); each must decode to exactly lengths[i] bytes)
-            const OffAcc code_offs(ch.offs);
-            const int64_t my_c0 = live ? code_offs(ii) - c_base : 0;
-            const int64_t my_c1 = live ? code_offs(ii + 1) - c_base : 0;
-            const uint8_t* gcodes = codes + c_base;
-            int64_t o = tile_out0 + my_rel;
-            const int64_t o_start = o, o_end = o + my_len;
-            for (int64_t k = my_c0; k < my_c1; k++) {
-                const uint8_t c = gcodes[k];
-                if (c == 255) {
-                    ++k;
-                    if (o < o_end) heap[o] = gcodes[k];
-                    o++;
-                } else {
-                    const uint64_t sym = s_sym[c];
-                    const int L = s_len[c];
-                    for (int b = 0; b < L; b++)
-                        if (o + b < o_end) heap[o + b] = uint8_t(sym >> (8 * b));
-                    o += L;
-                }
-            }
-            if (o != o_end) __hip_atomic_fetch_or(err, kErrFsst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (live) {
-                const uint8_t* hp = heap + o_start;
-                views[i] = valid ? build_view(vlen, uint32_t(o_start), bidx,
-                                              [&](int j) { return uint32_t(j) < vlen ? hp[j] : uint8_t(0); })
-                                 : make_uint4(0, 0, 0, 0);
-            }
-            if (has_next) publish();
-            __syncthreads();
-            if (has_next) issue_late(gn);
         }
-        if (!has_next) break;
-        g = gn;
-        __syncthreads();  // this tile's LDS reads (copy-out, views, direct path) are done
+        __syncthreads();
+        // (d) copy-out of [tile_out0, tile_out0 + ttot): the image sits at the same offset mod 16
+        // as its destination, so whole aligned chunks move as ds_read_b128 + 16-byte stores;
+        // the ragged first/last chunk byte by byte (shared with the neighbouring tiles)
+        {
+            uint8_t* const gbase = heap + (tile_out0 - hshift);
+            const int nchunk = (hshift + ttot + 15) >> 4;
+            for (int q = tid; q < nchunk; q += kTile) {
+                const int lb = 16 * q;
+                if (lb >= hshift && lb + 16 <= hshift + ttot) {
+                    nt_store(reinterpret_cast<uint4*>(gbase + lb), *reinterpret_cast<const uint4*>(s_heap + lb));
+                } else {
+                    for (int b = 0; b < 16; b++)
+                        if (lb + b >= hshift && lb + b < hshift + ttot) gbase[lb + b] = s_heap[lb + b];
+                }
+            }
+        }
+        if (live)
+            views[i] = valid ? lds_view(s_heap32, hshift + int(my_rel), vlen, uint32_t(tile_out0 + my_rel), bidx)
+                             : make_uint4(0, 0, 0, 0);
+    } else {
+        // direct path: per-string decode straight into HBM (codes of string i are
+        // [offs[i], offs[i+1]); each must decode to exactly lengths[i] bytes)
+        const int64_t my_c0 = live ? code_offs(ii) - c_base : 0;
+        const int64_t my_c1 = live ? code_offs(ii + 1) - c_base : 0;
+        const uint8_t* gcodes = codes + c_base;
+        int64_t o = tile_out0 + my_rel;
+        const int64_t o_start = o, o_end = o + my_len;
+        for (int64_t k = my_c0; k < my_c1; k++) {
+            const uint8_t c = gcodes[k];
+            if (c == 255) {
+                ++k;
+                if (o < o_end) heap[o] = gcodes[k];
+                o++;
+            } else {
+                const uint64_t sym = s_sym[c];
+                const int L = s_len[c];
+                for (int b = 0; b < L; b++)
+                    if (o + b < o_end) heap[o + b] = uint8_t(sym >> (8 * b));
+                o += L;
+            }
+        }
+        if (o != o_end) __hip_atomic_fetch_or(err, kErrFsst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (live) {
+            const uint8_t* hp = heap + o_start;
+            views[i] = valid ? build_view(vlen, uint32_t(o_start), bidx,
+                                          [&](int j) { return uint32_t(j) < vlen ? hp[j] : uint8_t(0); })
+                             : make_uint4(0, 0, 0, 0);
+        }
     }
 }
 
@@ -819,20 +677,8 @@ vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint
                         if (std::get<2>(key) < 0)
                             hipLaunchKernelGGL((fsst_tile_scan<LA, X>), dim3(unsigned(scans)), dim3(kTile), 0, s, tab,
                                                tp, bt);
-                        // persistent grid: as many workgroups as are resident at once (<= 4096, so
-                        // a workgroup's running block prefix takes <= 33 totals per tile)
-                        static const unsigned resident = [] {
-                            int per_cu = 0, cus = 0, dev = 0;
-                            (void)hipGetDevice(&dev);
-                            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-                            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                                &per_cu, reinterpret_cast<const void*>(&fsst_decode<OA, LA, X>), kTile, 0);
-                            const long r = long(per_cu > 0 ? per_cu : 1) * long(cus > 0 ? cus : 256);
-                            return unsigned(r < 4096 ? r : 4096);
-                        }();
-                        const unsigned grid = tiles < resident ? unsigned(tiles) : resident;
-                        hipLaunchKernelGGL((fsst_decode<OA, LA, X>), dim3(grid), dim3(kTile), 0, s, tab, tiles, tp, bt,
-                                           err);
+                        hipLaunchKernelGGL((fsst_decode<OA, LA, X>), dim3(unsigned(tiles)), dim3(kTile), 0, s, tab,
+                                           tiles, tp, bt, err);
                     };
                     if (tab.ext) go(std::true_type{});
                     else go(std::false_type{});
@@ -848,4 +694,3 @@ vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint
 }
 
 }  // namespace vxg
-

@@ -47,12 +47,6 @@ __device__ __forceinline__ int64_t fl_get(const void* packed, uint32_t W, uint32
     else return sgn ? int64_t(int32_t(r)) : int64_t(r);
 }
 
-// Raw words of one element (split reads: issue() only loads, finish() decodes later, so a
-// software-pipelined kernel can keep the load in flight across other work).
-struct ColRaw {
-    uint64_t lo, hi;
-};
-
 // Compile-time readers (hot loops): Plain<WIDTH> and Packed<T>.
 template <int WIDTH> struct PlainCol {
     const void* p;
@@ -60,12 +54,6 @@ template <int WIDTH> struct PlainCol {
     __host__ __device__ explicit PlainCol(const IntCol& c) : p(c.p), sgn(c.sgn) {}
     __device__ __forceinline__ int64_t operator()(uint64_t i) const {
         const int64_t u = ld<WIDTH, false>(p, i);
-        if constexpr (WIDTH == 8) return u;
-        else return sgn ? ((u << (64 - 8 * WIDTH)) >> (64 - 8 * WIDTH)) : u;
-    }
-    __device__ __forceinline__ ColRaw issue(uint64_t i) const { return {uint64_t(ld<WIDTH, false>(p, i)), 0}; }
-    __device__ __forceinline__ int64_t finish(const ColRaw& r, uint64_t) const {
-        const int64_t u = int64_t(r.lo);
         if constexpr (WIDTH == 8) return u;
         else return sgn ? ((u << (64 - 8 * WIDTH)) >> (64 - 8 * WIDTH)) : u;
     }
@@ -79,36 +67,6 @@ template <int T> struct PackedCol {
         : p(c.p), W(c.W), shift(c.shift), offset(c.offset), reference(c.reference), sgn(c.sgn) {}
     __device__ __forceinline__ int64_t operator()(uint64_t i) const {
         return fl_get<T>(p, W, shift, offset, reference, sgn, i);
-    }
-    // fl_get split at its loads
-    using E = std::conditional_t<T == 32, uint32_t, uint64_t>;
-    static constexpr uint32_t LANES = 1024 / T;
-    __device__ __forceinline__ uint32_t start_bit(uint64_t g) const {
-        const uint32_t idx = uint32_t(g & 1023);
-        const uint32_t lane = idx % LANES, s = idx >> 7;
-        const uint32_t fl = ((idx & 127) - lane) >> 4;
-        return ((((fl & 1) << 2) | (fl & 2) | (fl >> 2)) * 8 + s) * W;  // FL_ORDER[fl]*8 + s, times W
-    }
-    __device__ __forceinline__ ColRaw issue(uint64_t i) const {
-        if (W == 0) return {0, 0};
-        const uint64_t g = i + offset;
-        const uint32_t lane = uint32_t(g & 1023) % LANES;
-        const E* base = static_cast<const E*>(p) + (g >> 10) * (uint64_t(LANES) * W);
-        const uint32_t word = start_bit(g) / T;
-        const uint32_t word2 = word + 1 < W ? word + 1 : word;
-        return {uint64_t(base[LANES * word + lane]), uint64_t(base[LANES * word2 + lane])};
-    }
-    __device__ __forceinline__ int64_t finish(const ColRaw& r, uint64_t i) const {
-        E v = 0;
-        if (W != 0) {
-            const uint32_t sh = start_bit(i + offset) % T;
-            v = E(r.lo) >> sh;
-            if (sh + W > uint32_t(T)) v |= E(r.hi) << (T - sh);
-            if (W < uint32_t(T)) v &= (E(1) << W) - 1;
-        }
-        const E out = E(E(v << shift) + E(reference));
-        if constexpr (T == 64) return int64_t(out);
-        else return sgn ? int64_t(int32_t(out)) : int64_t(out);
     }
 };
 
