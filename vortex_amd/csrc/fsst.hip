@@ -347,9 +347,20 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
     const uint8_t vbyte = validity ? validity[ii >> 3] : uint8_t(0xFF);
     const int64_t tp = tile_prefix[tile];
     if (wave == 0) {  // prefix of the preceding scan blocks (<= a few hundred totals), one wave
+        // four loads per lane in flight per round (clamped index, no per-element branch), so a
+        // tile deep in a large chunk pays one memory round trip here, not one per 64 blocks
         const uint32_t nb = tile / kScanTiles;
         int64_t acc = 0;
-        for (uint32_t b = lane; b < nb; b += 64) acc += block_totals[b];
+        for (uint32_t b0 = 0; b0 < nb; b0 += 256) {
+            int64_t v[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const uint32_t b = b0 + 64 * k + lane;
+                v[k] = block_totals[b < nb ? b : nb - 1];
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++) acc += b0 + 64 * k + lane < nb ? v[k] : 0;
+        }
         acc = wave_sum(acc);
         if (lane == 0) s_block_prefix = acc;
     }
@@ -534,8 +545,23 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
                 if (lb >= hshift && lb + 16 <= hshift + ttot) {
                     nt_store(reinterpret_cast<uint4*>(gbase + lb), *reinterpret_cast<const uint4*>(s_heap + lb));
                 } else {
-                    for (int b = 0; b < 16; b++)
-                        if (lb + b >= hshift && lb + b < hshift + ttot) gbase[lb + b] = s_heap[lb + b];
+                    // ragged first/last chunk: its bytes [b0, b1) as byte / 2-byte / 4-byte stores
+                    // at their natural alignment (<= 7 stores instead of 16)
+                    int b0 = max(hshift - lb, 0);
+                    const int b1 = min(hshift + ttot - lb, 16);
+                    while (b0 < b1) {
+                        const int a = lb + b0;
+                        if ((b0 & 1) || b1 - b0 == 1) {
+                            gbase[a] = s_heap[a];
+                            b0 += 1;
+                        } else if ((b0 & 3) || b1 - b0 < 4) {
+                            *reinterpret_cast<uint16_t*>(gbase + a) = *reinterpret_cast<const uint16_t*>(s_heap + a);
+                            b0 += 2;
+                        } else {
+                            *reinterpret_cast<uint32_t*>(gbase + a) = *reinterpret_cast<const uint32_t*>(s_heap + a);
+                            b0 += 4;
+                        }
+                    }
                 }
             }
         }
