@@ -508,6 +508,28 @@ def test_lineitem_scan_every_column(ctx):
             assert_primitive_parity(arr, ctx, np.concatenate(plain[name]))
 
 
+@pytest.mark.parametrize("mean_run", [1, 4, 16, 17, 300])
+def test_runend_run_length_regimes(ctx, mean_run):
+    """Short runs (mean <= 16 rows) expand thread-per-run, long runs by output span: both forms,
+    single arrays and chunks, sliced, and ends that stop short of the length (error)."""
+    rng = np.random.default_rng(mean_run)
+    n_runs = 5000
+    lens = rng.integers(1, 2 * mean_run, n_runs) if mean_run > 1 else np.ones(n_runs, np.int64)
+    vals = np.repeat(rng.integers(-10**12, 10**12, n_runs).astype(np.int64), lens)
+    arr = E.encode_runend(vals)
+    assert_primitive_parity(arr, ctx, vals)
+    arr.meta["offset"] = 5
+    arr.len = vals.size - 9
+    assert_primitive_parity(arr, ctx, vals[5:5 + arr.len])
+    ch = A.chunked([E.encode_runend(vals[:7000]), E.encode_runend(vals[7000:])])
+    assert_primitive_parity(ch, ctx, vals)
+    ends, rv = E.runend_encode(vals)
+    short = A.run_end(A.primitive(ends), A.primitive(rv), length=int(ends[-1]) + 3)
+    with pytest.raises(V.VortexGpuError) as ei:
+        gpu(short, ctx)
+    assert ei.value.kind == "InvalidArgument"
+
+
 def test_chunked_runend_batched(ctx):
     """Chunked[RunEnd]: ends/values decoded with the other chunks' K1 launches into one
     temporary, expansions in shared launches; sliced chunks (offset) and primitive children."""

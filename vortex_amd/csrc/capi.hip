@@ -599,24 +599,31 @@ vxg_status Planner::decode_chunked_primitive(const vxg_array& a, void* dst) {
     VXG_TRY(launch_k1_jobs(jobs, ctx_->c.err_word, s_, plan_));
     for (const PatchJob& p : patches) VXG_TRY(apply_sparse_patches(*p.sp, p.T, p.epi, p.vw, p.a, p.dst, p.out_len));
     runs.erase(std::remove_if(runs.begin(), runs.end(), [](const RunEndChunk& r) { return r.len == 0; }), runs.end());
-    const size_t per = plan_ && runs.size() > size_t(kRunEndArgChunks) ? runs.size() : size_t(kRunEndArgChunks);
-    for (size_t i = 0; i < runs.size(); i += per) {
-        RunEndTable tab{};
-        tab.err = ctx_->c.err_word;
-        RunEndChunk* cs = tab.c;
-        RunEndChunk* host = nullptr;
-        if (per > size_t(kRunEndArgChunks)) {
-            VXG_TRY(plan_->table(runs.size(), &host, &tab.ext));
-            cs = host;
+    // short runs: thread per run; long runs: workgroup per kRunEndSpan outputs
+    std::vector<RunEndChunk> short_runs, long_runs;
+    for (const RunEndChunk& r : runs) (r.len <= kRunEndShortRun * r.n_runs ? short_runs : long_runs).push_back(r);
+    for (int pass = 0; pass < 2; pass++) {
+        std::vector<RunEndChunk>& rs = pass == 0 ? short_runs : long_runs;
+        const size_t per = plan_ && rs.size() > size_t(kRunEndArgChunks) ? rs.size() : size_t(kRunEndArgChunks);
+        for (size_t i = 0; i < rs.size(); i += per) {
+            RunEndTable tab{};
+            tab.err = ctx_->c.err_word;
+            RunEndChunk* cs = tab.c;
+            RunEndChunk* host = nullptr;
+            if (per > size_t(kRunEndArgChunks)) {
+                VXG_TRY(plan_->table(rs.size(), &host, &tab.ext));
+                cs = host;
+            }
+            uint64_t groups = 0;
+            for (size_t k = i; k < rs.size() && k - i < per; k++) {
+                RunEndChunk& r = cs[tab.n++];
+                r = rs[k];
+                r.first_group = groups;
+                groups += pass == 0 ? (r.n_runs + kRunEndRunsPerGroup - 1) / kRunEndRunsPerGroup
+                                    : (r.len + kRunEndSpan - 1) / kRunEndSpan;
+            }
+            VXG_TRY(pass == 0 ? launch_runend_runs(w, tab, groups, s_) : launch_runend_chunks(w, tab, groups, s_));
         }
-        uint64_t groups = 0;
-        for (size_t k = i; k < runs.size() && k - i < per; k++) {
-            RunEndChunk& r = cs[tab.n++];
-            r = runs[k];
-            r.first_group = groups;
-            groups += (r.len + kRunEndSpan - 1) / kRunEndSpan;
-        }
-        VXG_TRY(launch_runend_chunks(w, tab, groups, s_));
     }
     return VXG_OK;
 }

@@ -489,60 +489,8 @@ vxg_status launch_delta(int width, const void* bases, const void* deltas, uint64
 }
 
 // ------------------------------------------------------------------ K8 RunEnd expand
-// Thread per 8 consecutive outputs: upper_bound on ends for the first output, then walk.
-template <typename V>
-__global__ __launch_bounds__(kBlock) void runend_kernel(const V* __restrict__ values, const void* __restrict__ ends,
-                                                        int ends_width, uint64_t n_runs, uint64_t offset,
-                                                        uint64_t len, V* __restrict__ out, uint32_t* err) {
-    constexpr int ITEMS = 8;
-    const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
-    for (uint64_t t = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; t * ITEMS < len; t += stride) {
-        const uint64_t j0 = t * ITEMS;
-        // first run r with (ends[r] - offset) > j0
-        uint64_t lo = 0, hi = n_runs;
-        while (lo < hi) {
-            const uint64_t mid = (lo + hi) >> 1;
-            if (load_uint(ends, ends_width, false, mid) - offset > j0) hi = mid; else lo = mid + 1;
-        }
-        uint64_t r = lo;
-        if (r >= n_runs) {
-            __hip_atomic_fetch_or(err, kErrRunEnd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            continue;
-        }
-        uint64_t end = load_uint(ends, ends_width, false, r) - offset;
-#pragma unroll
-        for (int k = 0; k < ITEMS; k++) {
-            const uint64_t j = j0 + k;
-            if (j >= len) break;
-            while (end <= j && r + 1 < n_runs) {
-                r++;
-                end = load_uint(ends, ends_width, false, r) - offset;
-            }
-            nt_store(out + j, values[r]);
-        }
-    }
-}
-
-vxg_status launch_runend(int value_width, const void* values, int ends_width, const void* ends,
-                         uint64_t n_runs, uint64_t offset, uint64_t len, void* out, uint32_t* err,
-                         hipStream_t s) {
-    if (len == 0) return VXG_OK;
-    if (n_runs == 0) return set_error(VXG_ERR_INVALID_ARGUMENT, "RunEnd with len > 0 has no runs");
-    const unsigned g = grid_for((len + 7) / 8);
-    switch (value_width) {
-#define RE_CASE(W)                                                                                  \
-    case W:                                                                                         \
-        hipLaunchKernelGGL((runend_kernel<typename UInt<W>::t>), dim3(g), dim3(kBlock), 0, s,       \
-                           static_cast<const typename UInt<W>::t*>(values), ends, ends_width,       \
-                           n_runs, offset, len, static_cast<typename UInt<W>::t*>(out), err);       \
-        break;
-        RE_CASE(1) RE_CASE(2) RE_CASE(4) RE_CASE(8) RE_CASE(16)
-#undef RE_CASE
-    default: return VXG_ERR_INVALID_ARGUMENT;
-    }
-    return hip_check(hipGetLastError(), "runend_kernel");
-}
-
+// (kernels below: runend_runs_kernel for short runs, runend_chunks_kernel for long ones; a
+// single array is a one-chunk table, launch_runend at the end of this section)
 // Chunk-table form.  A workgroup expands outputs [j0, j0 + 2048) of one chunk:
 //   * wave 0 finds the runs holding j0 and the range's last output with 64-ary searches over the
 //     ends (3-4 dependent loads, not a 14-step binary search per thread);
@@ -704,6 +652,55 @@ __global__ __launch_bounds__(kBlock) void runend_chunks_kernel(RunEndTable tab) 
     for (int i = tid; i < jn; i += kBlock) nt_store(out + j0 + i, values[r0 + s_head[i]]);
 }
 
+// Short runs (C5's l_orderkey: 1-7 rows per order): one thread per RUN instead of a search per
+// output span.  Thread r loads ends[r - 1], ends[r] and values[r] together (one round trip) and
+// writes its run's trimmed range [min(ends[r-1] - offset, len), min(ends[r] - offset, len)) --
+// runend_decode_primitive's loop (runend/compress.rs:138-146) with every run independent.
+// A wave's stores cover a contiguous stretch of the output, so the L2 merges them into full
+// lines.  Chunks whose runs average > kRunEndShortRun rows take the span kernel above.
+static_assert(kRunEndRunsPerGroup == uint64_t(kBlock), "one run per thread");
+template <typename V>
+__global__ __launch_bounds__(kBlock) void runend_runs_kernel(RunEndTable tab) {
+    const uint64_t g = blockIdx.x;
+    RunEndChunk c;
+    if (tab.ext) {
+        c = tab.ext[ext_chunk_index(tab.ext, tab.n, g, [](RunEndChunk const& d) { return d.first_group; })];
+    } else {
+        uint32_t lo = 0, hi = tab.n;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (tab.c[mid].first_group <= g) lo = mid; else hi = mid;
+        }
+        c = tab.c[lo];
+    }
+    const uint64_t r = (g - c.first_group) * kBlock + threadIdx.x;
+    if (r >= c.n_runs) return;
+    const int ew = int(c.ends_width);
+    const uint64_t e1 = load_uint(c.ends, ew, false, r);
+    const uint64_t e0 = load_uint(c.ends, ew, false, r ? r - 1 : 0);
+    const V v = static_cast<const V*>(c.values)[r];
+    auto trim = [&](uint64_t e) { return e > c.offset ? (e - c.offset < c.len ? e - c.offset : c.len) : 0; };
+    const uint64_t t = trim(e1), st = r ? trim(e0) : 0;
+    V* __restrict__ out = static_cast<V*>(c.out);
+    for (uint64_t j = st; j < t; j++) nt_store(out + j, v);
+    if (r + 1 == c.n_runs && t < c.len)  // the ends do not reach the end of the array
+        __hip_atomic_fetch_or(tab.err, kErrRunEnd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+vxg_status launch_runend_runs(int value_width, const RunEndTable& t, uint64_t groups, hipStream_t s) {
+    if (groups == 0) return VXG_OK;
+    switch (value_width) {
+#define RR_CASE(W)                                                                                                \
+    case W:                                                                                                       \
+        hipLaunchKernelGGL((runend_runs_kernel<typename UInt<W>::t>), dim3(unsigned(groups)), dim3(kBlock), 0, s, t); \
+        break;
+        RR_CASE(1) RR_CASE(2) RR_CASE(4) RR_CASE(8) RR_CASE(16)
+#undef RR_CASE
+    default: return VXG_ERR_INVALID_ARGUMENT;
+    }
+    return hip_check(hipGetLastError(), "runend_runs_kernel");
+}
+
 vxg_status launch_runend_chunks(int value_width, const RunEndTable& t, uint64_t groups, hipStream_t s) {
     if (groups == 0) return VXG_OK;
     switch (value_width) {
@@ -716,6 +713,28 @@ vxg_status launch_runend_chunks(int value_width, const RunEndTable& t, uint64_t 
     default: return VXG_ERR_INVALID_ARGUMENT;
     }
     return hip_check(hipGetLastError(), "runend_chunks_kernel");
+}
+
+vxg_status launch_runend(int value_width, const void* values, int ends_width, const void* ends,
+                         uint64_t n_runs, uint64_t offset, uint64_t len, void* out, uint32_t* err,
+                         hipStream_t s) {
+    if (len == 0) return VXG_OK;
+    if (n_runs == 0) return set_error(VXG_ERR_INVALID_ARGUMENT, "RunEnd with len > 0 has no runs");
+    RunEndTable t{};
+    t.err = err;
+    t.n = 1;
+    RunEndChunk& c = t.c[0];
+    c.values = values;
+    c.ends = ends;
+    c.out = out;
+    c.n_runs = n_runs;
+    c.offset = offset;
+    c.len = len;
+    c.first_group = 0;
+    c.ends_width = uint32_t(ends_width);
+    if (len <= kRunEndShortRun * n_runs)
+        return launch_runend_runs(value_width, t, (n_runs + kRunEndRunsPerGroup - 1) / kRunEndRunsPerGroup, s);
+    return launch_runend_chunks(value_width, t, (len + kRunEndSpan - 1) / kRunEndSpan, s);
 }
 
 // ------------------------------------------------------------------ K10 fill

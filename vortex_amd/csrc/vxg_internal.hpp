@@ -246,6 +246,10 @@ struct RunEndTable {
     const RunEndChunk* ext;  // device table of n entries (plans), or null
 };
 vxg_status launch_runend_chunks(int value_width, const RunEndTable& t, uint64_t groups, hipStream_t s);
+// Thread-per-run form for chunks whose runs are short (first_group counts kBlock runs per group).
+constexpr uint64_t kRunEndShortRun = 16;  // mean rows per run at or below which a chunk uses it
+constexpr uint64_t kRunEndRunsPerGroup = 256;  // one run per thread of a 256-thread workgroup
+vxg_status launch_runend_runs(int value_width, const RunEndTable& t, uint64_t groups, hipStream_t s);
 
 // Batched VarBin -> views (+ copy of the bytes into the output's data buffer), e.g. the
 // dictionaries of a chunked Dict(VarBin) string column.
