@@ -518,12 +518,14 @@ def test_runend_run_length_regimes(ctx, mean_run):
     vals = np.repeat(rng.integers(-10**12, 10**12, n_runs).astype(np.int64), lens)
     arr = E.encode_runend(vals)
     assert_primitive_parity(arr, ctx, vals)
-    arr.meta["offset"] = 5
-    arr.len = vals.size - 9
-    assert_primitive_parity(arr, ctx, vals[5:5 + arr.len])
-    ch = A.chunked([E.encode_runend(vals[:7000]), E.encode_runend(vals[7000:])])
-    assert_primitive_parity(ch, ctx, vals)
     ends, rv = E.runend_encode(vals)
+    # RunEndArray::slice (runend/compute.rs:98-110): runs from the one holding `start`, ends absolute
+    start, length = 5, vals.size - 9
+    sb = int(np.searchsorted(ends, start, side="right"))
+    sl = A.run_end(A.primitive(ends[sb:]), A.primitive(rv[sb:]), length=length, offset=start)
+    assert_primitive_parity(sl, ctx, vals[start:start + length])
+    ch = A.chunked([E.encode_runend(vals[:7000]), sl])
+    assert_primitive_parity(ch, ctx, np.concatenate([vals[:7000], vals[start:start + length]]))
     short = A.run_end(A.primitive(ends), A.primitive(rv), length=int(ends[-1]) + 3)
     with pytest.raises(V.VortexGpuError) as ei:
         gpu(short, ctx)

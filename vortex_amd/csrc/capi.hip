@@ -1710,6 +1710,21 @@ vxg_status vxg_canonicalize(vxg_ctx* ctx, const vxg_array* a, vxg_canonical* out
 // ---- prepared canonicalize --------------------------------------------------------------
 }  // extern "C"
 
+// Bytes a canonicalize of `a` moves (every buffer of the tree read once + the canonical
+// output written): the plan's branch-balancing weight.
+static uint64_t tree_bytes(const vxg_array& a) {
+    uint64_t b = 0;
+    for (uint32_t i = 0; i < a.n_buffers; i++) b += a.buffers[i].len;
+    for (uint32_t i = 0; i < a.n_children; i++) b += tree_bytes(a.children[i]);
+    return b;
+}
+
+static uint64_t plan_cost(const vxg_array& a) {
+    const bool str = a.dtype == VXG_DTYPE_UTF8 || a.dtype == VXG_DTYPE_BINARY;
+    const uint64_t out = a.dtype == VXG_DTYPE_BOOL ? a.len / 8 : a.len * (str ? 16 : ptype_width(a.ptype));
+    return tree_bytes(a) + out;
+}
+
 struct vxg_plan {
     vxg_ctx* ctx = nullptr;
     hipGraph_t graph = nullptr;
@@ -1754,8 +1769,21 @@ vxg_status vxg_plan_create(vxg_ctx* ctx, const vxg_array* arrays, vxg_canonical*
         st = hip_check(hipEventRecord(ev[nb], cs), "fork");
         for (uint32_t b = 0; b < nb && st == VXG_OK; b++)
             st = hip_check(hipStreamWaitEvent(br[b], ev[nb], 0), "fork wait");
-        for (uint32_t i = 0; i < n && st == VXG_OK; i++) {
-            Planner p(ctx, br[i % nb], &pl->store);
+        // longest-processing-time-first: arrays in decreasing order of the bytes their decode
+        // moves, each onto the branch with the least work so far, so one heavy column (C5's
+        // l_comment) does not queue behind others on its branch
+        std::vector<uint32_t> order(n);
+        std::vector<uint64_t> cost(n), load(nb, 0);
+        for (uint32_t i = 0; i < n; i++) {
+            order[i] = i;
+            cost[i] = plan_cost(arrays[i]);
+        }
+        std::stable_sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return cost[x] > cost[y]; });
+        for (uint32_t k = 0; k < n && st == VXG_OK; k++) {
+            const uint32_t i = order[k];
+            const uint32_t b = uint32_t(std::min_element(load.begin(), load.end()) - load.begin());
+            load[b] += cost[i];
+            Planner p(ctx, br[b], &pl->store);
             st = p.canonical(arrays[i], outs[i]);
         }
         for (uint32_t b = 0; b < nb && st == VXG_OK; b++) {
