@@ -652,15 +652,23 @@ __global__ __launch_bounds__(kBlock) void runend_chunks_kernel(RunEndTable tab) 
     for (int i = tid; i < jn; i += kBlock) nt_store(out + j0 + i, values[r0 + s_head[i]]);
 }
 
-// Short runs (C5's l_orderkey: 1-7 rows per order): one thread per RUN instead of a search per
-// output span.  Thread r loads ends[r - 1], ends[r] and values[r] together (one round trip) and
-// writes its run's trimmed range [min(ends[r-1] - offset, len), min(ends[r] - offset, len)) --
-// runend_decode_primitive's loop (runend/compress.rs:138-146) with every run independent.
-// A wave's stores cover a contiguous stretch of the output, so the L2 merges them into full
-// lines.  Chunks whose runs average > kRunEndShortRun rows take the span kernel above.
-static_assert(kRunEndRunsPerGroup == uint64_t(kBlock), "one run per thread");
+// Short runs (C5's l_orderkey: 1-7 rows per order): a workgroup takes 256 consecutive RUNS
+// (not an output span), so no search is needed: thread r loads ends[r - 1], ends[r] and
+// values[r] in one round trip; its run covers the trimmed range
+// [min(ends[r-1] - offset, len), min(ends[r] - offset, len)) (runend_decode_primitive,
+// runend/compress.rs:138-146), and the workgroup's runs cover one contiguous output range.
+// That range is expanded in windows of 4096 outputs: each non-empty run writes its index at
+// its first output (a run head), a max-scan fills the window, and the window is written with
+// coalesced non-temporal stores (the run carried into the next window is the last scanned one).
+// Chunks whose runs average > kRunEndShortRun rows take the span kernel above.
 template <typename V>
 __global__ __launch_bounds__(kBlock) void runend_runs_kernel(RunEndTable tab) {
+    constexpr int SPAN = 4096, PER = SPAN / kBlock;
+    __shared__ uint32_t s_head[SPAN];
+    __shared__ V s_val[kBlock];
+    __shared__ uint32_t s_wmax[kBlock / 64];
+    __shared__ uint64_t s_range[2];
+    __shared__ uint32_t s_carry;
     const uint64_t g = blockIdx.x;
     RunEndChunk c;
     if (tab.ext) {
@@ -673,18 +681,65 @@ __global__ __launch_bounds__(kBlock) void runend_runs_kernel(RunEndTable tab) {
         }
         c = tab.c[lo];
     }
-    const uint64_t r = (g - c.first_group) * kBlock + threadIdx.x;
-    if (r >= c.n_runs) return;
+    const int tid = threadIdx.x;
+    const uint64_t r0 = (g - c.first_group) * kBlock;
+    const int nr = int(c.n_runs - r0 < uint64_t(kBlock) ? c.n_runs - r0 : uint64_t(kBlock));
+    const uint64_t r = r0 + tid;
+    const bool has = tid < nr;
     const int ew = int(c.ends_width);
-    const uint64_t e1 = load_uint(c.ends, ew, false, r);
-    const uint64_t e0 = load_uint(c.ends, ew, false, r ? r - 1 : 0);
-    const V v = static_cast<const V*>(c.values)[r];
+    const uint64_t rr = has ? r : r0;
+    const uint64_t e1 = load_uint(c.ends, ew, false, rr);
+    const uint64_t e0 = load_uint(c.ends, ew, false, rr ? rr - 1 : 0);
+    const V v = static_cast<const V*>(c.values)[rr];
     auto trim = [&](uint64_t e) { return e > c.offset ? (e - c.offset < c.len ? e - c.offset : c.len) : 0; };
-    const uint64_t t = trim(e1), st = r ? trim(e0) : 0;
-    V* __restrict__ out = static_cast<V*>(c.out);
-    for (uint64_t j = st; j < t; j++) nt_store(out + j, v);
-    if (r + 1 == c.n_runs && t < c.len)  // the ends do not reach the end of the array
+    const uint64_t t = has ? trim(e1) : 0, st = has ? (r ? trim(e0) : 0) : 0;
+    s_val[tid] = v;
+    if (tid == 0) s_range[0] = st;
+    if (tid == nr - 1) s_range[1] = t;
+    if (has && r + 1 == c.n_runs && t < c.len)  // the ends do not reach the end of the array
         __hip_atomic_fetch_or(tab.err, kErrRunEnd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const uint64_t lo = s_range[0], hi = s_range[1];
+    V* __restrict__ out = static_cast<V*>(c.out);
+    uint32_t carry = 0;
+    for (uint64_t wb = lo; wb < hi; wb += SPAN) {
+        const int wn = int(hi - wb < uint64_t(SPAN) ? hi - wb : uint64_t(SPAN));
+#pragma unroll
+        for (int k = 0; k < PER; k++) s_head[tid * PER + k] = 0;
+        __syncthreads();
+        if (has && t > st && st >= wb && st < wb + uint64_t(wn)) s_head[st - wb] = uint32_t(tid) + 1;
+        __syncthreads();
+        // inclusive max-scan of s_head (thread t owns entries [PER t, PER t + PER)), seeded
+        // with the run carried over from the previous window
+        uint32_t vv[PER];
+        uint32_t m = 0;
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            m = max(m, s_head[tid * PER + k]);
+            vv[k] = m;
+        }
+        uint32_t x = m;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d, 64);
+            if ((tid & 63) >= d) x = max(x, y);
+        }
+        if ((tid & 63) == 63) s_wmax[tid >> 6] = x;
+        __syncthreads();
+        uint32_t before = __shfl_up(x, 1, 64);
+        if ((tid & 63) == 0) before = 0;
+#pragma unroll
+        for (int w = 0; w < kBlock / 64; w++)
+            if (w < (tid >> 6)) before = max(before, s_wmax[w]);
+        before = max(before, carry);
+#pragma unroll
+        for (int k = 0; k < PER; k++) s_head[tid * PER + k] = max(vv[k], before);
+        __syncthreads();
+        for (int i = tid; i < wn; i += kBlock) nt_store(out + wb + i, s_val[s_head[i] - 1]);
+        if (tid == 0) s_carry = s_head[wn - 1];
+        __syncthreads();
+        carry = s_carry;
+    }
 }
 
 vxg_status launch_runend_runs(int value_width, const RunEndTable& t, uint64_t groups, hipStream_t s) {
