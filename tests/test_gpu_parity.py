@@ -6,6 +6,7 @@ with the oracle's CPU canonicalize of the same tree (tests/oracle_tree.py) — a
 original data (decode(encode(x)) == x).  Floating point is compared as raw bits.
 """
 import ctypes as C
+import dataclasses
 
 import numpy as np
 import pytest
@@ -530,6 +531,52 @@ def test_runend_run_length_regimes(ctx, mean_run):
     with pytest.raises(V.VortexGpuError) as ei:
         gpu(short, ctx)
     assert ei.value.kind == "InvalidArgument"
+
+
+def _slice_bitpacked(bp, start, length):
+    """BitPackedArray::slice (bitpacking/compute/slice.rs): whole blocks from the one holding
+    `start`, offset = start % 1024."""
+    w = bp.meta["bit_width"]
+    b0, b1 = start // 1024, (start + length + 1023) // 1024
+    packed = bp.buffers[0][b0 * 128 * w: b1 * 128 * w]
+    return A.bitpacked(packed, bp.ptype, w, length, offset=start % 1024)
+
+
+@pytest.mark.parametrize("vdt", [np.int32, np.uint32, np.int64, np.uint64, np.float64])
+def test_runend_short_runs_packed_children_in_place(ctx, vdt):
+    """Short-run RunEnd whose ends are BitPacked and values FoR(BitPacked) (C5's l_orderkey):
+    the runs kernel unpacks both children in place.  Single arrays and chunks, children sliced
+    inside a FastLanes block (BitPacked offset), FoR with negative references, float values
+    (plain bits), and a chunk mix with long-run chunks (plain temporaries)."""
+    rng = np.random.default_rng(np.dtype(vdt).itemsize * 7 + (vdt == np.float64))
+    n_runs = 9000
+    lens = rng.integers(1, 8, n_runs)
+    if vdt == np.float64:
+        rv = rng.standard_normal(n_runs)
+    else:
+        lo = -(1 << 20) if np.dtype(vdt).kind == "i" else 0
+        rv = rng.integers(lo, 1 << 21, n_runs).astype(vdt)
+    vals = np.repeat(rv, lens)
+    arr = E.encode_runend(vals, compress_values=True)
+    assert_primitive_parity(arr, ctx, vals)
+    ends, rvv = E.runend_encode(vals)
+    # children sliced at a non-block boundary: runs [sb, sb + m) of the full encoding
+    sb, m = 1500, 6000
+    e_full = E.encode_bitpacked(ends, allow_patches=False)
+    e_sl = _slice_bitpacked(e_full, sb, m)
+    if rvv.dtype.kind in "iu":
+        v_full = E.encode_for_bitpacked(rvv)
+        inner = _slice_bitpacked(v_full.children[0], sb, m)
+        v_sl = dataclasses.replace(v_full, len=m, children=[inner])  # FoRArray::slice
+    else:
+        v_sl = A.primitive(rvv[sb:sb + m])
+    start = int(ends[sb - 1]) + 2  # a slice starting inside run sb
+    length = int(ends[sb + m - 1]) - start - 3
+    sl = A.run_end(e_sl, v_sl, length=length, offset=start)
+    assert_primitive_parity(sl, ctx, vals[start:start + length])
+    long_vals = np.repeat(rv[:200], 50)
+    ch = A.chunked([arr, sl, E.encode_runend(long_vals, compress_values=True), arr])
+    assert_primitive_parity(ch, ctx, np.concatenate([vals, vals[start:start + length], long_vals, vals]))
 
 
 def test_chunked_runend_batched(ctx):

@@ -299,6 +299,10 @@ class Planner {
     // Canonical primitive values of `a` as a device pointer (aliases PRIMITIVE buffers).
     vxg_status view_primitive(const vxg_array& a, const void** p);
     vxg_status int_column(const vxg_array& a, IntCol& c);
+    // a patch-free 32/64-bit [FoR](BitPacked) integer column as a packed IntCol (*packed = true),
+    // validated; otherwise *packed = false and nothing is decoded
+    vxg_status packed_column(const vxg_array& a, IntCol& c, bool* packed);
+    vxg_status runend_column(const vxg_array& a, bool in_place, IntCol& c);
 
     vxg_status decode_bitpacked(const vxg_array& bp, Epi epi, int vw, UnpackArgs a, void* dst);
     vxg_status apply_sparse_patches(const vxg_array& sparse, int T, Epi epi, int vw, const UnpackArgs& a,
@@ -343,6 +347,25 @@ vxg_status Planner::int_column(const vxg_array& a, IntCol& c) {
     // [FoR](BitPacked) column stays packed (elements unpacked where used); anything else is
     // canonicalized to a primitive buffer first.
     if (!ptype_is_int(a.ptype)) return set_error(VXG_ERR_MISMATCHED_TYPES, "expected an integer array");
+    bool packed = false;
+    VXG_TRY(packed_column(a, c, &packed));
+    return packed ? VXG_OK : view_primitive(a, &c.p);
+}
+
+vxg_status Planner::runend_column(const vxg_array& a, bool in_place, IntCol& c) {
+    // RunEnd ends/values: read in place by the short-run kernel when packable, else a plain
+    // buffer (canonicalized child-first).  Non-integer values (floats) are plain bits.
+    bool packed = false;
+    if (in_place && ptype_is_int(a.ptype)) VXG_TRY(packed_column(a, c, &packed));
+    if (packed) return VXG_OK;
+    c = IntCol{};
+    c.width = width(a);
+    c.sgn = ptype_is_signed(a.ptype);
+    return view_primitive(a, &c.p);
+}
+
+vxg_status Planner::packed_column(const vxg_array& a, IntCol& c, bool* packed) {
+    *packed = false;
     c = IntCol{};
     c.width = width(a);
     c.sgn = ptype_is_signed(a.ptype);
@@ -356,22 +379,22 @@ vxg_status Planner::int_column(const vxg_array& a, IntCol& c) {
     }
     if (bp && !bp->meta.bitpacked.has_patches && width(*bp) == c.width && (c.width == 4 || c.width == 8) &&
         bp->len == a.len) {
-        const vxg_buffer* packed = buf(*bp, 0);
+        const vxg_buffer* pk = buf(*bp, 0);
         const unsigned W = bp->meta.bitpacked.bit_width, off = bp->meta.bitpacked.offset;
         const uint64_t nblk = (bp->len + off + 1023) / 1024;
         if (off > 1023) return set_error(VXG_ERR_INVALID_ARGUMENT, "Offset must be less than full block, i.e. 1024");
         if (W > unsigned(8 * c.width)) return set_error(VXG_ERR_INVALID_ARGUMENT, "Unsupported bit width");
-        const uint64_t have = packed ? packed->len : 0;
+        const uint64_t have = pk ? pk->len : 0;
         if (W > 0 && have != nblk * 128ull * W)  // bitpacking/mod.rs:80-88
             return set_error(VXG_ERR_INVALID_ARGUMENT, "Expected " + std::to_string(nblk * 128ull * W) +
                                                            " packed bytes, got " + std::to_string(have));
         c.packed = true;
-        c.p = packed ? packed->ptr : nullptr;
+        c.p = pk ? pk->ptr : nullptr;
         c.W = W;
         c.offset = off;
-        return VXG_OK;
+        *packed = true;
     }
-    return view_primitive(a, &c.p);
+    return VXG_OK;
 }
 
 vxg_status Planner::apply_sparse_patches(const vxg_array& sp, int T, Epi epi, int vw, const UnpackArgs& a,
@@ -533,14 +556,23 @@ vxg_status Planner::decode_chunked_primitive(const vxg_array& a, void* dst) {
         return c.encoding == VXG_ENC_RUN_END && child_ok(e) && v && width(*v) == w && e->len == v->len &&
                (v->encoding == VXG_ENC_PRIMITIVE || k1_fusable(*v)) && e->len > 0;
     };
+    // short-run chunks read packed ends/values in place (no temporary, no level-0 launch)
+    std::vector<IntCol> inplace(2 * n);
+    std::vector<uint8_t> is_inplace(2 * n, 0);
     uint64_t tmp_bytes = 0;
     for (uint64_t i = 0; i < n; i++) {
         const vxg_array& c = a.children[i + 1];
         if (!batch_runend(c)) continue;
         const vxg_array* e = child(c, 0);
         const vxg_array* v = child(c, 1);
-        if (e->encoding != VXG_ENC_PRIMITIVE) tmp_bytes += (e->len * width(*e) + 15) & ~15ull;
-        if (v->encoding != VXG_ENC_PRIMITIVE) tmp_bytes += (v->len * width(*v) + 15) & ~15ull;
+        const bool short_runs = c.len <= kRunEndShortRun * e->len;
+        const vxg_array* xs[2] = {e, v};
+        for (int k = 0; k < 2; k++) {
+            bool pk = false;
+            if (short_runs && ptype_is_int(xs[k]->ptype)) VXG_TRY(packed_column(*xs[k], inplace[2 * i + k], &pk));
+            is_inplace[2 * i + k] = pk;
+            if (!pk && xs[k]->encoding != VXG_ENC_PRIMITIVE) tmp_bytes += (xs[k]->len * width(*xs[k]) + 15) & ~15ull;
+        }
     }
     uint8_t* tmp = nullptr;
     if (tmp_bytes) {
@@ -578,13 +610,21 @@ vxg_status Planner::decode_chunked_primitive(const vxg_array& a, void* dst) {
             const vxg_array& e = *child(c, 0);
             const vxg_array& v = *child(c, 1);
             RunEndChunk r{};
-            VXG_TRY(level0(e, &r.ends));
-            VXG_TRY(level0(v, &r.values));
+            IntCol* cols[2] = {&r.ends, &r.values};
+            const vxg_array* xs[2] = {&e, &v};
+            for (int k = 0; k < 2; k++) {
+                if (is_inplace[2 * i + k]) {
+                    *cols[k] = inplace[2 * i + k];
+                } else {
+                    cols[k]->width = width(*xs[k]);
+                    cols[k]->sgn = ptype_is_signed(xs[k]->ptype);
+                    VXG_TRY(level0(*xs[k], &cols[k]->p));
+                }
+            }
             r.out = slice;
             r.n_runs = e.len;
             r.offset = c.meta.runend.offset;
             r.len = c.len;
-            r.ends_width = uint32_t(width(e));
             runs.push_back(r);
         } else if ((reinterpret_cast<uintptr_t>(slice) & 15) == 0) {
             VXG_TRY(decode_into(c, slice));
@@ -735,11 +775,14 @@ vxg_status Planner::decode_into(const vxg_array& a, void* dst) {
         const vxg_array* values = child(a, 1);
         if (!ends || !values) return set_error(VXG_ERR_INVALID_ARGUMENT, "RunEndArray needs ends and values");
         if (ends->len != values->len) return set_error(VXG_ERR_INVALID_ARGUMENT, "RunEnd ends/values length mismatch");
-        const void *pe, *pv;
-        VXG_TRY(view_primitive(*ends, &pe));
-        VXG_TRY(view_primitive(*values, &pv));
-        return launch_runend(w, pv, width(*ends), pe, ends->len, a.meta.runend.offset, a.len, dst,
-                             ctx_->c.err_word, s_);
+        RunEndChunk c{};
+        c.out = dst;
+        c.n_runs = ends->len;
+        c.offset = a.meta.runend.offset;
+        c.len = a.len;
+        VXG_TRY(runend_column(*ends, a.len <= kRunEndShortRun * ends->len, c.ends));
+        VXG_TRY(runend_column(*values, a.len <= kRunEndShortRun * ends->len, c.values));
+        return launch_runend(w, c, ctx_->c.err_word, s_);
     }
     case VXG_ENC_SPARSE:
         return decode_sparse_values(a, dst);
@@ -1970,8 +2013,17 @@ vxg_status vxg_runend_decode(vxg_ctx* ctx, unsigned value_width, const void* val
                              void* stream) {
     VXG_TRY(use_device(ctx));
     if (!ptype_is_int(ends_ptype)) return set_error(VXG_ERR_MISMATCHED_TYPES, "RunEnd ends must be integers");
-    return launch_runend(int(value_width), values, ptype_width(ends_ptype), ends, n_runs, offset, len, out,
-                         ctx->c.err_word, S(stream));
+    RunEndChunk c{};
+    c.ends.p = ends;
+    c.ends.width = ptype_width(ends_ptype);
+    c.ends.sgn = ptype_is_signed(ends_ptype);
+    c.values.p = values;
+    c.values.width = int(value_width);
+    c.out = out;
+    c.n_runs = n_runs;
+    c.offset = offset;
+    c.len = len;
+    return launch_runend(int(value_width), c, ctx->c.err_word, S(stream));
 }
 
 vxg_status vxg_take_array(vxg_ctx* ctx, const vxg_array* a, int indices_ptype, const void* indices,

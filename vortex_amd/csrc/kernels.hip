@@ -590,17 +590,18 @@ __global__ __launch_bounds__(kBlock) void runend_chunks_kernel(RunEndTable tab) 
         }
         c = tab.c[lo];
     }
-    const V* __restrict__ values = static_cast<const V*>(c.values);
+    const V* __restrict__ values = static_cast<const V*>(c.values.p);  // plain columns only
+    const void* ends = c.ends.p;
     V* __restrict__ out = static_cast<V*>(c.out);
-    const int ew = int(c.ends_width), tid = threadIdx.x;
+    const int ew = c.ends.width, tid = threadIdx.x;
     const uint64_t j0 = (g - c.first_group) * SPAN;
     const int jn = int(c.len - j0 < uint64_t(SPAN) ? c.len - j0 : uint64_t(SPAN));
     const uint64_t jend = j0 + uint64_t(jn);
     if (tid < 64) {
-        const uint64_t r0 = runend_locate(c.ends, ew, c.offset, c.n_runs, c.len, j0);
+        const uint64_t r0 = runend_locate(ends, ew, c.offset, c.n_runs, c.len, j0);
         if (tid == 0) s_r0 = r0;
     } else if (tid == 64) {  // the last run must reach the chunk's end
-        s_bad = c.n_runs == 0 || load_uint(c.ends, ew, false, c.n_runs - 1) - c.offset < c.len;
+        s_bad = c.n_runs == 0 || load_uint(ends, ew, false, c.n_runs - 1) - c.offset < c.len;
     }
 #pragma unroll
     for (int k = 0; k < PER; k++) s_head[tid + k * kBlock] = 0;
@@ -617,7 +618,7 @@ __global__ __launch_bounds__(kBlock) void runend_chunks_kernel(RunEndTable tab) 
 #pragma unroll
         for (int q = 0; q < Q; q++) {
             const uint64_t r = rb + uint64_t(q) * kBlock + uint64_t(tid);
-            st[q] = r + 1 < c.n_runs ? load_uint(c.ends, ew, false, r) - c.offset : ~0ull;
+            st[q] = r + 1 < c.n_runs ? load_uint(ends, ew, false, r) - c.offset : ~0ull;
         }
 #pragma unroll
         for (int q = 0; q < Q; q++)
@@ -652,22 +653,34 @@ __global__ __launch_bounds__(kBlock) void runend_chunks_kernel(RunEndTable tab) 
     for (int i = tid; i < jn; i += kBlock) nt_store(out + j0 + i, values[r0 + s_head[i]]);
 }
 
-// Short runs (C5's l_orderkey: 1-7 rows per order): a workgroup takes 256 consecutive RUNS
-// (not an output span), so no search is needed: thread r loads ends[r - 1], ends[r] and
-// values[r] in one round trip; its run covers the trimmed range
+// Short runs (C5's l_orderkey: 1-7 rows per order): a workgroup takes 1024 consecutive RUNS
+// (not an output span), so no search is needed: thread t reads ends[r] and values[r] of runs
+// r0 + t + 256 k (k < 4) in one round trip -- from plain buffers, or unpacked in place from
+// patch-free [FoR](BitPacked) children (fastlanes unpack_single, bitpacking/compress.rs:295-306),
+// so the children are never materialised.  Run r covers the trimmed range
 // [min(ends[r-1] - offset, len), min(ends[r] - offset, len)) (runend_decode_primitive,
-// runend/compress.rs:138-146), and the workgroup's runs cover one contiguous output range.
-// That range is expanded in windows of 4096 outputs: each non-empty run writes its index at
-// its first output (a run head), a max-scan fills the window, and the window is written with
-// coalesced non-temporal stores (the run carried into the next window is the last scanned one).
-// Chunks whose runs average > kRunEndShortRun rows take the span kernel above.
+// runend/compress.rs:138-146; the previous end comes through LDS), and the workgroup's runs cover
+// one contiguous output range.  That range is expanded in windows of 4096 outputs: each
+// non-empty run writes its index at its first output (a run head), a max-scan fills the window,
+// and the window is written with coalesced non-temporal stores (the run carried into the next
+// window is the last scanned one).  Chunks whose runs average > kRunEndShortRun rows take the
+// span kernel above.
+template <typename V>
+__device__ __forceinline__ V runend_value(const IntCol& c, uint64_t r) {
+    if constexpr (sizeof(V) == 4 || sizeof(V) == 8) {
+        if (c.packed) return V(uint64_t(intcol_get(c, r)));  // low bytes: the value's bits
+    }
+    return static_cast<const V*>(c.p)[r];
+}
+
 template <typename V>
 __global__ __launch_bounds__(kBlock) void runend_runs_kernel(RunEndTable tab) {
-    constexpr int SPAN = 4096, PER = SPAN / kBlock;
-    __shared__ uint32_t s_head[SPAN];
-    __shared__ V s_val[kBlock];
+    constexpr int SPAN = 4096, PER = SPAN / kBlock, RPG = int(kRunEndRunsPerGroup), RPT = RPG / kBlock;
+    __shared__ __attribute__((aligned(16))) uint32_t s_head[SPAN];
+    __shared__ V s_val[RPG];
+    __shared__ uint64_t s_end[RPG];
     __shared__ uint32_t s_wmax[kBlock / 64];
-    __shared__ uint64_t s_range[2];
+    __shared__ uint64_t s_lo;
     __shared__ uint32_t s_carry;
     const uint64_t g = blockIdx.x;
     RunEndChunk c;
@@ -682,32 +695,53 @@ __global__ __launch_bounds__(kBlock) void runend_runs_kernel(RunEndTable tab) {
         c = tab.c[lo];
     }
     const int tid = threadIdx.x;
-    const uint64_t r0 = (g - c.first_group) * kBlock;
-    const int nr = int(c.n_runs - r0 < uint64_t(kBlock) ? c.n_runs - r0 : uint64_t(kBlock));
-    const uint64_t r = r0 + tid;
-    const bool has = tid < nr;
-    const int ew = int(c.ends_width);
-    const uint64_t rr = has ? r : r0;
-    const uint64_t e1 = load_uint(c.ends, ew, false, rr);
-    const uint64_t e0 = load_uint(c.ends, ew, false, rr ? rr - 1 : 0);
-    const V v = static_cast<const V*>(c.values)[rr];
+    const uint64_t r0 = (g - c.first_group) * uint64_t(RPG);
+    const int nr = int(c.n_runs - r0 < uint64_t(RPG) ? c.n_runs - r0 : uint64_t(RPG));
     auto trim = [&](uint64_t e) { return e > c.offset ? (e - c.offset < c.len ? e - c.offset : c.len) : 0; };
-    const uint64_t t = has ? trim(e1) : 0, st = has ? (r ? trim(e0) : 0) : 0;
-    s_val[tid] = v;
-    if (tid == 0) s_range[0] = st;
-    if (tid == nr - 1) s_range[1] = t;
-    if (has && r + 1 == c.n_runs && t < c.len)  // the ends do not reach the end of the array
-        __hip_atomic_fetch_or(tab.err, kErrRunEnd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // every load of the round trip issued before any is used
+    uint64_t e[RPT];
+    V v[RPT];
+#pragma unroll
+    for (int k = 0; k < RPT; k++) {
+        const int i = tid + k * kBlock;
+        const uint64_t rr = r0 + uint64_t(i < nr ? i : 0);
+        e[k] = uint64_t(intcol_get(c.ends, rr));
+        v[k] = runend_value<V>(c.values, rr);
+    }
+    const uint64_t eprev = tid == 0 && r0 > 0 ? uint64_t(intcol_get(c.ends, r0 - 1)) : 0;
+#pragma unroll
+    for (int k = 0; k < RPT; k++) {
+        const int i = tid + k * kBlock;
+        if (i < nr) {
+            const uint64_t t = trim(e[k]);
+            s_end[i] = t;
+            s_val[i] = v[k];
+            if (r0 + uint64_t(i) + 1 == c.n_runs && t < c.len)  // the ends do not reach the end of the array
+                __hip_atomic_fetch_or(tab.err, kErrRunEnd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    if (tid == 0) s_lo = r0 > 0 ? trim(eprev) : 0;
     __syncthreads();
-    const uint64_t lo = s_range[0], hi = s_range[1];
+    const uint64_t lo = s_lo, hi = s_end[nr - 1];
+    // run starts (the previous run's trimmed end)
+    uint64_t st[RPT], en[RPT];
+#pragma unroll
+    for (int k = 0; k < RPT; k++) {
+        const int i = tid + k * kBlock;
+        en[k] = i < nr ? s_end[i] : 0;
+        st[k] = i < nr ? (i > 0 ? s_end[i - 1] : lo) : 0;
+    }
     V* __restrict__ out = static_cast<V*>(c.out);
     uint32_t carry = 0;
     for (uint64_t wb = lo; wb < hi; wb += SPAN) {
         const int wn = int(hi - wb < uint64_t(SPAN) ? hi - wb : uint64_t(SPAN));
 #pragma unroll
-        for (int k = 0; k < PER; k++) s_head[tid * PER + k] = 0;
+        for (int k = 0; k < PER / 4; k++) reinterpret_cast<uint4*>(s_head)[tid * (PER / 4) + k] = make_uint4(0, 0, 0, 0);
         __syncthreads();
-        if (has && t > st && st >= wb && st < wb + uint64_t(wn)) s_head[st - wb] = uint32_t(tid) + 1;
+#pragma unroll
+        for (int k = 0; k < RPT; k++)
+            if (en[k] > st[k] && st[k] >= wb && st[k] < wb + uint64_t(wn))
+                s_head[st[k] - wb] = uint32_t(tid + k * kBlock) + 1;
         __syncthreads();
         // inclusive max-scan of s_head (thread t owns entries [PER t, PER t + PER)), seeded
         // with the run carried over from the previous window
@@ -770,26 +804,19 @@ vxg_status launch_runend_chunks(int value_width, const RunEndTable& t, uint64_t 
     return hip_check(hipGetLastError(), "runend_chunks_kernel");
 }
 
-vxg_status launch_runend(int value_width, const void* values, int ends_width, const void* ends,
-                         uint64_t n_runs, uint64_t offset, uint64_t len, void* out, uint32_t* err,
-                         hipStream_t s) {
-    if (len == 0) return VXG_OK;
-    if (n_runs == 0) return set_error(VXG_ERR_INVALID_ARGUMENT, "RunEnd with len > 0 has no runs");
+vxg_status launch_runend(int value_width, const RunEndChunk& chunk, uint32_t* err, hipStream_t s) {
+    if (chunk.len == 0) return VXG_OK;
+    if (chunk.n_runs == 0) return set_error(VXG_ERR_INVALID_ARGUMENT, "RunEnd with len > 0 has no runs");
     RunEndTable t{};
     t.err = err;
     t.n = 1;
-    RunEndChunk& c = t.c[0];
-    c.values = values;
-    c.ends = ends;
-    c.out = out;
-    c.n_runs = n_runs;
-    c.offset = offset;
-    c.len = len;
-    c.first_group = 0;
-    c.ends_width = uint32_t(ends_width);
-    if (len <= kRunEndShortRun * n_runs)
-        return launch_runend_runs(value_width, t, (n_runs + kRunEndRunsPerGroup - 1) / kRunEndRunsPerGroup, s);
-    return launch_runend_chunks(value_width, t, (len + kRunEndSpan - 1) / kRunEndSpan, s);
+    t.c[0] = chunk;
+    t.c[0].first_group = 0;
+    if (chunk.len <= kRunEndShortRun * chunk.n_runs)
+        return launch_runend_runs(value_width, t, (chunk.n_runs + kRunEndRunsPerGroup - 1) / kRunEndRunsPerGroup, s);
+    if (chunk.ends.packed || chunk.values.packed)
+        return set_error(VXG_ERR_INVALID_ARGUMENT, "long-run RunEnd expansion reads plain ends/values");
+    return launch_runend_chunks(value_width, t, (chunk.len + kRunEndSpan - 1) / kRunEndSpan, s);
 }
 
 // ------------------------------------------------------------------ K10 fill

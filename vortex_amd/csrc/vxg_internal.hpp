@@ -223,22 +223,23 @@ VXG_DECL_DICT(16)
 constexpr int kDictFusedMaxW = 16;
 vxg_status launch_delta(int width, const void* bases, const void* deltas, uint64_t n_deltas,
                         uint64_t offset, uint64_t len, void* out, hipStream_t s);
-vxg_status launch_runend(int value_width, const void* values, int ends_width, const void* ends,
-                         uint64_t n_runs, uint64_t offset, uint64_t len, void* out, uint32_t* err,
-                         hipStream_t s);
 // Batched RunEnd expansion: many chunks' runs in one launch (chunk table as kernel argument).
+// ends/values: plain buffers, or (short-run kernel only) patch-free [FoR](BitPacked) 32/64-bit
+// columns read in place -- the runs kernel unpacks the elements it needs, so a
+// RunEnd(ends=BitPacked, values=FoR(BitPacked)) chunk is ONE launch with no temporaries.
+// values.width is the output width (1..16); a packed values column has width 4 or 8.
 struct RunEndChunk {
-    const void* values;
-    const void* ends;
+    IntCol ends;
+    IntCol values;
     void* out;
     uint64_t n_runs;
     uint64_t offset;
     uint64_t len;
-    uint64_t first_group;  // first workgroup of this chunk (kRunEndSpan outputs per workgroup)
-    uint32_t ends_width;
+    uint64_t first_group;  // first workgroup of this chunk in the launch
 };
+vxg_status launch_runend(int value_width, const RunEndChunk& chunk, uint32_t* err, hipStream_t s);
 constexpr uint64_t kRunEndSpan = 4096;
-constexpr int kRunEndArgChunks = 48;
+constexpr int kRunEndArgChunks = 32;
 struct RunEndTable {
     RunEndChunk c[kRunEndArgChunks];
     uint32_t n;
@@ -248,7 +249,7 @@ struct RunEndTable {
 vxg_status launch_runend_chunks(int value_width, const RunEndTable& t, uint64_t groups, hipStream_t s);
 // Thread-per-run form for chunks whose runs are short (first_group counts kBlock runs per group).
 constexpr uint64_t kRunEndShortRun = 16;  // mean rows per run at or below which a chunk uses it
-constexpr uint64_t kRunEndRunsPerGroup = 256;  // one run per thread of a 256-thread workgroup
+constexpr uint64_t kRunEndRunsPerGroup = 1024;  // four runs per thread of a 256-thread workgroup
 vxg_status launch_runend_runs(int value_width, const RunEndTable& t, uint64_t groups, hipStream_t s);
 
 // Batched VarBin -> views (+ copy of the bytes into the output's data buffer), e.g. the
