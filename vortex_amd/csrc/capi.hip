@@ -1768,6 +1768,16 @@ static uint64_t plan_cost(const vxg_array& a) {
     return tree_bytes(a) + out;
 }
 
+// Parallel graph branches of a plan (VXG_PLAN_BRANCHES overrides, 1..16).
+static uint32_t plan_branches() {
+    static const uint32_t nb = [] {
+        const char* e = std::getenv("VXG_PLAN_BRANCHES");
+        const long v = e ? std::strtol(e, nullptr, 10) : 0;
+        return v >= 1 && v <= 16 ? uint32_t(v) : 2u;
+    }();
+    return nb;
+}
+
 struct vxg_plan {
     vxg_ctx* ctx = nullptr;
     hipGraph_t graph = nullptr;
@@ -1790,11 +1800,12 @@ vxg_status vxg_plan_create(vxg_ctx* ctx, const vxg_array* arrays, vxg_canonical*
         if (a.nullable && !o.validity)
             return set_error(VXG_ERR_INVALID_ARGUMENT, "a plan needs caller-allocated validity for nullable arrays");
     }
-    // Record on an origin stream forked into up to kPlanBranches streams: the arrays are
+    // Record on an origin stream forked into kPlanBranches streams (2: measured 0.343-0.358
+    // ms/step on C5 vs 0.363-0.364 with 4 and 0.389 with 1, tools/gpu_branches.sh): the arrays are
     // independent, so their launches become parallel graph branches (the graph runs them on
     // several hardware queues, overlapping the ramp and drain of the many small kernels of a
     // chunked scan), joined back into the origin stream.
-    constexpr uint32_t kPlanBranches = 4;
+    const uint32_t kPlanBranches = plan_branches();
     const uint32_t nb = n < kPlanBranches ? (n ? n : 1) : kPlanBranches;
     hipStream_t cs;
     VXG_TRY(hip_check(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking), "plan stream"));

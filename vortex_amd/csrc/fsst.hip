@@ -166,14 +166,31 @@ __device__ __forceinline__ int block_excl_scan32(int v, int* ws, int& total) {
 // Pre-pass: per workgroup of 128 tiles, the tile length sums, their exclusive scan
 // (tile_prefix) and the workgroup total (block_totals).  The decode adds the totals of the
 // preceding workgroups (<= a few hundred) itself.
+// The absolute code offset at which each tile's codes end (code_offs[min(256 (t + 1), n)]): the
+// decode reads its tile's code range from these (with the tile prefix, one L2 round trip) and
+// issues the code loads together with its other prologue loads.  One element per thread of the
+// first kScanTiles threads, read before the pre-pass's barrier.
+__device__ __forceinline__ int64_t tile_code_end(const FsstChunk& c, uint64_t sb) {
+    const uint64_t tt = sb * kScanTiles + threadIdx.x;
+    const uint64_t n_tiles = (c.n + kTile - 1) / kTile;
+    if (threadIdx.x >= kScanTiles || tt >= n_tiles) return 0;
+    const uint64_t e = (tt + 1) * kTile < c.n ? (tt + 1) * kTile : c.n;
+    return intcol_get(c.offs, e);
+}
+
 __device__ __forceinline__ void scan_tile_sums(const int64_t* s_ts, int64_t* ws, uint64_t n_tiles, uint64_t sb,
-                                               int64_t* __restrict__ tile_prefix, int64_t* __restrict__ block_totals) {
-    // sb = scan block within the chunk; tile_prefix / block_totals point at the chunk's slices
+                                               int64_t* __restrict__ tile_prefix, int64_t* __restrict__ block_totals,
+                                               int64_t* __restrict__ tile_code, int64_t code_end) {
+    // sb = scan block within the chunk; tile_prefix / block_totals / tile_code point at the
+    // chunk's slices
     const int tid = threadIdx.x;
     int64_t tot;
     const int64_t ex = block_exclusive_scan<kTile / 64>(tid < kScanTiles ? s_ts[tid] : 0, ws, tot);
     const uint64_t tt = sb * kScanTiles + tid;
-    if (tid < kScanTiles && tt < n_tiles) tile_prefix[tt] = ex;
+    if (tid < kScanTiles && tt < n_tiles) {
+        tile_prefix[tt] = ex;
+        tile_code[tt] = code_end;
+    }
     if (tid == 0) block_totals[sb] = tot;
 }
 
@@ -198,7 +215,8 @@ __device__ __forceinline__ const FsstChunk& fsst_chunk_of(const FsstTable& tab, 
 // Any length column: wave w sums tile 4r + w in round r (4 consecutive lengths per lane).
 template <class LenAcc, bool EXT>
 __global__ __launch_bounds__(kTile) void fsst_tile_scan(FsstTable tab, int64_t* __restrict__ tile_prefix_all,
-                                                        int64_t* __restrict__ block_totals_all) {
+                                                        int64_t* __restrict__ block_totals_all,
+                                                        int64_t* __restrict__ tile_code_all) {
     __shared__ int64_t s_ts[kScanTiles];
     __shared__ int64_t ws[kTile / 64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -207,6 +225,7 @@ __global__ __launch_bounds__(kTile) void fsst_tile_scan(FsstTable tab, int64_t* 
     const uint64_t n = c.n, n_tiles = (n + kTile - 1) / kTile, sb = blockIdx.x - c.first_scan;
     int64_t* const tile_prefix = tile_prefix_all + c.first_tile;
     int64_t* const block_totals = block_totals_all + c.first_scan;
+    const int64_t code_end = tile_code_end(c, sb);
     const uint64_t t0 = sb * kScanTiles;
     for (int r0 = 0; r0 < kScanTiles / 4; r0 += 8) {
         int64_t v[8];
@@ -229,7 +248,7 @@ __global__ __launch_bounds__(kTile) void fsst_tile_scan(FsstTable tab, int64_t* 
         }
     }
     __syncthreads();
-    scan_tile_sums(s_ts, ws, n_tiles, sb, tile_prefix, block_totals);
+    scan_tile_sums(s_ts, ws, n_tiles, sb, tile_prefix, block_totals, tile_code_all + c.first_tile, code_end);
 }
 
 // Patch-free FoR(BitPacked u32/i32) lengths with offset 0 (the reference cascade): decode
@@ -256,7 +275,8 @@ __device__ __forceinline__ void fl32_tile_rows(const Vec16<32>* p, int t, uint64
 
 template <int W, bool EXT>
 __global__ __launch_bounds__(kTile) void fsst_tile_scan_fl32(FsstTable tab, int64_t* __restrict__ tile_prefix_all,
-                                                             int64_t* __restrict__ block_totals_all) {
+                                                             int64_t* __restrict__ block_totals_all,
+                                                             int64_t* __restrict__ tile_code_all) {
     __shared__ int64_t s_ts[kScanTiles];
     __shared__ int64_t ws[kTile / 64];
     const int tid = threadIdx.x, t = tid & 7;
@@ -268,6 +288,7 @@ __global__ __launch_bounds__(kTile) void fsst_tile_scan_fl32(FsstTable tab, int6
     int64_t* const tile_prefix = tile_prefix_all + c.first_tile;
     int64_t* const block_totals = block_totals_all + c.first_scan;
     const uint64_t blk = sb * (kScanTiles / 4) + (tid >> 3);
+    const int64_t code_end = tile_code_end(c, sb);
     int64_t acc[4] = {0, 0, 0, 0};
     if (blk * 1024 < n) {
         Vec16<32> p[W > 0 ? W : 1];
@@ -287,13 +308,14 @@ __global__ __launch_bounds__(kTile) void fsst_tile_scan_fl32(FsstTable tab, int6
         for (int k = 0; k < 4; k++) s_ts[(tid >> 3) * 4 + k] = acc[k];
     }
     __syncthreads();
-    scan_tile_sums(s_ts, ws, n_tiles, sb, tile_prefix, block_totals);
+    scan_tile_sums(s_ts, ws, n_tiles, sb, tile_prefix, block_totals, tile_code_all + c.first_tile, code_end);
 }
 
 template <class OffAcc, class LenAcc, bool EXT>
 __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t total_tiles,
                                                      const int64_t* __restrict__ tile_prefix_all,
                                                      const int64_t* __restrict__ block_totals_all,
+                                                     const int64_t* __restrict__ tile_code_all,
                                                      uint32_t* __restrict__ err) {
     __shared__ uint64_t s_sym[256];
     __shared__ uint8_t s_len[256];
@@ -301,7 +323,6 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
     __shared__ unsigned ws_bad[kTile / 64];
     __shared__ int64_t ws64[kTile / 64];
     __shared__ int64_t s_block_prefix;
-    __shared__ int64_t s_coff[3];  // code_offs[0], code_offs[first], code_offs[last]
     __shared__ __attribute__((aligned(16))) uint8_t s_codes[kCodeLds + 48];
     // + slack: view reads past a string, and ORs of the (<= 3) code bytes past the tile
     __shared__ __attribute__((aligned(16))) uint32_t s_heap32[(kHeapLds + 96) / 4];
@@ -319,6 +340,7 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
     const uint8_t* __restrict__ validity = ch.validity;
     const int64_t* __restrict__ tile_prefix = tile_prefix_all + ch.first_tile;
     const int64_t* __restrict__ block_totals = block_totals_all + ch.first_scan;
+    const int64_t* __restrict__ tile_code = tile_code_all + ch.first_tile;
     uint8_t* __restrict__ heap = ch.heap;
     uint4* __restrict__ views = reinterpret_cast<uint4*>(ch.views);
     const uint32_t bidx = ch.bidx;
@@ -341,11 +363,28 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
     const uint64_t i = first + tid;
     const bool live = i < n;
     const uint64_t ii = live ? i : n - 1;
-    const uint64_t last = first + kTile < n ? first + kTile : n;
     const int64_t len_v = lens(ii);
-    if (tid < 3) s_coff[tid] = code_offs(tid == 0 ? 0 : (tid == 1 ? first : last));  // read after a barrier
     const uint8_t vbyte = validity ? validity[ii >> 3] : uint8_t(0xFF);
     const int64_t tp = tile_prefix[tile];
+    // the tile's code range [cf, cl) (absolute offsets into `codes`) from the pre-pass records
+    // (uniform loads, L2-resident), so the code bytes below are requested in this same round
+    // trip instead of after the length scan
+    const int64_t cl = tile_code[tile];
+    const int64_t cf = tile > 0 ? tile_code[tile - 1] : code_offs(0);
+    const uintptr_t ga = reinterpret_cast<uintptr_t>(codes) + uintptr_t(cf);
+    const int cshift = int(ga & 15);
+    const int64_t span64 = cl - cf;
+    const bool span_ok = span64 >= 0 && span64 <= kCodeLds;
+    const int span = span_ok ? int(span64) : 0;  // tile codes at s_codes[0, span) once staged
+    const uint4* const a0 = reinterpret_cast<const uint4*>(ga - uintptr_t(cshift));
+    const int nchunk = (span + 15) >> 4;
+    // chunk `tid` of the staged image: two aligned 16-byte loads (an aligned chunk that holds a
+    // tile byte never crosses a page, so it is read whole), funnel-shifted when written
+    uint4 cx = make_uint4(0, 0, 0, 0), cy = make_uint4(0, 0, 0, 0);
+    if (tid < nchunk) {
+        cx = a0[tid];
+        if (cshift != 0 && 16 * (tid + 1) - cshift < span) cy = a0[tid + 1];
+    }
     if (wave == 0) {  // prefix of the preceding scan blocks (<= a few hundred totals), one wave
         // four loads per lane in flight per round (clamped index, no per-element branch), so a
         // tile deep in a large chunk pays one memory round trip here, not one per 64 blocks
@@ -378,27 +417,19 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
     if (any_bad) my_rel = block_exclusive_scan<kTile / 64>(my_len, ws64, tile_total);  // uniform branch
     const int64_t tile_out0 = tp + s_block_prefix;
 
-    const int64_t c_base = s_coff[0], cf = s_coff[1], cl = s_coff[2];
-    // code offsets are relative to code_offs[0] (sliced_bytes(), varbin/mod.rs:130-136)
-    const int64_t c0 = cf - c_base, c1 = cl - c_base;
     const bool valid = live && ((vbyte >> (ii & 7)) & 1);
     const uint32_t vlen = valid ? uint32_t(my_len) : 0u;
-    const bool stage = !any_bad && (c1 - c0) <= kCodeLds && c1 >= c0 && tile_total <= kHeapLds;
+    const bool stage = !any_bad && span_ok && tile_total <= kHeapLds;
 
     if (stage) {
         // (b) stage the tile's code bytes into LDS shifted so that the tile's first code is
-        // s_codes[0] (two aligned 16-byte loads + a byte funnel per chunk; an aligned chunk that
-        // holds a tile byte never crosses a page, so it is read whole), and zero the image
-        const int64_t cabs0 = c_base + c0;
-        const uintptr_t ga = reinterpret_cast<uintptr_t>(codes) + uintptr_t(cabs0);
-        const int cshift = int(ga & 15);
+        // s_codes[0] (chunk tid was loaded in the prologue; larger tiles load the rest here),
+        // and zero the image
         const int hshift = int((reinterpret_cast<uintptr_t>(heap) + tile_out0) & 15);  // image byte hshift = heap[tile_out0]
-        const int span = int(c1 - c0);  // tile codes at s_codes[0, span)
         const int ttot = int(tile_total);
         {
-            const uint4* a0 = reinterpret_cast<const uint4*>(ga - uintptr_t(cshift));
-            const int nchunk = (span + 15) >> 4;
-            for (int q = tid; q < nchunk; q += kTile) {
+            if (tid < nchunk) *reinterpret_cast<uint4*>(s_codes + 16 * tid) = funnel16(cx, cy, cshift);
+            for (int q = tid + kTile; q < nchunk; q += kTile) {
                 const uint4 x = a0[q];
                 uint4 y = make_uint4(0, 0, 0, 0);
                 if (cshift != 0 && 16 * (q + 1) - cshift < span) y = a0[q + 1];
@@ -571,9 +602,9 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
     } else {
         // direct path: per-string decode straight into HBM (codes of string i are
         // [offs[i], offs[i+1]); each must decode to exactly lengths[i] bytes)
-        const int64_t my_c0 = live ? code_offs(ii) - c_base : 0;
-        const int64_t my_c1 = live ? code_offs(ii + 1) - c_base : 0;
-        const uint8_t* gcodes = codes + c_base;
+        const int64_t my_c0 = live ? code_offs(ii) : 0;
+        const int64_t my_c1 = live ? code_offs(ii + 1) : 0;
+        const uint8_t* gcodes = codes;
         int64_t o = tile_out0 + my_rel;
         const int64_t o_start = o, o_end = o + my_len;
         for (int64_t k = my_c0; k < my_c1; k++) {
@@ -601,8 +632,9 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
 }
 
 uint64_t fsst_scratch_bytes(uint64_t n) {
+    // tile prefixes + scan-block totals + tile code ends
     const uint64_t n_tiles = (n + kTile - 1) / kTile;
-    return (n_tiles + (n_tiles + kScanTiles - 1) / kScanTiles + 2) * sizeof(int64_t);
+    return (2 * n_tiles + (n_tiles + kScanTiles - 1) / kScanTiles + 2) * sizeof(int64_t);
 }
 
 uint64_t fsst_batch_scratch_bytes(const FsstChunk* chunks, size_t n_chunks) {
@@ -623,11 +655,11 @@ std::tuple<int, int, int> fsst_key(const FsstChunk& c) {
 
 template <int... Ws>
 void launch_tile_scan_fl32(int W, dim3 grid, hipStream_t s, const FsstTable& t, int64_t* tiles, int64_t* blocks,
-                           std::integer_sequence<int, Ws...>) {
-    using Fn = void (*)(FsstTable, int64_t*, int64_t*);
+                           int64_t* codes, std::integer_sequence<int, Ws...>) {
+    using Fn = void (*)(FsstTable, int64_t*, int64_t*, int64_t*);
     static constexpr Fn table[] = {&fsst_tile_scan_fl32<Ws, false>...};
     static constexpr Fn table_ext[] = {&fsst_tile_scan_fl32<Ws, true>...};
-    hipLaunchKernelGGL((t.ext ? table_ext : table)[W], grid, dim3(kTile), 0, s, t, tiles, blocks);
+    hipLaunchKernelGGL((t.ext ? table_ext : table)[W], grid, dim3(kTile), 0, s, t, tiles, blocks, codes);
 }
 
 // accessor = plain width 1/2/4/8 or packed T = 32/64
@@ -688,10 +720,11 @@ vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint
         if (tab.n) {
             int64_t* tp = tiles_all;
             int64_t* bt = tiles_all + tiles;
-            tiles_all += tiles + scans;
+            int64_t* tc = bt + scans;
+            tiles_all += 2 * tiles + scans;
             const auto key = fsst_key(cs[0]);
             if (std::get<2>(key) >= 0)
-                launch_tile_scan_fl32(std::get<2>(key), dim3(unsigned(scans)), s, tab, tp, bt,
+                launch_tile_scan_fl32(std::get<2>(key), dim3(unsigned(scans)), s, tab, tp, bt, tc,
                                       std::make_integer_sequence<int, 33>{});
             bool ok = true;
             with_acc(std::get<0>(key), [&](auto* oa) {
@@ -702,9 +735,9 @@ vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint
                         constexpr bool X = decltype(ext)::value;
                         if (std::get<2>(key) < 0)
                             hipLaunchKernelGGL((fsst_tile_scan<LA, X>), dim3(unsigned(scans)), dim3(kTile), 0, s, tab,
-                                               tp, bt);
+                                               tp, bt, tc);
                         hipLaunchKernelGGL((fsst_decode<OA, LA, X>), dim3(unsigned(tiles)), dim3(kTile), 0, s, tab,
-                                           tiles, tp, bt, err);
+                                           tiles, tp, bt, tc, err);
                     };
                     if (tab.ext) go(std::true_type{});
                     else go(std::false_type{});
