@@ -327,31 +327,41 @@ def chk(st):
 
 
 def run_workload(wl, steps: int, warmup: int, dist):
-    """Warmup, then exactly `steps` back-to-back steps between barrier + synchronize.  HIP events
-    on the decode stream (torch's current stream, the stream the engine is given) bracket every
-    step: (last - first) / steps is the mean device time per step (per launch for a one-kernel
-    step like C1), and the per-step differences give the median."""
+    """Warmup, then exactly `steps` back-to-back steps between barrier + synchronize.  Two HIP
+    events on the decode stream (torch's current stream, the stream the engine is given) bracket
+    the timed steps: (end - start) / steps is the mean device time per step (per launch for a
+    one-kernel step like C1).  No event sits between the timed steps: a timing event between two
+    kernels waits for the first one's memory release and stretches each interval by ~2-3 us on a
+    60 us kernel (rocprofv3's average of the same launches agrees with the two-event mean, not
+    with per-step events).  A second, untimed pass with an event after every step gives the
+    per-step median."""
     import torch
     for _ in range(warmup):
         wl.step()
     wl.ctx.sync()
-    evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    evs[0].record()
+    e0.record()
     for s in range(steps):
         wl.step()
-        evs[s + 1].record()
+    e1.record()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     wl.ctx.sync()  # surfaces device-side errors (OOB codes, ...)
-    per = [evs[i].elapsed_time(evs[i + 1]) for i in range(steps)]
-    kmean = evs[0].elapsed_time(evs[-1]) / steps
-    kmed = float(np.median(per))
+    kmean = e0.elapsed_time(e1) / steps
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+    evs[0].record()
+    for s in range(steps):
+        wl.step()
+        evs[s + 1].record()
+    torch.cuda.synchronize()
+    wl.ctx.sync()
+    kmed = float(np.median([evs[i].elapsed_time(evs[i + 1]) for i in range(steps)]))
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -655,11 +655,12 @@ __global__ __launch_bounds__(kBlock) void runend_chunks_kernel(RunEndTable tab) 
 
 // Short runs (C5's l_orderkey: 1-7 rows per order): a workgroup takes 1024 consecutive RUNS
 // (not an output span), so no search is needed: thread t reads ends[r] and values[r] of runs
-// r0 + t + 256 k (k < 4) in one round trip -- from plain buffers, or unpacked in place from
+// r0 + 4 t + k (k < 4) in one round trip -- from plain buffers, or unpacked in place from
 // patch-free [FoR](BitPacked) children (fastlanes unpack_single, bitpacking/compress.rs:295-306),
 // so the children are never materialised.  Run r covers the trimmed range
 // [min(ends[r-1] - offset, len), min(ends[r] - offset, len)) (runend_decode_primitive,
-// runend/compress.rs:138-146; the previous end comes through LDS), and the workgroup's runs cover
+// runend/compress.rs:138-146; the previous end is the thread's own, its left lane's, or the
+// previous wave's last, through LDS), and the workgroup's runs cover
 // one contiguous output range.  That range is expanded in windows of 4096 outputs: each
 // non-empty run writes its index at its first output (a run head), a max-scan fills the window,
 // and the window is written with coalesced non-temporal stores (the run carried into the next
@@ -678,9 +679,9 @@ __global__ __launch_bounds__(kBlock) void runend_runs_kernel(RunEndTable tab) {
     constexpr int SPAN = 4096, PER = SPAN / kBlock, RPG = int(kRunEndRunsPerGroup), RPT = RPG / kBlock;
     __shared__ __attribute__((aligned(16))) uint32_t s_head[SPAN];
     __shared__ V s_val[RPG];
-    __shared__ uint64_t s_end[RPG];
+    __shared__ uint64_t s_wlast[kBlock / 64];
     __shared__ uint32_t s_wmax[kBlock / 64];
-    __shared__ uint64_t s_lo;
+    __shared__ uint64_t s_lo, s_hi;
     __shared__ uint32_t s_carry;
     const uint64_t g = blockIdx.x;
     RunEndChunk c;
@@ -698,39 +699,43 @@ __global__ __launch_bounds__(kBlock) void runend_runs_kernel(RunEndTable tab) {
     const uint64_t r0 = (g - c.first_group) * uint64_t(RPG);
     const int nr = int(c.n_runs - r0 < uint64_t(RPG) ? c.n_runs - r0 : uint64_t(RPG));
     auto trim = [&](uint64_t e) { return e > c.offset ? (e - c.offset < c.len ? e - c.offset : c.len) : 0; };
-    // every load of the round trip issued before any is used
+    // thread t owns runs RPT t .. RPT t + RPT - 1; every load of the round trip issued before
+    // any is used
     uint64_t e[RPT];
     V v[RPT];
 #pragma unroll
     for (int k = 0; k < RPT; k++) {
-        const int i = tid + k * kBlock;
+        const int i = RPT * tid + k;
         const uint64_t rr = r0 + uint64_t(i < nr ? i : 0);
         e[k] = uint64_t(intcol_get(c.ends, rr));
         v[k] = runend_value<V>(c.values, rr);
     }
     const uint64_t eprev = tid == 0 && r0 > 0 ? uint64_t(intcol_get(c.ends, r0 - 1)) : 0;
+    uint64_t en[RPT], st[RPT];
 #pragma unroll
     for (int k = 0; k < RPT; k++) {
-        const int i = tid + k * kBlock;
+        const int i = RPT * tid + k;
+        en[k] = trim(e[k]);
         if (i < nr) {
-            const uint64_t t = trim(e[k]);
-            s_end[i] = t;
             s_val[i] = v[k];
-            if (r0 + uint64_t(i) + 1 == c.n_runs && t < c.len)  // the ends do not reach the end of the array
+            if (i == nr - 1) s_hi = en[k];
+            if (r0 + uint64_t(i) + 1 == c.n_runs && en[k] < c.len)  // the ends do not reach the end of the array
                 __hip_atomic_fetch_or(tab.err, kErrRunEnd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
+    // a run starts at the previous run's trimmed end: in this thread, in lane t - 1, or in the
+    // previous wave's last lane
+    const uint64_t left = __shfl_up(en[RPT - 1], 1, 64);
+    if ((tid & 63) == 63) s_wlast[tid >> 6] = en[RPT - 1];
     if (tid == 0) s_lo = r0 > 0 ? trim(eprev) : 0;
     __syncthreads();
-    const uint64_t lo = s_lo, hi = s_end[nr - 1];
-    // run starts (the previous run's trimmed end)
-    uint64_t st[RPT], en[RPT];
+    const uint64_t lo = s_lo, hi = s_hi;
+    st[0] = tid == 0 ? lo : ((tid & 63) == 0 ? s_wlast[(tid >> 6) - 1] : left);
 #pragma unroll
-    for (int k = 0; k < RPT; k++) {
-        const int i = tid + k * kBlock;
-        en[k] = i < nr ? s_end[i] : 0;
-        st[k] = i < nr ? (i > 0 ? s_end[i - 1] : lo) : 0;
-    }
+    for (int k = 1; k < RPT; k++) st[k] = en[k - 1];
+#pragma unroll
+    for (int k = 0; k < RPT; k++)
+        if (RPT * tid + k >= nr) st[k] = en[k] = 0;  // no run here
     V* __restrict__ out = static_cast<V*>(c.out);
     uint32_t carry = 0;
     for (uint64_t wb = lo; wb < hi; wb += SPAN) {
@@ -741,7 +746,7 @@ __global__ __launch_bounds__(kBlock) void runend_runs_kernel(RunEndTable tab) {
 #pragma unroll
         for (int k = 0; k < RPT; k++)
             if (en[k] > st[k] && st[k] >= wb && st[k] < wb + uint64_t(wn))
-                s_head[st[k] - wb] = uint32_t(tid + k * kBlock) + 1;
+                s_head[st[k] - wb] = uint32_t(RPT * tid + k) + 1;
         __syncthreads();
         // inclusive max-scan of s_head (thread t owns entries [PER t, PER t + PER)), seeded
         // with the run carried over from the previous window
