@@ -654,6 +654,68 @@ def test_plan_lineitem_columns(ctx, rows, cr):
     plan.close()
 
 
+def _k1g_columns(rng):
+    """Chunked columns covering every K1g body (k1g.hip): T = 8..64 bits plain / FoR / ZigZag,
+    ALP f32 / f64, Dict with 1/2/4/8-byte values and string dictionaries (16-byte views), with
+    ragged chunk lengths, an empty chunk and sliced BitPacked chunks (offset > 0)."""
+    lens = [1000, 2500, 1024, 0, 3, 7000]
+    cols = []
+
+    def chunked(make):
+        arrs, exp = [], []
+        for n in lens:
+            a, v = make(n)
+            arrs.append(a)
+            exp.append(v)
+        return A.chunked(arrs), np.concatenate(exp)
+
+    for dt in (np.uint8, np.uint16, np.uint32, np.uint64):
+        bits = np.iinfo(dt).bits
+        for W in (1, bits // 2 + 1, bits - 1):
+            def mk(n, dt=dt, W=W):
+                v = rng.integers(0, 1 << W, n, dtype=np.uint64).astype(dt)
+                off = int(rng.integers(1, 1000)) if n > 2000 else 0  # sliced chunk
+                return E.encode_bitpacked(v, bit_width=W, allow_patches=False, offset=off), v
+            cols.append(chunked(mk))
+    for dt in (np.int8, np.int16, np.int32, np.int64):
+        lo = int(np.iinfo(dt).min) // 2
+        cols.append(chunked(lambda n, dt=dt, lo=lo: (lambda v: (E.encode_for_bitpacked(v, allow_patches=False), v))(
+            (lo + 3 * rng.integers(0, 40, n)).astype(dt))))
+        cols.append(chunked(lambda n, dt=dt: (lambda v: (E.encode_zigzag(v), v))(
+            (rng.integers(-60, 60, n)).astype(dt))))
+    for ft in (np.float64, np.float32):
+        cols.append(chunked(lambda n, ft=ft: (lambda v: (E.encode_alp(v), v))(
+            (np.round(rng.uniform(0, 1000, n) * 100) / 100).astype(ft))))
+    for vdt in (np.uint8, np.int16, np.uint32, np.int64):
+        pool = np.unique(rng.integers(0, 100, 64).astype(vdt))
+        cols.append(chunked(lambda n, pool=pool: (lambda v: (E.encode_dict(v), v))(pool[rng.integers(0, pool.size, n)])))
+    return cols
+
+
+def test_plan_k1g_every_kind(ctx):
+    """A plan of small chunked columns: their K1 decodes are batched across columns onto one graph
+    branch and run as ONE K1g launch (runtime T / W / epilogue per chunk table entry); every
+    column equals the oracle, string dictionaries included."""
+    import torch
+    rng = np.random.default_rng(77)
+    cols = _k1g_columns(rng)
+    words = [b"DELIVER IN PERSON", b"NONE", b"TAKE BACK RETURN", b"COLLECT COD"]
+    strs = [[words[i] for i in rng.integers(0, 4, n)] for n in (3000, 1, 5000)]
+    sarr = A.chunked([E.encode_dict_strings(s) for s in strs])
+    arrs = [c for c, _ in cols] + [sarr]
+    plan = V.Plan([a.to(torch.device("cuda", 0)) for a in arrs], ctx)
+    for _ in range(2):
+        res = plan.launch(sync=True)
+        for k, ((a, exp), r) in enumerate(zip(cols, res)):
+            got = r.numpy()
+            ref, _ = canon(a)
+            assert got.tobytes() == ref.tobytes() == exp.tobytes(), (k, a.children[1].encoding)
+        (rviews, rbufs), _ = canon(sarr)
+        assert res[-1].numpy()[0].tobytes() == rviews.tobytes()
+        assert [b.tobytes() for b in res[-1].buffers()] == [b.tobytes() for b in rbufs]
+    plan.close()
+
+
 # ------------------------------------------------------------------ edge cases: empty inputs
 def test_empty_arrays_every_encoding(ctx):
     """len = 0 through every encoding and container (the reference canonicalizes empty arrays

@@ -19,6 +19,7 @@
 
 #include "encode_gpu.hpp"
 #include "filter.hpp"
+#include "k1g.hpp"
 #include "take.hpp"
 #include "vxg_internal.hpp"
 
@@ -133,19 +134,48 @@ bool same_kernel(const K1Job& a, const K1Job& b) {
     return a.T == b.T && a.W == b.W && a.epi == b.epi && a.vw == b.vw;
 }
 
+// Output bytes below which a plan batch's kernel group goes to the one K1g launch instead of its
+// own K1 launch (VXG_K1G_MAX_BYTES overrides; 0 disables K1g).  Measured on the simulated 8-GPU
+// C5 shard: 0.120 ms/step with per-kernel launches, 0.094 with K1g below 16 MiB, 0.085 below
+// 64 MiB (tools/gpu_ab_c5.sh).
+static uint64_t k1g_max_bytes() {
+    static const uint64_t v = [] {
+        const char* e = std::getenv("VXG_K1G_MAX_BYTES");
+        return e ? uint64_t(std::strtoull(e, nullptr, 10)) : uint64_t(64) << 20;
+    }();
+    return v;
+}
+
+static int k1_out_width(const K1Job& j) {
+    return j.epi == Epi::Dict ? j.vw : (j.epi == Epi::AlpF32 ? 4 : (j.epi == Epi::AlpF64 ? 8 : j.T / 8));
+}
+
 // Launch K1 jobs grouped by kernel (T, W, epilogue, value width), kArgChunks chunks per launch
 // with the chunk table as the kernel argument (no device table, no upload, no host sync).
-// While a plan is recorded (dt set), a group of any size is one launch over a device table.
-vxg_status launch_k1_jobs(std::vector<K1Job>& jobs, uint32_t* err, hipStream_t s, DevTables* dt = nullptr) {
+// While a plan is recorded (dt set), a group of any size is one launch over a device table, and
+// (generic_small: a plan's batch) the groups whose output is small all share ONE K1g launch
+// (k1g.hpp): a sharded scan's many small per-column kernels cost more in ramp, drain and graph
+// edges than in data.
+vxg_status launch_k1_jobs(std::vector<K1Job>& jobs, uint32_t* err, hipStream_t s, DevTables* dt = nullptr,
+                          bool generic_small = false) {
     std::stable_sort(jobs.begin(), jobs.end(), [](const K1Job& a, const K1Job& b) {
         return std::make_tuple(a.T, a.W, int(a.epi), a.vw) < std::make_tuple(b.T, b.W, int(b.epi), b.vw);
     });
+    std::vector<const K1Job*> gen;  // jobs for the shared K1g launch
     size_t i = 0;
     while (i < jobs.size()) {
         size_t j = i, live = 0;
+        uint64_t out_bytes = 0;
         while (j < jobs.size() && (dt || j - i < size_t(kArgChunks)) && same_kernel(jobs[i], jobs[j])) {
             live += jobs[j].d.n_blocks != 0;
+            out_bytes += jobs[j].d.len * uint64_t(k1_out_width(jobs[j]));
             j++;
+        }
+        if (dt && generic_small && out_bytes < k1g_max_bytes() && gen_kind(jobs[i].T, int(jobs[i].epi), jobs[i].vw) >= 0) {
+            for (size_t k = i; k < j; k++)
+                if (jobs[k].d.n_blocks) gen.push_back(&jobs[k]);
+            i = j;
+            continue;
         }
         ChunkTable tab{};
         tab.err = err;
@@ -169,6 +199,28 @@ vxg_status launch_k1_jobs(std::vector<K1Job>& jobs, uint32_t* err, hipStream_t s
             if (st != VXG_OK) return st;
         }
         i = j;
+    }
+    if (!gen.empty()) {
+        if (gen.size() > 0xFFFFFFFFull) return set_error(VXG_ERR_INVALID_ARGUMENT, "too many chunks");
+        GenChunk* host;
+        const GenChunk* ext;
+        VXG_TRY_S(dt->table(gen.size(), &host, &ext));
+        uint64_t groups = 0;
+        bool dict_lds = true;
+        for (size_t k = 0; k < gen.size(); k++) {
+            const K1Job& jb = *gen[k];
+            GenChunk& g = host[k];
+            g.d = jb.d;
+            g.kind = uint32_t(gen_kind(jb.T, int(jb.epi), jb.vw));
+            g.W = uint32_t(jb.W);
+            g.bpw = gen_bpw(jb.T, jb.W);
+            g.d.first_group = groups;
+            groups += (jb.d.n_blocks + g.bpw - 1) / g.bpw;
+            if (jb.epi == Epi::Dict)
+                dict_lds = dict_lds && jb.d.dict_len * uint64_t(jb.vw) <= uint64_t(kDictLdsBytes) &&
+                           (reinterpret_cast<uintptr_t>(jb.d.dict) & 15) == 0;
+        }
+        VXG_TRY_S(launch_k1_generic(ext, uint32_t(gen.size()), groups, dict_lds, err, s));
     }
     return VXG_OK;
 }
@@ -228,12 +280,95 @@ vxg_status bitunpack_common(vxg_ctx* ctx, int T, unsigned W, unsigned offset, ui
     return launch_k1_jobs(jobs, ctx->c.err_word, S(stream));
 }
 
+// RunEnd expansions of one value width: short runs thread-per-run (K8r), long runs workgroup
+// per kRunEndSpan outputs (K8), kRunEndArgChunks chunks per launch (a plan: one launch per kind
+// over a device table).
+vxg_status launch_runs(std::vector<RunEndChunk> runs, int w, uint32_t* err, hipStream_t s, DevTables* dt) {
+    runs.erase(std::remove_if(runs.begin(), runs.end(), [](const RunEndChunk& r) { return r.len == 0; }), runs.end());
+    std::vector<RunEndChunk> short_runs, long_runs;
+    for (const RunEndChunk& r : runs) (r.len <= kRunEndShortRun * r.n_runs ? short_runs : long_runs).push_back(r);
+    for (int pass = 0; pass < 2; pass++) {
+        std::vector<RunEndChunk>& rs = pass == 0 ? short_runs : long_runs;
+        const size_t per = dt && rs.size() > size_t(kRunEndArgChunks) ? rs.size() : size_t(kRunEndArgChunks);
+        for (size_t i = 0; i < rs.size(); i += per) {
+            RunEndTable tab{};
+            tab.err = err;
+            RunEndChunk* cs = tab.c;
+            RunEndChunk* host = nullptr;
+            if (per > size_t(kRunEndArgChunks)) {
+                VXG_TRY_S(dt->table(rs.size(), &host, &tab.ext));
+                cs = host;
+            }
+            uint64_t groups = 0;
+            for (size_t k = i; k < rs.size() && k - i < per; k++) {
+                RunEndChunk& r = cs[tab.n++];
+                r = rs[k];
+                r.first_group = groups;
+                groups += pass == 0 ? (r.n_runs + kRunEndRunsPerGroup - 1) / kRunEndRunsPerGroup
+                                    : (r.len + kRunEndSpan - 1) / kRunEndSpan;
+            }
+            VXG_TRY_S(pass == 0 ? launch_runend_runs(w, tab, groups, s) : launch_runend_chunks(w, tab, groups, s));
+        }
+    }
+    return VXG_OK;
+}
+
+// A recorded plan's deferred launches, shared by the planners of all its arrays: the K1 decodes,
+// RunEnd expansions and string-dictionary views of every chunked column, launched together at
+// the end of recording on one graph branch (dictionary views, then one launch per large K1 kernel
+// group + one K1g launch for all the small ones, then the expansions), instead of per column.
+struct PlanBatch {
+    std::vector<VarBinChunk> dicts;
+    std::vector<K1Job> jobs;
+    std::vector<std::pair<int, RunEndChunk>> runs;  // (value width, chunk)
+    bool empty() const { return dicts.empty() && jobs.empty() && runs.empty(); }
+};
+
+vxg_status launch_varbin_dicts(const std::vector<VarBinChunk>& dicts, hipStream_t s, DevTables* dt) {
+    const size_t per = dt && dicts.size() > size_t(kVarBinArgChunks) ? dicts.size() : size_t(kVarBinArgChunks);
+    for (size_t i = 0; i < dicts.size(); i += per) {
+        VarBinTable tab{};
+        VarBinChunk* cs = tab.c;
+        if (per > size_t(kVarBinArgChunks)) {
+            VarBinChunk* host;
+            VXG_TRY_S(dt->table(dicts.size(), &host, &tab.ext));
+            cs = host;
+        }
+        uint64_t groups = 0;
+        for (size_t j = i; j < dicts.size() && j - i < per; j++) {
+            VarBinChunk& d = cs[tab.n++];
+            d = dicts[j];
+            d.first_group = groups;
+            groups += d.n ? (d.n + 255) / 256 : 1;
+        }
+        VXG_TRY_S(launch_varbin_chunks(tab, groups, s));
+    }
+    return VXG_OK;
+}
+
+vxg_status flush_plan_batch(PlanBatch& b, uint32_t* err, hipStream_t s, DevTables* dt) {
+    VXG_TRY_S(launch_varbin_dicts(b.dicts, s, dt));
+    VXG_TRY_S(launch_k1_jobs(b.jobs, err, s, dt, true));
+    std::vector<int> widths;
+    for (const auto& r : b.runs) widths.push_back(r.first);
+    std::sort(widths.begin(), widths.end());
+    widths.erase(std::unique(widths.begin(), widths.end()), widths.end());
+    for (int w : widths) {
+        std::vector<RunEndChunk> rs;
+        for (const auto& r : b.runs)
+            if (r.first == w) rs.push_back(r.second);
+        VXG_TRY_S(launch_runs(rs, w, err, s, dt));
+    }
+    return VXG_OK;
+}
+
 // ===================================================================================
 // Planner
 // ===================================================================================
 class Planner {
   public:
-    Planner(vxg_ctx* ctx, hipStream_t s, DevTables* plan = nullptr) : ctx_(ctx), s_(s), plan_(plan) {}
+    Planner(vxg_ctx* ctx, hipStream_t s, DevTables* plan = nullptr, PlanBatch* batch = nullptr)
+        : ctx_(ctx), s_(s), plan_(plan), batch_(batch) {}
     ~Planner() {
         for (void* p : temps_) (void)hipFreeAsync(p, s_);
     }
@@ -256,6 +391,7 @@ class Planner {
     // replays) instead of stream-ordered ones, and chunk tables longer than a kernel argument
     // holds become device tables (one launch per kernel group).
     DevTables* plan_ = nullptr;
+    PlanBatch* batch_ = nullptr;  // a plan's deferred launches (all its arrays), or null
     // Deferred K1 decodes of the chunks of a ChunkedArray (grouped into shared launches) and
     // the patch scatters that must follow them; null = launch immediately.
     struct PatchJob {
@@ -636,36 +772,14 @@ vxg_status Planner::decode_chunked_primitive(const vxg_array& a, void* dst) {
         off += c.len;
     }
     if (off != a.len) return set_error(VXG_ERR_INVALID_ARGUMENT, "Chunked len != sum of chunk lens");
+    if (batch_ && patches.empty()) {  // a plan: launched with the other arrays' jobs (PlanBatch)
+        batch_->jobs.insert(batch_->jobs.end(), jobs.begin(), jobs.end());
+        for (const RunEndChunk& r : runs) batch_->runs.emplace_back(w, r);
+        return VXG_OK;
+    }
     VXG_TRY(launch_k1_jobs(jobs, ctx_->c.err_word, s_, plan_));
     for (const PatchJob& p : patches) VXG_TRY(apply_sparse_patches(*p.sp, p.T, p.epi, p.vw, p.a, p.dst, p.out_len));
-    runs.erase(std::remove_if(runs.begin(), runs.end(), [](const RunEndChunk& r) { return r.len == 0; }), runs.end());
-    // short runs: thread per run; long runs: workgroup per kRunEndSpan outputs
-    std::vector<RunEndChunk> short_runs, long_runs;
-    for (const RunEndChunk& r : runs) (r.len <= kRunEndShortRun * r.n_runs ? short_runs : long_runs).push_back(r);
-    for (int pass = 0; pass < 2; pass++) {
-        std::vector<RunEndChunk>& rs = pass == 0 ? short_runs : long_runs;
-        const size_t per = plan_ && rs.size() > size_t(kRunEndArgChunks) ? rs.size() : size_t(kRunEndArgChunks);
-        for (size_t i = 0; i < rs.size(); i += per) {
-            RunEndTable tab{};
-            tab.err = ctx_->c.err_word;
-            RunEndChunk* cs = tab.c;
-            RunEndChunk* host = nullptr;
-            if (per > size_t(kRunEndArgChunks)) {
-                VXG_TRY(plan_->table(rs.size(), &host, &tab.ext));
-                cs = host;
-            }
-            uint64_t groups = 0;
-            for (size_t k = i; k < rs.size() && k - i < per; k++) {
-                RunEndChunk& r = cs[tab.n++];
-                r = rs[k];
-                r.first_group = groups;
-                groups += pass == 0 ? (r.n_runs + kRunEndRunsPerGroup - 1) / kRunEndRunsPerGroup
-                                    : (r.len + kRunEndSpan - 1) / kRunEndSpan;
-            }
-            VXG_TRY(pass == 0 ? launch_runend_runs(w, tab, groups, s_) : launch_runend_chunks(w, tab, groups, s_));
-        }
-    }
-    return VXG_OK;
+    return launch_runs(runs, w, ctx_->c.err_word, s_, plan_);
 }
 
 vxg_status Planner::decode_alprd(const vxg_array& a, void* dst) {
@@ -1380,6 +1494,7 @@ vxg_status Planner::strings_into(const vxg_array& a, uint8_t* views, uint8_t* da
         f.n = a.len;
         f.validity = validity;
         f.heap = data + bufs[0].offset;
+        f.heap_len = bufs[0].len;
         f.views = views;
         f.bidx = bidx;
         if (fsst_batch_) {  // a chunk: decoded with the other FSST chunks
@@ -1505,24 +1620,12 @@ vxg_status Planner::strings_into(const vxg_array& a, uint8_t* views, uint8_t* da
             VXG_TRY(temp(fsst_batch_scratch_bytes(fssts.data(), fssts.size()), &scratch));
             VXG_TRY(launch_fsst_batch(fssts, scratch, ctx_->c.err_word, s_, plan_));
         }
-        const size_t per = plan_ && dicts.size() > size_t(kVarBinArgChunks) ? dicts.size() : size_t(kVarBinArgChunks);
-        for (size_t i = 0; i < dicts.size(); i += per) {
-            VarBinTable tab{};
-            VarBinChunk* cs = tab.c;
-            if (per > size_t(kVarBinArgChunks)) {
-                VarBinChunk* host;
-                VXG_TRY(plan_->table(dicts.size(), &host, &tab.ext));
-                cs = host;
-            }
-            uint64_t groups = 0;
-            for (size_t j = i; j < dicts.size() && j - i < per; j++) {
-                VarBinChunk& d = cs[tab.n++];
-                d = dicts[j];
-                d.first_group = groups;
-                groups += d.n ? (d.n + 255) / 256 : 1;
-            }
-            VXG_TRY(launch_varbin_chunks(tab, groups, s_));
+        if (batch_ && patches.empty()) {  // a plan: launched with the other arrays' jobs (PlanBatch)
+            batch_->dicts.insert(batch_->dicts.end(), dicts.begin(), dicts.end());
+            batch_->jobs.insert(batch_->jobs.end(), jobs.begin(), jobs.end());
+            return VXG_OK;
         }
+        VXG_TRY(launch_varbin_dicts(dicts, s_, plan_));
         VXG_TRY(launch_k1_jobs(jobs, ctx_->c.err_word, s_, plan_));
         for (const PatchJob& p : patches) VXG_TRY(apply_sparse_patches(*p.sp, p.T, p.epi, p.vw, p.a, p.dst, p.out_len));
         return VXG_OK;
@@ -1778,6 +1881,23 @@ static uint32_t plan_branches() {
     return nb;
 }
 
+// Deferred launches of a plan's SMALL arrays (canonical output <= VXG_PLAN_BATCH_MAX_BYTES,
+// default 16 MiB; 0 disables) batched onto one branch.  A sharded scan's columns are all small
+// (C5 at 8 GPUs: 3-12 MB each, 0.120 -> 0.085-0.094 ms/step); a whole-table scan's columns keep
+// their own balanced branches (C5 at 1 GPU: batching them all onto one branch cost 6 %).
+static uint64_t plan_batch_max_bytes() {
+    static const uint64_t v = [] {
+        const char* e = std::getenv("VXG_PLAN_BATCH_MAX_BYTES");
+        return e ? uint64_t(std::strtoull(e, nullptr, 10)) : uint64_t(16) << 20;
+    }();
+    return v;
+}
+
+static uint64_t canonical_out_bytes(const vxg_array& a) {
+    const bool str = a.dtype == VXG_DTYPE_UTF8 || a.dtype == VXG_DTYPE_BINARY;
+    return a.dtype == VXG_DTYPE_BOOL ? a.len / 8 : a.len * (str ? 16 : ptype_width(a.ptype));
+}
+
 struct vxg_plan {
     vxg_ctx* ctx = nullptr;
     hipGraph_t graph = nullptr;
@@ -1805,8 +1925,15 @@ vxg_status vxg_plan_create(vxg_ctx* ctx, const vxg_array* arrays, vxg_canonical*
     // independent, so their launches become parallel graph branches (the graph runs them on
     // several hardware queues, overlapping the ramp and drain of the many small kernels of a
     // chunked scan), joined back into the origin stream.
+    // The small arrays' deferrable launches (PlanBatch: K1 decodes, RunEnd expansions,
+    // dictionary views of chunked columns) go to one more branch, recorded after all arrays were
+    // visited.
     const uint32_t kPlanBranches = plan_branches();
-    const uint32_t nb = n < kPlanBranches ? (n ? n : 1) : kPlanBranches;
+    bool batching = false;
+    for (uint32_t i = 0; i < n; i++) batching = batching || canonical_out_bytes(arrays[i]) <= plan_batch_max_bytes();
+    const uint32_t nb = (n < kPlanBranches ? (n ? n : 1) : kPlanBranches) + (batching ? 1 : 0);
+    const uint32_t na = batching ? nb - 1 : nb;  // branches the arrays are spread over
+    PlanBatch batch;
     hipStream_t cs;
     VXG_TRY(hip_check(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking), "plan stream"));
     std::vector<hipStream_t> br(nb, nullptr);
@@ -1827,7 +1954,7 @@ vxg_status vxg_plan_create(vxg_ctx* ctx, const vxg_array* arrays, vxg_canonical*
         // moves, each onto the branch with the least work so far, so one heavy column (C5's
         // l_comment) does not queue behind others on its branch
         std::vector<uint32_t> order(n);
-        std::vector<uint64_t> cost(n), load(nb, 0);
+        std::vector<uint64_t> cost(n), load(na, 0);
         for (uint32_t i = 0; i < n; i++) {
             order[i] = i;
             cost[i] = plan_cost(arrays[i]);
@@ -1837,9 +1964,11 @@ vxg_status vxg_plan_create(vxg_ctx* ctx, const vxg_array* arrays, vxg_canonical*
             const uint32_t i = order[k];
             const uint32_t b = uint32_t(std::min_element(load.begin(), load.end()) - load.begin());
             load[b] += cost[i];
-            Planner p(ctx, br[b], &pl->store);
+            const bool small = batching && canonical_out_bytes(arrays[i]) <= plan_batch_max_bytes();
+            Planner p(ctx, br[b], &pl->store, small ? &batch : nullptr);
             st = p.canonical(arrays[i], outs[i]);
         }
+        if (batching && st == VXG_OK) st = flush_plan_batch(batch, ctx->c.err_word, br[nb - 1], &pl->store);
         for (uint32_t b = 0; b < nb && st == VXG_OK; b++) {
             st = hip_check(hipEventRecord(ev[b], br[b]), "join");
             if (st == VXG_OK) st = hip_check(hipStreamWaitEvent(cs, ev[b], 0), "join wait");

@@ -1,0 +1,154 @@
+// k1g.hip — K1g: the K1 decodes of a recorded plan with DIFFERENT kernels in one launch
+// (k1g.hpp).  Same decode and epilogues as K1 (fl_unpack_impl.hpp: FoR for/compress.rs:100-117,
+// ZigZag zigzag/compress.rs:35-57, ALP alp/mod.rs:161-163, Dict dict/array.rs:68-73), but the
+// bit width is a runtime value: a 256-thread workgroup stages `bpw` FastLanes blocks' packed words
+// (128 * W bytes each) in LDS and thread t produces values t, t + 256, t + 512, t + 768 of every
+// block (64 consecutive values per store wave-instruction); value i of a block is unpack_single's
+// (lane, row) -> one or two T-bit words of that lane.  The body (T, epilogue, value width) is a
+// workgroup-uniform switch on the job's kind.
+#include "fl_unpack_impl.hpp"
+#include "k1g.hpp"
+
+namespace vxg {
+
+namespace {
+
+constexpr int kGenThreads = 256;
+constexpr uint32_t kGenPackedLds = 16 * 1024;  // staged packed words per workgroup
+
+// FL_ORDER[i] (0, 4, 2, 6, 1, 5, 3, 7) is the 3-bit reversal of i
+__device__ __forceinline__ uint32_t fl_order_rt(uint32_t i) { return ((i & 1u) << 2) | (i & 2u) | (i >> 2); }
+
+template <typename O>
+__device__ __forceinline__ void gen_store(O* p, const O& v) {
+    if constexpr (sizeof(O) >= 4) nt_store(p, v);
+    else *p = v;
+}
+
+template <int T, Epi EPI, int VW>
+__device__ __forceinline__ void gen_body(const GenChunk& gc, uint64_t g, uint8_t* lds, bool dict_lds, uint32_t* err) {
+    using E = typename Fl<T>::E;
+    using O = typename EpiOut<T, EPI, VW>::type;
+    constexpr uint32_t LANES = 1024 / T;
+    const ChunkDev& c = gc.d;
+    const uint32_t W = gc.W, tid = threadIdx.x;
+    const uint64_t blk0 = (g - c.first_group) * gc.bpw;
+    const uint32_t nb = uint32_t(c.n_blocks - blk0 < uint64_t(gc.bpw) ? c.n_blocks - blk0 : uint64_t(gc.bpw));
+    E* const s_packed = reinterpret_cast<E*>(lds);
+    const uint32_t q16 = nb * 8 * W;
+    for (uint32_t q = tid; q < q16; q += kGenThreads)
+        reinterpret_cast<uint4*>(s_packed)[q] = reinterpret_cast<const uint4*>(c.packed + blk0 * (128ull * W))[q];
+    EpiParams ep;
+    ep.reference = c.reference;
+    ep.shift = c.shift;
+    ep.alp_a = c.alp_a;
+    ep.alp_b = c.alp_b;
+    ep.dict = c.dict;
+    ep.dict_len = c.dict_len;
+    ep.err = err;
+    if constexpr (EPI == Epi::Dict) {
+        if (dict_lds) {
+            uint8_t* const s_dict = lds + kGenPackedLds;
+            const uint32_t n16 = uint32_t((c.dict_len * VW + 15) / 16);
+            for (uint32_t q = tid; q < n16; q += kGenThreads)
+                reinterpret_cast<uint4*>(s_dict)[q] = static_cast<const uint4*>(c.dict)[q];
+            ep.dict = s_dict;
+        }
+    }
+    __syncthreads();
+    O* __restrict__ out = static_cast<O*>(c.out);
+    const E mask = W >= uint32_t(T) ? E(~E(0)) : E((E(1) << W) - E(1));
+    bool oob = false;
+    for (uint32_t b = 0; b < nb; b++) {
+        const E* __restrict__ pw = s_packed + b * (LANES * W);
+        const int64_t base = int64_t((blk0 + b) * 1024) - int64_t(c.offset);
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) {
+            const uint32_t i = k * kGenThreads + tid;  // value index inside the block
+            const int64_t o = base + int64_t(i);
+            if (o < 0 || uint64_t(o) >= c.len) continue;
+            const uint32_t lane = i % LANES, s = i >> 7, fl = (i - s * 128 - lane) >> 4;
+            const uint32_t start = (fl_order_rt(fl) * 8 + s) * W, w0 = start / T, sh = start % T;
+            E v = 0;
+            if (W) {
+                uint64_t x = uint64_t(pw[LANES * w0 + lane]) >> sh;
+                if (sh + W > uint32_t(T)) x |= uint64_t(pw[LANES * (w0 + 1) + lane]) << (T - sh);
+                v = E(x) & mask;
+            }
+            gen_store(out + o, apply_epi<T, EPI, VW>(v, ep, oob));
+        }
+    }
+    if constexpr (EPI == Epi::Dict)
+        if (oob) __hip_atomic_fetch_or(err, kErrTakeOOB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// kinds: T index ti (8, 16, 32, 64 -> 0..3); Plain/For/ForZigZag 3 ti + e (0..11); AlpF32 12;
+// AlpF64 13; Dict 14 + 5 ti + value-width index (1, 2, 4, 8, 16 -> 0..4) (14..33)
+constexpr int kGenKinds = 34;
+
+template <int K>
+__device__ __forceinline__ void gen_dispatch_one(const GenChunk& gc, uint64_t g, uint8_t* lds, bool dl, uint32_t* err) {
+    constexpr int Ts[4] = {8, 16, 32, 64};
+    constexpr int VWs[5] = {1, 2, 4, 8, 16};
+    if constexpr (K < 12) {
+        constexpr Epi e = K % 3 == 0 ? Epi::Plain : (K % 3 == 1 ? Epi::For : Epi::ForZigZag);
+        gen_body<Ts[K / 3], e, 0>(gc, g, lds, dl, err);
+    } else if constexpr (K == 12) {
+        gen_body<32, Epi::AlpF32, 0>(gc, g, lds, dl, err);
+    } else if constexpr (K == 13) {
+        gen_body<64, Epi::AlpF64, 0>(gc, g, lds, dl, err);
+    } else {
+        gen_body<Ts[(K - 14) / 5], Epi::Dict, VWs[(K - 14) % 5]>(gc, g, lds, dl, err);
+    }
+}
+
+template <int... Ks>
+__device__ __forceinline__ void gen_dispatch(int kind, const GenChunk& gc, uint64_t g, uint8_t* lds, bool dl, uint32_t* err,
+                                             std::integer_sequence<int, Ks...>) {
+    ((kind == Ks ? gen_dispatch_one<Ks>(gc, g, lds, dl, err) : void()), ...);
+}
+
+__global__ __launch_bounds__(kGenThreads) void k1_generic_kernel(const GenChunk* __restrict__ tab, uint32_t n,
+                                                                 bool dict_lds, uint32_t* err) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const uint64_t g = blockIdx.x;
+    const GenChunk& gc = tab[ext_chunk_index(tab, n, g, [](const GenChunk& d) { return d.d.first_group; })];
+    gen_dispatch(int(gc.kind), gc, g, lds, dict_lds, err, std::make_integer_sequence<int, kGenKinds>{});
+}
+
+}  // namespace
+
+int gen_kind(int T, int epi, int vw) {
+    const int ti = T == 8 ? 0 : T == 16 ? 1 : T == 32 ? 2 : T == 64 ? 3 : -1;
+    if (ti < 0) return -1;
+    switch (Epi(epi)) {
+    case Epi::Plain: return 3 * ti;
+    case Epi::For: return 3 * ti + 1;
+    case Epi::ForZigZag: return 3 * ti + 2;
+    case Epi::AlpF32: return T == 32 ? 12 : -1;
+    case Epi::AlpF64: return T == 64 ? 13 : -1;
+    case Epi::Dict: {
+        const int vi = vw == 1 ? 0 : vw == 2 ? 1 : vw == 4 ? 2 : vw == 8 ? 3 : vw == 16 ? 4 : -1;
+        return vi < 0 ? -1 : 14 + 5 * ti + vi;
+    }
+    }
+    return -1;
+}
+
+uint32_t gen_bpw(int T, int W) {
+    (void)T;
+    const uint32_t per = 128u * uint32_t(W > 0 ? W : 1);
+    const uint32_t b = kGenPackedLds / per;
+    return b > 4 ? 4 : (b < 1 ? 1 : b);
+}
+
+vxg_status launch_k1_generic(const GenChunk* ext, uint32_t n, uint64_t groups, bool dict_lds, uint32_t* err,
+                             hipStream_t s) {
+    if (n == 0 || groups == 0) return VXG_OK;
+    if (groups > 0xFFFFFFFFull) return set_error(VXG_ERR_INVALID_ARGUMENT, "array too long for one launch");
+    const size_t shm = kGenPackedLds + (dict_lds ? size_t(kDictLdsBytes) : 0);
+    hipLaunchKernelGGL(k1_generic_kernel, dim3(unsigned(groups)), dim3(kGenThreads), shm, s, ext, n, dict_lds, err);
+    return hip_check(hipGetLastError(), "k1_generic_kernel launch");
+}
+
+}  // namespace vxg

@@ -1,0 +1,33 @@
+// k1g.hpp — K1g: one launch for many K1 decodes of DIFFERENT (T, W, epilogue) kernels.
+//
+// A recorded plan of a sharded scan (one GPU's chunk range of every column)
+// holds many small BitPacked decodes, one K1 kernel variant per column; at 1/8 of TPC-H SF1 each
+// is a 2-6 MB launch whose ramp/drain and graph edge cost more than its data.  K1g decodes every
+// job of such a plan in ONE launch: the job's (T, W, epilogue, value width) travel in its table
+// entry, the workgroup stages its blocks' packed words in LDS and each thread extracts output
+// values with runtime shifts (fastlanes unpack_single addressing, bitpacking/compress.rs:
+// 295-306), then applies the same epilogues as K1 (fl_unpack_impl.hpp).
+#pragma once
+
+#include "vxg_internal.hpp"
+
+namespace vxg {
+
+struct GenChunk {
+    ChunkDev d;        // first_group = first workgroup of this job in the launch
+    uint32_t kind;     // body index (gen_kind)
+    uint32_t W;        // bit width
+    uint32_t bpw;      // FastLanes blocks per workgroup
+    uint32_t pad;
+};
+
+// Body index of a (T, W, epilogue, value width) job, or -1 when K1g has no body for it.
+int gen_kind(int T, int epi, int vw);
+// Blocks per workgroup of a job (its packed words staged in <= 16 KiB of LDS).
+uint32_t gen_bpw(int T, int W);
+// One launch over a device table of n jobs (first_group filled in); `dict_lds` = every Dict job's
+// dictionary fits the LDS stage (16 KiB, 16-byte aligned).
+vxg_status launch_k1_generic(const GenChunk* ext, uint32_t n, uint64_t groups, bool dict_lds, uint32_t* err,
+                             hipStream_t s);
+
+}  // namespace vxg

@@ -286,8 +286,9 @@ struct FsstChunk {
     IntCol offs;              // codes VarBin offsets (n + 1)
     IntCol lens;              // uncompressed lengths (n)
     uint64_t n;
-    uint64_t first_tile;      // launch-local: first 256-string tile / first 128-tile scan block
-    uint64_t first_scan;
+    uint64_t heap_len;        // decoded bytes (sum of the lengths) if known, else 0: picks the LDS budget
+    uint64_t first_tile;      // launch-local: first decode workgroup (4 tiles of 64 strings) /
+    uint64_t first_scan;      //               first pre-pass workgroup (512 tiles)
     uint32_t n_symbols;
     uint32_t bidx;            // buffer_index of non-inlined views
 };
