@@ -3,7 +3,6 @@
 Builds C5 (this GPU's whole lineitem table), records it as a vxg_plan, and reports
   * host time of vxg_plan_launch alone (no sync), per call,
   * device time per replay (HIP events around back-to-back replays),
-  * the same for direct vxg_canonicalize calls per column (bench --no-graph path).
 Run on the GPU box: python tools/plan_probe.py
 """
 import os
@@ -23,10 +22,9 @@ def main():
 
     world = int(sys.argv[1]) if len(sys.argv) > 1 else 1
     ctx = V.Context(0)
-    arrs, info = bench.make_c5_shard(np.random.default_rng(42), world, 0)
-    dev = torch.device("cuda", 0)
-    trees = [a.to(dev) for a in arrs]
-    plan = A.Plan(trees, ctx)
+    (_, host, c0, c1), info = bench.make_c5(np.random.default_rng(42), world, 0)
+    wl = bench.FileWorkload(host, ctx, c0, c1)  # C5 as bench runs it: reader-built trees, one plan
+    plan = wl.plan
     for _ in range(5):
         plan.launch()
     ctx.sync()
@@ -47,24 +45,7 @@ def main():
         host_us.append(np.median(host) * 1e6)
     print(f"plan[{os.environ.get('VXG_GPU_LIB', 'in-tree')}] world={world}: host launch {min(host_us):.1f} us, "
           f"device us/replay min {min(dev_us):.1f} median {np.median(dev_us):.1f}")
-    if os.environ.get("PROBE_DIRECT") != "1":
-        plan.close()
-        return
-    # host launch into an idle-then-blocked stream: measures pure submission
-    wl = bench.Workload(arrs, info, ctx, 1, graph=False)
-    for _ in range(3):
-        wl.step()
-    ctx.sync()
-    host = []
-    e0.record()
-    for _ in range(20):
-        t = time.perf_counter()
-        wl.step()
-        host.append(time.perf_counter() - t)
-    e1.record()
-    torch.cuda.synchronize()
-    print(f"direct: host {np.median(host) * 1e6:.1f} us/step median, device {e0.elapsed_time(e1) / 20 * 1e3:.1f} us/step")
-    plan.close()
+    wl.close()
 
 
 if __name__ == "__main__":

@@ -128,10 +128,14 @@ struct K1Job {
     Epi epi;
     int vw;
     ChunkDev d;
+    // a plan batch's Dict over a small VarBin dictionary: K1g builds the dictionary's views
+    // (d.dict unused) and copies its bytes (vb.src -> vb.dst); only K1g runs such a job
+    bool vb = false;
+    VarBinChunk vbc{};
 };
 
 bool same_kernel(const K1Job& a, const K1Job& b) {
-    return a.T == b.T && a.W == b.W && a.epi == b.epi && a.vw == b.vw;
+    return a.T == b.T && a.W == b.W && a.epi == b.epi && a.vw == b.vw && a.vb == b.vb;
 }
 
 // Output bytes below which a plan batch's kernel group goes to the one K1g launch instead of its
@@ -159,7 +163,7 @@ static int k1_out_width(const K1Job& j) {
 vxg_status launch_k1_jobs(std::vector<K1Job>& jobs, uint32_t* err, hipStream_t s, DevTables* dt = nullptr,
                           bool generic_small = false) {
     std::stable_sort(jobs.begin(), jobs.end(), [](const K1Job& a, const K1Job& b) {
-        return std::make_tuple(a.T, a.W, int(a.epi), a.vw) < std::make_tuple(b.T, b.W, int(b.epi), b.vw);
+        return std::make_tuple(a.T, a.W, int(a.epi), a.vw, a.vb) < std::make_tuple(b.T, b.W, int(b.epi), b.vw, b.vb);
     });
     std::vector<const K1Job*> gen;  // jobs for the shared K1g launch
     size_t i = 0;
@@ -171,7 +175,9 @@ vxg_status launch_k1_jobs(std::vector<K1Job>& jobs, uint32_t* err, hipStream_t s
             out_bytes += jobs[j].d.len * uint64_t(k1_out_width(jobs[j]));
             j++;
         }
-        if (dt && generic_small && out_bytes < k1g_max_bytes() && gen_kind(jobs[i].T, int(jobs[i].epi), jobs[i].vw) >= 0) {
+        if (jobs[i].vb || (dt && generic_small && out_bytes < k1g_max_bytes() &&
+                           gen_kind(jobs[i].T, int(jobs[i].epi), jobs[i].vw) >= 0)) {
+            if (!dt) return set_error(VXG_ERR_INVALID_ARGUMENT, "VarBin-dictionary K1 jobs need a plan");
             for (size_t k = i; k < j; k++)
                 if (jobs[k].d.n_blocks) gen.push_back(&jobs[k]);
             i = j;
@@ -206,21 +212,30 @@ vxg_status launch_k1_jobs(std::vector<K1Job>& jobs, uint32_t* err, hipStream_t s
         const GenChunk* ext;
         VXG_TRY_S(dt->table(gen.size(), &host, &ext));
         uint64_t groups = 0;
-        bool dict_lds = true;
+        bool dict_lds = true, any_vb = false;
         for (size_t k = 0; k < gen.size(); k++) {
             const K1Job& jb = *gen[k];
             GenChunk& g = host[k];
             g.d = jb.d;
-            g.kind = uint32_t(gen_kind(jb.T, int(jb.epi), jb.vw));
+            g.kind = uint32_t(gen_kind(jb.T, int(jb.epi), jb.vw, jb.vb));
             g.W = uint32_t(jb.W);
             g.bpw = gen_bpw(jb.T, jb.W);
             g.d.first_group = groups;
             groups += (jb.d.n_blocks + g.bpw - 1) / g.bpw;
-            if (jb.epi == Epi::Dict)
+            if (jb.vb) {
+                any_vb = true;
+                g.vb_src = jb.vbc.src;
+                g.vb_offs = jb.vbc.offsets;
+                g.vb_offs_width = jb.vbc.offs_width;
+                g.vb_dst = jb.vbc.dst;
+                g.vb_bytes = jb.vbc.bytes;
+                g.vb_bidx = jb.vbc.bidx;
+            } else if (jb.epi == Epi::Dict) {
                 dict_lds = dict_lds && jb.d.dict_len * uint64_t(jb.vw) <= uint64_t(kDictLdsBytes) &&
                            (reinterpret_cast<uintptr_t>(jb.d.dict) & 15) == 0;
+            }
         }
-        VXG_TRY_S(launch_k1_generic(ext, uint32_t(gen.size()), groups, dict_lds, err, s));
+        VXG_TRY_S(launch_k1_generic(ext, uint32_t(gen.size()), groups, dict_lds, any_vb, err, s));
     }
     return VXG_OK;
 }
@@ -1585,17 +1600,29 @@ vxg_status Planner::strings_into(const vxg_array& a, uint8_t* views, uint8_t* da
                 d.n = v.len;
                 d.offs_width = uint32_t(width(v.children[0]));
                 d.bidx = bidx + b;
-                dicts.push_back(d);
+                // a plan batch with a small dictionary: K1g builds its views in LDS (no views
+                // launch); otherwise the views are built into dviews first
+                const vxg_array& codes = c.children[1];
+                const bool vb = batch_ && v.len <= kGenVarBinDictMax && v.len > 0 && codes.len > 0 &&
+                                !codes.meta.bitpacked.has_patches;
+                if (!vb) dicts.push_back(d);
                 UnpackArgs ua{};
-                ua.dict = dviews;
+                ua.dict = vb ? nullptr : dviews;
                 ua.dict_len = v.len;
                 dviews += 16 * v.len;
                 k1_batch_ = &jobs;
                 patch_batch_ = &patches;
+                const size_t nj = jobs.size(), np = patches.size();
                 const vxg_status st = decode_bitpacked(c.children[1], Epi::Dict, 16, ua, views + 16 * row);
                 k1_batch_ = nullptr;
                 patch_batch_ = nullptr;
                 VXG_TRY(st);
+                if (vb) {
+                    if (jobs.size() != nj + 1 || patches.size() != np)
+                        return set_error(VXG_ERR_INVALID_ARGUMENT, "internal: VarBin-dictionary job shape");
+                    jobs.back().vb = true;
+                    jobs.back().vbc = d;
+                }
             } else {
                 void* cv = nullptr;  // the chunk's own validity (null views are all-zero)
                 const vxg_array* vn;
@@ -1871,12 +1898,12 @@ static uint64_t plan_cost(const vxg_array& a) {
     return tree_bytes(a) + out;
 }
 
-// Parallel graph branches of a plan (VXG_PLAN_BRANCHES overrides, 1..16).
-static uint32_t plan_branches() {
+// Parallel graph branches of a plan (VXG_PLAN_BRANCHES overrides, 1..16; 0 = unset).
+static uint32_t plan_branches_env() {
     static const uint32_t nb = [] {
         const char* e = std::getenv("VXG_PLAN_BRANCHES");
         const long v = e ? std::strtol(e, nullptr, 10) : 0;
-        return v >= 1 && v <= 16 ? uint32_t(v) : 2u;
+        return v >= 1 && v <= 16 ? uint32_t(v) : 0u;
     }();
     return nb;
 }
@@ -1928,11 +1955,20 @@ vxg_status vxg_plan_create(vxg_ctx* ctx, const vxg_array* arrays, vxg_canonical*
     // The small arrays' deferrable launches (PlanBatch: K1 decodes, RunEnd expansions,
     // dictionary views of chunked columns) go to one more branch, recorded after all arrays were
     // visited.
-    const uint32_t kPlanBranches = plan_branches();
-    bool batching = false;
-    for (uint32_t i = 0; i < n; i++) batching = batching || canonical_out_bytes(arrays[i]) <= plan_batch_max_bytes();
-    const uint32_t nb = (n < kPlanBranches ? (n ? n : 1) : kPlanBranches) + (batching ? 1 : 0);
-    const uint32_t na = batching ? nb - 1 : nb;  // branches the arrays are spread over
+    bool batching = false, all_small = n > 0;
+    for (uint32_t i = 0; i < n; i++) {
+        const bool small = canonical_out_bytes(arrays[i]) <= plan_batch_max_bytes();
+        batching = batching || small;
+        all_small = all_small && small;
+    }
+    // Branches: 2 by default; ONE when every array is small (a sharded scan): each cross-branch
+    // edge of a graph costs the replay several microseconds of queue synchronisation, more than
+    // the small kernels gain from overlapping (C5 8-GPU shard: 82 -> 68 us per replay).
+    const uint32_t kPlanBranches = plan_branches_env() ? plan_branches_env() : (all_small ? 1u : 2u);
+    // (one branch requested: the batch follows the arrays on that branch -- a single-stream graph)
+    const bool own = batching && kPlanBranches > 1;
+    const uint32_t nb = (n < kPlanBranches ? (n ? n : 1) : kPlanBranches) + (own ? 1 : 0);
+    const uint32_t na = own ? nb - 1 : nb;  // branches the arrays are spread over
     PlanBatch batch;
     hipStream_t cs;
     VXG_TRY(hip_check(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking), "plan stream"));

@@ -25,7 +25,28 @@ __device__ __forceinline__ void gen_store(O* p, const O& v) {
     else *p = v;
 }
 
-template <int T, Epi EPI, int VW>
+__device__ __forceinline__ uint64_t vb_offset(const void* p, uint32_t w, uint64_t i) {
+    switch (w) {  // VarBin offsets are non-negative: signedness does not matter
+    case 1: return static_cast<const uint8_t*>(p)[i];
+    case 2: return static_cast<const uint16_t*>(p)[i];
+    case 4: return static_cast<const uint32_t*>(p)[i];
+    default: return static_cast<const uint64_t*>(p)[i];
+    }
+}
+
+// arrow-array 53.2 make_view (as kernels.hip: len <= 12 inline, else prefix + buffer + offset)
+__device__ __forceinline__ uint4 vb_view(const uint8_t* __restrict__ heap, uint64_t start, uint32_t len, uint32_t bidx) {
+    const uint8_t* p = heap + start;
+    uint32_t w[3] = {0, 0, 0};
+    if (len <= 12) {
+        for (uint32_t j = 0; j < len; j++) w[j >> 2] |= uint32_t(p[j]) << (8 * (j & 3));
+        return make_uint4(len, w[0], w[1], w[2]);
+    }
+    for (uint32_t j = 0; j < 4; j++) w[0] |= uint32_t(p[j]) << (8 * j);
+    return make_uint4(len, w[0], bidx, uint32_t(start));
+}
+
+template <int T, Epi EPI, int VW, bool VB = false>
 __device__ __forceinline__ void gen_body(const GenChunk& gc, uint64_t g, uint8_t* lds, bool dict_lds, uint32_t* err) {
     using E = typename Fl<T>::E;
     using O = typename EpiOut<T, EPI, VW>::type;
@@ -46,7 +67,22 @@ __device__ __forceinline__ void gen_body(const GenChunk& gc, uint64_t g, uint8_t
     ep.dict = c.dict;
     ep.dict_len = c.dict_len;
     ep.err = err;
-    if constexpr (EPI == Epi::Dict) {
+    if constexpr (VB) {
+        static_assert(EPI == Epi::Dict && VW == 16, "VarBin dictionaries are string views");
+        // this workgroup's share of the dictionary bytes -> the output data buffer
+        const uint64_t ng = (c.n_blocks + gc.bpw - 1) / gc.bpw, lg = g - c.first_group;
+        const uint64_t per = (gc.vb_bytes + ng - 1) / ng;
+        const uint64_t b1 = (lg + 1) * per < gc.vb_bytes ? (lg + 1) * per : gc.vb_bytes;
+        for (uint64_t b = lg * per + tid; b < b1; b += kGenThreads) gc.vb_dst[b] = gc.vb_src[b];
+        // the dictionary's views, in LDS
+        uint4* const s_views = reinterpret_cast<uint4*>(lds + kGenPackedLds);
+        for (uint32_t k = tid; k < c.dict_len; k += kGenThreads) {
+            const uint64_t a = vb_offset(gc.vb_offs, gc.vb_offs_width, k);
+            const uint64_t e = vb_offset(gc.vb_offs, gc.vb_offs_width, k + 1);
+            s_views[k] = vb_view(gc.vb_src, a, uint32_t(e - a), gc.vb_bidx);
+        }
+        ep.dict = s_views;
+    } else if constexpr (EPI == Epi::Dict) {
         if (dict_lds) {
             uint8_t* const s_dict = lds + kGenPackedLds;
             const uint32_t n16 = uint32_t((c.dict_len * VW + 15) / 16);
@@ -83,8 +119,9 @@ __device__ __forceinline__ void gen_body(const GenChunk& gc, uint64_t g, uint8_t
 }
 
 // kinds: T index ti (8, 16, 32, 64 -> 0..3); Plain/For/ForZigZag 3 ti + e (0..11); AlpF32 12;
-// AlpF64 13; Dict 14 + 5 ti + value-width index (1, 2, 4, 8, 16 -> 0..4) (14..33)
-constexpr int kGenKinds = 34;
+// AlpF64 13; Dict 14 + 5 ti + value-width index (1, 2, 4, 8, 16 -> 0..4) (14..33); Dict over a
+// VarBin dictionary 34 + ti (34..37)
+constexpr int kGenKinds = 38;
 
 template <int K>
 __device__ __forceinline__ void gen_dispatch_one(const GenChunk& gc, uint64_t g, uint8_t* lds, bool dl, uint32_t* err) {
@@ -97,8 +134,10 @@ __device__ __forceinline__ void gen_dispatch_one(const GenChunk& gc, uint64_t g,
         gen_body<32, Epi::AlpF32, 0>(gc, g, lds, dl, err);
     } else if constexpr (K == 13) {
         gen_body<64, Epi::AlpF64, 0>(gc, g, lds, dl, err);
-    } else {
+    } else if constexpr (K < 34) {
         gen_body<Ts[(K - 14) / 5], Epi::Dict, VWs[(K - 14) % 5]>(gc, g, lds, dl, err);
+    } else {
+        gen_body<Ts[K - 34], Epi::Dict, 16, true>(gc, g, lds, dl, err);
     }
 }
 
@@ -118,9 +157,10 @@ __global__ __launch_bounds__(kGenThreads) void k1_generic_kernel(const GenChunk*
 
 }  // namespace
 
-int gen_kind(int T, int epi, int vw) {
+int gen_kind(int T, int epi, int vw, bool varbin_dict) {
     const int ti = T == 8 ? 0 : T == 16 ? 1 : T == 32 ? 2 : T == 64 ? 3 : -1;
     if (ti < 0) return -1;
+    if (varbin_dict) return Epi(epi) == Epi::Dict && vw == 16 ? 34 + ti : -1;
     switch (Epi(epi)) {
     case Epi::Plain: return 3 * ti;
     case Epi::For: return 3 * ti + 1;
@@ -142,11 +182,12 @@ uint32_t gen_bpw(int T, int W) {
     return b > 4 ? 4 : (b < 1 ? 1 : b);
 }
 
-vxg_status launch_k1_generic(const GenChunk* ext, uint32_t n, uint64_t groups, bool dict_lds, uint32_t* err,
-                             hipStream_t s) {
+vxg_status launch_k1_generic(const GenChunk* ext, uint32_t n, uint64_t groups, bool dict_lds, bool any_vb,
+                             uint32_t* err, hipStream_t s) {
+    static_assert(kGenVarBinDictMax * 16 <= uint64_t(kDictLdsBytes), "VarBin views must fit the dictionary stage");
     if (n == 0 || groups == 0) return VXG_OK;
     if (groups > 0xFFFFFFFFull) return set_error(VXG_ERR_INVALID_ARGUMENT, "array too long for one launch");
-    const size_t shm = kGenPackedLds + (dict_lds ? size_t(kDictLdsBytes) : 0);
+    const size_t shm = kGenPackedLds + (dict_lds || any_vb ? size_t(kDictLdsBytes) : 0);
     hipLaunchKernelGGL(k1_generic_kernel, dim3(unsigned(groups)), dim3(kGenThreads), shm, s, ext, n, dict_lds, err);
     return hip_check(hipGetLastError(), "k1_generic_kernel launch");
 }

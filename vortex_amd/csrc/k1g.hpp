@@ -18,16 +18,29 @@ struct GenChunk {
     uint32_t kind;     // body index (gen_kind)
     uint32_t W;        // bit width
     uint32_t bpw;      // FastLanes blocks per workgroup
+    uint32_t vb_offs_width;
+    // Dict over a VarBin string dictionary (<= 1024 entries): every workgroup builds the
+    // dictionary's 16-byte views in LDS (the K10 views launch disappears) and copies its share of
+    // the dictionary bytes into the chunk's output data buffer (varbin_chunks_kernel's work)
+    const uint8_t* vb_src;   // dictionary bytes
+    const void* vb_offs;     // dictionary offsets (dict_len + 1)
+    uint8_t* vb_dst;         // the chunk's output data buffer
+    uint64_t vb_bytes;       // bytes to copy
+    uint32_t vb_bidx;        // buffer_index of non-inlined views
     uint32_t pad;
 };
 
-// Body index of a (T, W, epilogue, value width) job, or -1 when K1g has no body for it.
-int gen_kind(int T, int epi, int vw);
+// Body index of a (T, W, epilogue, value width) job, or -1 when K1g has no body for it
+// (varbin_dict: Dict over a VarBin dictionary whose views K1g builds, value width 16).
+int gen_kind(int T, int epi, int vw, bool varbin_dict = false);
+// Largest VarBin dictionary a K1g job builds in LDS.
+constexpr uint64_t kGenVarBinDictMax = 1024;
 // Blocks per workgroup of a job (its packed words staged in <= 16 KiB of LDS).
 uint32_t gen_bpw(int T, int W);
 // One launch over a device table of n jobs (first_group filled in); `dict_lds` = every Dict job's
-// dictionary fits the LDS stage (16 KiB, 16-byte aligned).
-vxg_status launch_k1_generic(const GenChunk* ext, uint32_t n, uint64_t groups, bool dict_lds, uint32_t* err,
-                             hipStream_t s);
+// dictionary fits the LDS stage (16 KiB, 16-byte aligned); `any_vb` = some job builds VarBin
+// dictionary views (their stage is always allocated).
+vxg_status launch_k1_generic(const GenChunk* ext, uint32_t n, uint64_t groups, bool dict_lds, bool any_vb,
+                             uint32_t* err, hipStream_t s);
 
 }  // namespace vxg
