@@ -161,7 +161,8 @@ static int k1_out_width(const K1Job& j) {
 // (k1g.hpp): a sharded scan's many small per-column kernels cost more in ramp, drain and graph
 // edges than in data.
 vxg_status launch_k1_jobs(std::vector<K1Job>& jobs, uint32_t* err, hipStream_t s, DevTables* dt = nullptr,
-                          bool generic_small = false) {
+                          bool generic_small = false,
+                          const std::vector<std::pair<int, RunEndChunk>>* gen_runs = nullptr) {
     std::stable_sort(jobs.begin(), jobs.end(), [](const K1Job& a, const K1Job& b) {
         return std::make_tuple(a.T, a.W, int(a.epi), a.vw, a.vb) < std::make_tuple(b.T, b.W, int(b.epi), b.vw, b.vb);
     });
@@ -206,11 +207,12 @@ vxg_status launch_k1_jobs(std::vector<K1Job>& jobs, uint32_t* err, hipStream_t s
         }
         i = j;
     }
-    if (!gen.empty()) {
-        if (gen.size() > 0xFFFFFFFFull) return set_error(VXG_ERR_INVALID_ARGUMENT, "too many chunks");
+    const size_t n_runs = gen_runs ? gen_runs->size() : 0;
+    if (!gen.empty() || n_runs) {
+        if (gen.size() + n_runs > 0xFFFFFFFFull) return set_error(VXG_ERR_INVALID_ARGUMENT, "too many chunks");
         GenChunk* host;
         const GenChunk* ext;
-        VXG_TRY_S(dt->table(gen.size(), &host, &ext));
+        VXG_TRY_S(dt->table(gen.size() + n_runs, &host, &ext));
         uint64_t groups = 0;
         bool dict_lds = true, any_vb = false;
         for (size_t k = 0; k < gen.size(); k++) {
@@ -235,7 +237,17 @@ vxg_status launch_k1_jobs(std::vector<K1Job>& jobs, uint32_t* err, hipStream_t s
                            (reinterpret_cast<uintptr_t>(jb.d.dict) & 15) == 0;
             }
         }
-        VXG_TRY_S(launch_k1_generic(ext, uint32_t(gen.size()), groups, dict_lds, any_vb, err, s));
+        for (size_t k = 0; k < n_runs; k++) {  // short-run RunEnd expansions (runend_runs.hpp)
+            const auto& [w, r] = (*gen_runs)[k];
+            GenChunk& g = host[gen.size() + k];
+            g.kind = uint32_t(gen_runs_kind(w));
+            g.re = r;
+            g.d.first_group = groups;
+            g.d.n_blocks = r.n_runs;  // (unused by the body; keeps the entry self-describing)
+            groups += (r.n_runs + kRunEndRunsPerGroup - 1) / kRunEndRunsPerGroup;
+        }
+        VXG_TRY_S(launch_k1_generic(ext, uint32_t(gen.size() + n_runs), groups, dict_lds, any_vb, n_runs > 0, err,
+                                    s));
     }
     return VXG_OK;
 }
@@ -333,9 +345,14 @@ vxg_status launch_runs(std::vector<RunEndChunk> runs, int w, uint32_t* err, hipS
 // the end of recording on one graph branch (dictionary views, then one launch per large K1 kernel
 // group + one K1g launch for all the small ones, then the expansions), instead of per column.
 struct PlanBatch {
+    struct Run {
+        int w;             // value width
+        RunEndChunk c;
+        bool indep;        // ends/values read in place (no K1 decode of this batch feeds it)
+    };
     std::vector<VarBinChunk> dicts;
     std::vector<K1Job> jobs;
-    std::vector<std::pair<int, RunEndChunk>> runs;  // (value width, chunk)
+    std::vector<Run> runs;
     bool empty() const { return dicts.empty() && jobs.empty() && runs.empty(); }
 };
 
@@ -363,15 +380,24 @@ vxg_status launch_varbin_dicts(const std::vector<VarBinChunk>& dicts, hipStream_
 
 vxg_status flush_plan_batch(PlanBatch& b, uint32_t* err, hipStream_t s, DevTables* dt) {
     VXG_TRY_S(launch_varbin_dicts(b.dicts, s, dt));
-    VXG_TRY_S(launch_k1_jobs(b.jobs, err, s, dt, true));
+    // short-run expansions that read their children in place join the K1g launch; the others
+    // follow the K1 decodes that produce their children
+    std::vector<std::pair<int, RunEndChunk>> gen_runs;
+    std::vector<PlanBatch::Run> rest;
+    for (const PlanBatch::Run& r : b.runs) {
+        if (r.c.len == 0) continue;
+        if (r.indep && r.c.len <= kRunEndShortRun * r.c.n_runs && gen_runs_kind(r.w) >= 0) gen_runs.emplace_back(r.w, r.c);
+        else rest.push_back(r);
+    }
+    VXG_TRY_S(launch_k1_jobs(b.jobs, err, s, dt, true, &gen_runs));
     std::vector<int> widths;
-    for (const auto& r : b.runs) widths.push_back(r.first);
+    for (const auto& r : rest) widths.push_back(r.w);
     std::sort(widths.begin(), widths.end());
     widths.erase(std::unique(widths.begin(), widths.end()), widths.end());
     for (int w : widths) {
         std::vector<RunEndChunk> rs;
-        for (const auto& r : b.runs)
-            if (r.first == w) rs.push_back(r.second);
+        for (const auto& r : rest)
+            if (r.w == w) rs.push_back(r.c);
         VXG_TRY_S(launch_runs(rs, w, err, s, dt));
     }
     return VXG_OK;
@@ -697,6 +723,7 @@ vxg_status Planner::decode_chunked_primitive(const vxg_array& a, void* dst) {
     std::vector<K1Job> jobs;
     std::vector<PatchJob> patches;
     std::vector<RunEndChunk> runs;
+    std::vector<uint8_t> runs_indep;  // the run's children are read in place (no level-0 decode)
     // RunEnd chunks whose ends/values are primitive or one K1 decode: their temporaries
     auto child_ok = [&](const vxg_array* x) {
         return x && ptype_is_int(x->ptype) && (x->encoding == VXG_ENC_PRIMITIVE || k1_fusable(*x));
@@ -777,6 +804,8 @@ vxg_status Planner::decode_chunked_primitive(const vxg_array& a, void* dst) {
             r.offset = c.meta.runend.offset;
             r.len = c.len;
             runs.push_back(r);
+            runs_indep.push_back(uint8_t((is_inplace[2 * i] || e.encoding == VXG_ENC_PRIMITIVE) &&
+                                         (is_inplace[2 * i + 1] || v.encoding == VXG_ENC_PRIMITIVE)));
         } else if ((reinterpret_cast<uintptr_t>(slice) & 15) == 0) {
             VXG_TRY(decode_into(c, slice));
         } else {
@@ -789,7 +818,7 @@ vxg_status Planner::decode_chunked_primitive(const vxg_array& a, void* dst) {
     if (off != a.len) return set_error(VXG_ERR_INVALID_ARGUMENT, "Chunked len != sum of chunk lens");
     if (batch_ && patches.empty()) {  // a plan: launched with the other arrays' jobs (PlanBatch)
         batch_->jobs.insert(batch_->jobs.end(), jobs.begin(), jobs.end());
-        for (const RunEndChunk& r : runs) batch_->runs.emplace_back(w, r);
+        for (size_t k = 0; k < runs.size(); k++) batch_->runs.push_back(PlanBatch::Run{w, runs[k], runs_indep[k] != 0});
         return VXG_OK;
     }
     VXG_TRY(launch_k1_jobs(jobs, ctx_->c.err_word, s_, plan_));

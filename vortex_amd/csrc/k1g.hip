@@ -6,8 +6,11 @@
 // block (64 consecutive values per store wave-instruction); value i of a block is unpack_single's
 // (lane, row) -> one or two T-bit words of that lane.  The body (T, epilogue, value width) is a
 // workgroup-uniform switch on the job's kind.
+#include <algorithm>
+
 #include "fl_unpack_impl.hpp"
 #include "k1g.hpp"
+#include "runend_runs.hpp"
 
 namespace vxg {
 
@@ -120,8 +123,8 @@ __device__ __forceinline__ void gen_body(const GenChunk& gc, uint64_t g, uint8_t
 
 // kinds: T index ti (8, 16, 32, 64 -> 0..3); Plain/For/ForZigZag 3 ti + e (0..11); AlpF32 12;
 // AlpF64 13; Dict 14 + 5 ti + value-width index (1, 2, 4, 8, 16 -> 0..4) (14..33); Dict over a
-// VarBin dictionary 34 + ti (34..37)
-constexpr int kGenKinds = 38;
+// VarBin dictionary 34 + ti (34..37); RunEnd short runs 38 + value-width index (38..42)
+constexpr int kGenKinds = 43;
 
 template <int K>
 __device__ __forceinline__ void gen_dispatch_one(const GenChunk& gc, uint64_t g, uint8_t* lds, bool dl, uint32_t* err) {
@@ -136,8 +139,17 @@ __device__ __forceinline__ void gen_dispatch_one(const GenChunk& gc, uint64_t g,
         gen_body<64, Epi::AlpF64, 0>(gc, g, lds, dl, err);
     } else if constexpr (K < 34) {
         gen_body<Ts[(K - 14) / 5], Epi::Dict, VWs[(K - 14) % 5]>(gc, g, lds, dl, err);
-    } else {
+    } else if constexpr (K < 38) {
         gen_body<Ts[K - 34], Epi::Dict, 16, true>(gc, g, lds, dl, err);
+    } else {
+        using V = std::conditional_t<
+            VWs[K - 38] == 1, uint8_t,
+            std::conditional_t<VWs[K - 38] == 2, uint16_t,
+                               std::conditional_t<VWs[K - 38] == 4, uint32_t,
+                                                  std::conditional_t<VWs[K - 38] == 8, uint64_t, uint4>>>>;
+        RunEndChunk rc = gc.re;
+        rc.first_group = gc.d.first_group;
+        runend_runs_body<V>(rc, g, err, lds);
     }
 }
 
@@ -156,6 +168,17 @@ __global__ __launch_bounds__(kGenThreads) void k1_generic_kernel(const GenChunk*
 }
 
 }  // namespace
+
+int gen_runs_kind(int value_width) {
+    switch (value_width) {
+    case 1: return 38;
+    case 2: return 39;
+    case 4: return 40;
+    case 8: return 41;
+    case 16: return 42;
+    default: return -1;
+    }
+}
 
 int gen_kind(int T, int epi, int vw, bool varbin_dict) {
     const int ti = T == 8 ? 0 : T == 16 ? 1 : T == 32 ? 2 : T == 64 ? 3 : -1;
@@ -183,11 +206,12 @@ uint32_t gen_bpw(int T, int W) {
 }
 
 vxg_status launch_k1_generic(const GenChunk* ext, uint32_t n, uint64_t groups, bool dict_lds, bool any_vb,
-                             uint32_t* err, hipStream_t s) {
+                             bool any_runs, uint32_t* err, hipStream_t s) {
     static_assert(kGenVarBinDictMax * 16 <= uint64_t(kDictLdsBytes), "VarBin views must fit the dictionary stage");
     if (n == 0 || groups == 0) return VXG_OK;
     if (groups > 0xFFFFFFFFull) return set_error(VXG_ERR_INVALID_ARGUMENT, "array too long for one launch");
-    const size_t shm = kGenPackedLds + (dict_lds || any_vb ? size_t(kDictLdsBytes) : 0);
+    size_t shm = kGenPackedLds + (dict_lds || any_vb ? size_t(kDictLdsBytes) : 0);
+    if (any_runs) shm = std::max(shm, runs_lds_bytes<uint4>());
     hipLaunchKernelGGL(k1_generic_kernel, dim3(unsigned(groups)), dim3(kGenThreads), shm, s, ext, n, dict_lds, err);
     return hip_check(hipGetLastError(), "k1_generic_kernel launch");
 }

@@ -28,11 +28,16 @@ struct GenChunk {
     uint64_t vb_bytes;       // bytes to copy
     uint32_t vb_bidx;        // buffer_index of non-inlined views
     uint32_t pad;
+    // RunEnd kinds: a short-run chunk (runend_runs.hpp) whose ends/values are read in place
+    // (re.first_group unused: d.first_group is the job's first workgroup)
+    RunEndChunk re;
 };
 
 // Body index of a (T, W, epilogue, value width) job, or -1 when K1g has no body for it
 // (varbin_dict: Dict over a VarBin dictionary whose views K1g builds, value width 16).
 int gen_kind(int T, int epi, int vw, bool varbin_dict = false);
+// Body index of a short-run RunEnd expansion with `value_width`-byte values, or -1.
+int gen_runs_kind(int value_width);
 // Largest VarBin dictionary a K1g job builds in LDS.
 constexpr uint64_t kGenVarBinDictMax = 1024;
 // Blocks per workgroup of a job (its packed words staged in <= 16 KiB of LDS).
@@ -41,6 +46,6 @@ uint32_t gen_bpw(int T, int W);
 // dictionary fits the LDS stage (16 KiB, 16-byte aligned); `any_vb` = some job builds VarBin
 // dictionary views (their stage is always allocated).
 vxg_status launch_k1_generic(const GenChunk* ext, uint32_t n, uint64_t groups, bool dict_lds, bool any_vb,
-                             uint32_t* err, hipStream_t s);
+                             bool any_runs, uint32_t* err, hipStream_t s);
 
 }  // namespace vxg

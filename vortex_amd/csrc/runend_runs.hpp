@@ -1,0 +1,139 @@
+// runend_runs.hpp — K8r body: RunEnd expansion of chunks with short runs, 1024 runs per
+// 256-thread workgroup (runend/compress.rs:115-148).  Shared by the K8r launch (kernels.hip) and
+// the K1g launch of a plan batch (k1g.hip), which hands it LDS of its own.
+#pragma once
+
+#include "intcol.hpp"
+
+namespace vxg {
+
+// Short runs (C5's l_orderkey: 1-7 rows per order): a workgroup takes 1024 consecutive RUNS
+// (not an output span), so no search is needed: thread t reads ends[r] and values[r] of runs
+// r0 + 4 t + k (k < 4) in one round trip -- from plain buffers, or unpacked in place from
+// patch-free [FoR](BitPacked) children (fastlanes unpack_single, bitpacking/compress.rs:295-306),
+// so the children are never materialised.  Run r covers the trimmed range
+// [min(ends[r-1] - offset, len), min(ends[r] - offset, len)) (runend_decode_primitive,
+// runend/compress.rs:138-146; the previous end is the thread's own, its left lane's, or the
+// previous wave's last, through LDS), and the workgroup's runs cover
+// one contiguous output range.  That range is expanded in windows of 4096 outputs: each
+// non-empty run writes its index at its first output (a run head), a max-scan fills the window,
+// and the window is written with coalesced non-temporal stores (the run carried into the next
+// window is the last scanned one).  Chunks whose runs average > kRunEndShortRun rows take the
+// span kernel above.
+template <typename V>
+__device__ __forceinline__ V runend_value(const IntCol& c, uint64_t r) {
+    if constexpr (sizeof(V) == 4 || sizeof(V) == 8) {
+        if (c.packed) return V(uint64_t(intcol_get(c, r)));  // low bytes: the value's bits
+    }
+    return static_cast<const V*>(c.p)[r];
+}
+
+constexpr int kRunsThreads = 256;
+constexpr int kRunsSpan = 4096;  // outputs per expansion window
+// LDS of one workgroup: run heads (kRunsSpan u32), run values (kRunEndRunsPerGroup V), scratch
+template <typename V>
+constexpr size_t runs_lds_bytes() {
+    return kRunsSpan * 4 + kRunEndRunsPerGroup * sizeof(V) + 128;
+}
+
+// Workgroup g of the launch expands its 1024 runs of chunk c (c.first_group = its first
+// workgroup).  `lds` = runs_lds_bytes<V>() bytes, 16-byte aligned.
+template <typename V>
+__device__ __forceinline__ void runend_runs_body(const RunEndChunk& c, uint64_t g, uint32_t* err, uint8_t* lds) {
+    constexpr int kBlock = kRunsThreads;
+    constexpr int SPAN = kRunsSpan, PER = SPAN / kBlock, RPG = int(kRunEndRunsPerGroup), RPT = RPG / kBlock;
+    uint32_t* const s_head = reinterpret_cast<uint32_t*>(lds);
+    V* const s_val = reinterpret_cast<V*>(lds + SPAN * 4);
+    uint8_t* const misc = lds + SPAN * 4 + RPG * sizeof(V);
+    uint64_t* const s_wlast = reinterpret_cast<uint64_t*>(misc);           // kBlock / 64
+    uint64_t& s_lo = reinterpret_cast<uint64_t*>(misc)[4];
+    uint64_t& s_hi = reinterpret_cast<uint64_t*>(misc)[5];
+    uint32_t* const s_wmax = reinterpret_cast<uint32_t*>(misc + 48);       // kBlock / 64
+    uint32_t& s_carry = reinterpret_cast<uint32_t*>(misc + 48)[4];
+    const int tid = threadIdx.x;
+    const uint64_t r0 = (g - c.first_group) * uint64_t(RPG);
+    const int nr = int(c.n_runs - r0 < uint64_t(RPG) ? c.n_runs - r0 : uint64_t(RPG));
+    auto trim = [&](uint64_t e) { return e > c.offset ? (e - c.offset < c.len ? e - c.offset : c.len) : 0; };
+    // thread t owns runs RPT t .. RPT t + RPT - 1; every load of the round trip issued before
+    // any is used
+    uint64_t e[RPT];
+    V v[RPT];
+#pragma unroll
+    for (int k = 0; k < RPT; k++) {
+        const int i = RPT * tid + k;
+        const uint64_t rr = r0 + uint64_t(i < nr ? i : 0);
+        e[k] = uint64_t(intcol_get(c.ends, rr));
+        v[k] = runend_value<V>(c.values, rr);
+    }
+    const uint64_t eprev = tid == 0 && r0 > 0 ? uint64_t(intcol_get(c.ends, r0 - 1)) : 0;
+    uint64_t en[RPT], st[RPT];
+#pragma unroll
+    for (int k = 0; k < RPT; k++) {
+        const int i = RPT * tid + k;
+        en[k] = trim(e[k]);
+        if (i < nr) {
+            s_val[i] = v[k];
+            if (i == nr - 1) s_hi = en[k];
+            if (r0 + uint64_t(i) + 1 == c.n_runs && en[k] < c.len)  // the ends do not reach the end of the array
+                __hip_atomic_fetch_or(err, kErrRunEnd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    // a run starts at the previous run's trimmed end: in this thread, in lane t - 1, or in the
+    // previous wave's last lane
+    const uint64_t left = __shfl_up(en[RPT - 1], 1, 64);
+    if ((tid & 63) == 63) s_wlast[tid >> 6] = en[RPT - 1];
+    if (tid == 0) s_lo = r0 > 0 ? trim(eprev) : 0;
+    __syncthreads();
+    const uint64_t lo = s_lo, hi = s_hi;
+    st[0] = tid == 0 ? lo : ((tid & 63) == 0 ? s_wlast[(tid >> 6) - 1] : left);
+#pragma unroll
+    for (int k = 1; k < RPT; k++) st[k] = en[k - 1];
+#pragma unroll
+    for (int k = 0; k < RPT; k++)
+        if (RPT * tid + k >= nr) st[k] = en[k] = 0;  // no run here
+    V* __restrict__ out = static_cast<V*>(c.out);
+    uint32_t carry = 0;
+    for (uint64_t wb = lo; wb < hi; wb += SPAN) {
+        const int wn = int(hi - wb < uint64_t(SPAN) ? hi - wb : uint64_t(SPAN));
+#pragma unroll
+        for (int k = 0; k < PER / 4; k++) reinterpret_cast<uint4*>(s_head)[tid * (PER / 4) + k] = make_uint4(0, 0, 0, 0);
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < RPT; k++)
+            if (en[k] > st[k] && st[k] >= wb && st[k] < wb + uint64_t(wn))
+                s_head[st[k] - wb] = uint32_t(RPT * tid + k) + 1;
+        __syncthreads();
+        // inclusive max-scan of s_head (thread t owns entries [PER t, PER t + PER)), seeded
+        // with the run carried over from the previous window
+        uint32_t vv[PER];
+        uint32_t m = 0;
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+            m = max(m, s_head[tid * PER + k]);
+            vv[k] = m;
+        }
+        uint32_t x = m;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d, 64);
+            if ((tid & 63) >= d) x = max(x, y);
+        }
+        if ((tid & 63) == 63) s_wmax[tid >> 6] = x;
+        __syncthreads();
+        uint32_t before = __shfl_up(x, 1, 64);
+        if ((tid & 63) == 0) before = 0;
+#pragma unroll
+        for (int w = 0; w < kBlock / 64; w++)
+            if (w < (tid >> 6)) before = max(before, s_wmax[w]);
+        before = max(before, carry);
+#pragma unroll
+        for (int k = 0; k < PER; k++) s_head[tid * PER + k] = max(vv[k], before);
+        __syncthreads();
+        for (int i = tid; i < wn; i += kBlock) nt_store(out + wb + i, s_val[s_head[i] - 1]);
+        if (tid == 0) s_carry = s_head[wn - 1];
+        __syncthreads();
+        carry = s_carry;
+    }
+}
+
+}  // namespace vxg
