@@ -214,7 +214,8 @@ vxg_status launch_k1_jobs(std::vector<K1Job>& jobs, uint32_t* err, hipStream_t s
         const GenChunk* ext;
         VXG_TRY_S(dt->table(gen.size() + n_runs, &host, &ext));
         uint64_t groups = 0;
-        bool dict_lds = true, any_vb = false;
+        bool dict_lds = true;
+        uint32_t packed_bytes = 0, dict_bytes = 0, runs_bytes = 0;
         for (size_t k = 0; k < gen.size(); k++) {
             const K1Job& jb = *gen[k];
             GenChunk& g = host[k];
@@ -224,8 +225,9 @@ vxg_status launch_k1_jobs(std::vector<K1Job>& jobs, uint32_t* err, hipStream_t s
             g.bpw = gen_bpw(jb.T, jb.W);
             g.d.first_group = groups;
             groups += (jb.d.n_blocks + g.bpw - 1) / g.bpw;
+            packed_bytes = std::max(packed_bytes, g.bpw * 128u * uint32_t(jb.W));
             if (jb.vb) {
-                any_vb = true;
+                dict_bytes = std::max(dict_bytes, uint32_t(16 * jb.d.dict_len));
                 g.vb_src = jb.vbc.src;
                 g.vb_offs = jb.vbc.offsets;
                 g.vb_offs_width = jb.vbc.offs_width;
@@ -237,6 +239,10 @@ vxg_status launch_k1_jobs(std::vector<K1Job>& jobs, uint32_t* err, hipStream_t s
                            (reinterpret_cast<uintptr_t>(jb.d.dict) & 15) == 0;
             }
         }
+        if (dict_lds)  // every plain Dict job stages its dictionary
+            for (const K1Job* jp : gen)
+                if (jp->epi == Epi::Dict && !jp->vb)
+                    dict_bytes = std::max(dict_bytes, uint32_t((jp->d.dict_len * uint64_t(jp->vw) + 15) & ~15ull));
         for (size_t k = 0; k < n_runs; k++) {  // short-run RunEnd expansions (runend_runs.hpp)
             const auto& [w, r] = (*gen_runs)[k];
             GenChunk& g = host[gen.size() + k];
@@ -245,9 +251,10 @@ vxg_status launch_k1_jobs(std::vector<K1Job>& jobs, uint32_t* err, hipStream_t s
             g.d.first_group = groups;
             g.d.n_blocks = r.n_runs;  // (unused by the body; keeps the entry self-describing)
             groups += (r.n_runs + kRunEndRunsPerGroup - 1) / kRunEndRunsPerGroup;
+            runs_bytes = std::max(runs_bytes, gen_runs_lds_bytes(w));
         }
-        VXG_TRY_S(launch_k1_generic(ext, uint32_t(gen.size() + n_runs), groups, dict_lds, any_vb, n_runs > 0, err,
-                                    s));
+        VXG_TRY_S(launch_k1_generic(ext, uint32_t(gen.size() + n_runs), groups, dict_lds, packed_bytes, dict_bytes,
+                                    runs_bytes, err, s));
     }
     return VXG_OK;
 }
@@ -1959,7 +1966,64 @@ struct vxg_plan {
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
     DevTables store;  // the recorded launches' temporaries and device chunk tables
+    // A recorded graph that is one short chain of kernels (a sharded scan after batching:
+    // FSST pre-pass -> decode -> K1g) replays as direct launches of its kernel nodes: one stream,
+    // no graph-to-graph dependency (a graph replay boundary cost ~14 us on the C5 shard).
+    std::vector<hipKernelNodeParams> direct;
 };
+
+// Direct replay of short kernel chains (VXG_PLAN_DIRECT=0 disables; at most kPlanDirectMax nodes).
+constexpr size_t kPlanDirectMax = 8;
+static bool plan_direct_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("VXG_PLAN_DIRECT");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+// The kernel nodes of `g` in order if g is a chain of <= kPlanDirectMax kernel nodes, else empty.
+static std::vector<hipKernelNodeParams> kernel_chain(hipGraph_t g) {
+    std::vector<hipKernelNodeParams> out;
+    size_t nn = 0;
+    if (hipGraphGetNodes(g, nullptr, &nn) != hipSuccess || nn == 0 || nn > kPlanDirectMax) return out;
+    std::vector<hipGraphNode_t> nodes(nn);
+    if (hipGraphGetNodes(g, nodes.data(), &nn) != hipSuccess) return out;
+    std::vector<hipGraphNode_t> dep(nn, nullptr);
+    size_t roots = 0, root = 0;
+    for (size_t i = 0; i < nn; i++) {
+        hipGraphNodeType t;
+        if (hipGraphNodeGetType(nodes[i], &t) != hipSuccess || t != hipGraphNodeTypeKernel) return out;
+        size_t nd = 0;
+        if (hipGraphNodeGetDependencies(nodes[i], nullptr, &nd) != hipSuccess || nd > 1) return out;
+        if (nd == 1 && hipGraphNodeGetDependencies(nodes[i], &dep[i], &nd) != hipSuccess) return out;
+        if (nd == 0) {
+            roots++;
+            root = i;
+        }
+    }
+    if (roots != 1) return out;
+    std::vector<size_t> order{root};
+    while (order.size() < nn) {  // the unique node depending on the last one
+        size_t next = nn, cnt = 0;
+        for (size_t i = 0; i < nn; i++)
+            if (dep[i] == nodes[order.back()]) {
+                next = i;
+                cnt++;
+            }
+        if (cnt != 1) return out;
+        order.push_back(next);
+    }
+    for (size_t i : order) {
+        hipKernelNodeParams p{};
+        if (hipGraphKernelNodeGetParams(nodes[i], &p) != hipSuccess || p.extra || !p.kernelParams || !p.func) {
+            out.clear();
+            return out;
+        }
+        out.push_back(p);
+    }
+    return out;
+}
 
 extern "C" {
 
@@ -2045,6 +2109,7 @@ vxg_status vxg_plan_create(vxg_ctx* ctx, const vxg_array* arrays, vxg_canonical*
         if (st == VXG_OK)
             st = hip_check(hipGraphInstantiate(&pl->exec, g, nullptr, nullptr, 0), "hipGraphInstantiate");
         if (st == VXG_OK) st = pl->store.upload();  // device chunk tables, once for all replays
+        if (st == VXG_OK && plan_direct_enabled()) pl->direct = kernel_chain(g);
     }
     for (hipEvent_t e : ev)
         if (e) (void)hipEventDestroy(e);
@@ -2059,6 +2124,12 @@ vxg_status vxg_plan_create(vxg_ctx* ctx, const vxg_array* arrays, vxg_canonical*
 vxg_status vxg_plan_launch(vxg_plan* plan, void* stream) {
     if (!plan || !plan->exec) return set_error(VXG_ERR_INVALID_ARGUMENT, "null plan");
     VXG_TRY(use_device(plan->ctx));
+    if (!plan->direct.empty()) {
+        for (const hipKernelNodeParams& p : plan->direct)
+            VXG_TRY(hip_check(hipLaunchKernel(p.func, p.gridDim, p.blockDim, p.kernelParams, p.sharedMemBytes, S(stream)),
+                              "plan kernel"));
+        return VXG_OK;
+    }
     return hip_check(hipGraphLaunch(plan->exec, S(stream)), "hipGraphLaunch");
 }
 

@@ -50,7 +50,8 @@ __device__ __forceinline__ uint4 vb_view(const uint8_t* __restrict__ heap, uint6
 }
 
 template <int T, Epi EPI, int VW, bool VB = false>
-__device__ __forceinline__ void gen_body(const GenChunk& gc, uint64_t g, uint8_t* lds, bool dict_lds, uint32_t* err) {
+__device__ __forceinline__ void gen_body(const GenChunk& gc, uint64_t g, uint8_t* lds, uint32_t dict_off, bool dict_lds,
+                                         uint32_t* err) {
     using E = typename Fl<T>::E;
     using O = typename EpiOut<T, EPI, VW>::type;
     constexpr uint32_t LANES = 1024 / T;
@@ -78,7 +79,7 @@ __device__ __forceinline__ void gen_body(const GenChunk& gc, uint64_t g, uint8_t
         const uint64_t b1 = (lg + 1) * per < gc.vb_bytes ? (lg + 1) * per : gc.vb_bytes;
         for (uint64_t b = lg * per + tid; b < b1; b += kGenThreads) gc.vb_dst[b] = gc.vb_src[b];
         // the dictionary's views, in LDS
-        uint4* const s_views = reinterpret_cast<uint4*>(lds + kGenPackedLds);
+        uint4* const s_views = reinterpret_cast<uint4*>(lds + dict_off);
         for (uint32_t k = tid; k < c.dict_len; k += kGenThreads) {
             const uint64_t a = vb_offset(gc.vb_offs, gc.vb_offs_width, k);
             const uint64_t e = vb_offset(gc.vb_offs, gc.vb_offs_width, k + 1);
@@ -87,7 +88,7 @@ __device__ __forceinline__ void gen_body(const GenChunk& gc, uint64_t g, uint8_t
         ep.dict = s_views;
     } else if constexpr (EPI == Epi::Dict) {
         if (dict_lds) {
-            uint8_t* const s_dict = lds + kGenPackedLds;
+            uint8_t* const s_dict = lds + dict_off;
             const uint32_t n16 = uint32_t((c.dict_len * VW + 15) / 16);
             for (uint32_t q = tid; q < n16; q += kGenThreads)
                 reinterpret_cast<uint4*>(s_dict)[q] = static_cast<const uint4*>(c.dict)[q];
@@ -127,20 +128,21 @@ __device__ __forceinline__ void gen_body(const GenChunk& gc, uint64_t g, uint8_t
 constexpr int kGenKinds = 43;
 
 template <int K>
-__device__ __forceinline__ void gen_dispatch_one(const GenChunk& gc, uint64_t g, uint8_t* lds, bool dl, uint32_t* err) {
+__device__ __forceinline__ void gen_dispatch_one(const GenChunk& gc, uint64_t g, uint8_t* lds, uint32_t doff, bool dl,
+                                                 uint32_t* err) {
     constexpr int Ts[4] = {8, 16, 32, 64};
     constexpr int VWs[5] = {1, 2, 4, 8, 16};
     if constexpr (K < 12) {
         constexpr Epi e = K % 3 == 0 ? Epi::Plain : (K % 3 == 1 ? Epi::For : Epi::ForZigZag);
-        gen_body<Ts[K / 3], e, 0>(gc, g, lds, dl, err);
+        gen_body<Ts[K / 3], e, 0>(gc, g, lds, doff, dl, err);
     } else if constexpr (K == 12) {
-        gen_body<32, Epi::AlpF32, 0>(gc, g, lds, dl, err);
+        gen_body<32, Epi::AlpF32, 0>(gc, g, lds, doff, dl, err);
     } else if constexpr (K == 13) {
-        gen_body<64, Epi::AlpF64, 0>(gc, g, lds, dl, err);
+        gen_body<64, Epi::AlpF64, 0>(gc, g, lds, doff, dl, err);
     } else if constexpr (K < 34) {
-        gen_body<Ts[(K - 14) / 5], Epi::Dict, VWs[(K - 14) % 5]>(gc, g, lds, dl, err);
+        gen_body<Ts[(K - 14) / 5], Epi::Dict, VWs[(K - 14) % 5]>(gc, g, lds, doff, dl, err);
     } else if constexpr (K < 38) {
-        gen_body<Ts[K - 34], Epi::Dict, 16, true>(gc, g, lds, dl, err);
+        gen_body<Ts[K - 34], Epi::Dict, 16, true>(gc, g, lds, doff, dl, err);
     } else {
         using V = std::conditional_t<
             VWs[K - 38] == 1, uint8_t,
@@ -154,17 +156,17 @@ __device__ __forceinline__ void gen_dispatch_one(const GenChunk& gc, uint64_t g,
 }
 
 template <int... Ks>
-__device__ __forceinline__ void gen_dispatch(int kind, const GenChunk& gc, uint64_t g, uint8_t* lds, bool dl, uint32_t* err,
-                                             std::integer_sequence<int, Ks...>) {
-    ((kind == Ks ? gen_dispatch_one<Ks>(gc, g, lds, dl, err) : void()), ...);
+__device__ __forceinline__ void gen_dispatch(int kind, const GenChunk& gc, uint64_t g, uint8_t* lds, uint32_t doff, bool dl,
+                                             uint32_t* err, std::integer_sequence<int, Ks...>) {
+    ((kind == Ks ? gen_dispatch_one<Ks>(gc, g, lds, doff, dl, err) : void()), ...);
 }
 
 __global__ __launch_bounds__(kGenThreads) void k1_generic_kernel(const GenChunk* __restrict__ tab, uint32_t n,
-                                                                 bool dict_lds, uint32_t* err) {
+                                                                 uint32_t dict_off, bool dict_lds, uint32_t* err) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const uint64_t g = blockIdx.x;
     const GenChunk& gc = tab[ext_chunk_index(tab, n, g, [](const GenChunk& d) { return d.d.first_group; })];
-    gen_dispatch(int(gc.kind), gc, g, lds, dict_lds, err, std::make_integer_sequence<int, kGenKinds>{});
+    gen_dispatch(int(gc.kind), gc, g, lds, dict_off, dict_lds, err, std::make_integer_sequence<int, kGenKinds>{});
 }
 
 }  // namespace
@@ -205,14 +207,29 @@ uint32_t gen_bpw(int T, int W) {
     return b > 4 ? 4 : (b < 1 ? 1 : b);
 }
 
-vxg_status launch_k1_generic(const GenChunk* ext, uint32_t n, uint64_t groups, bool dict_lds, bool any_vb,
-                             bool any_runs, uint32_t* err, hipStream_t s) {
+uint32_t gen_runs_lds_bytes(int value_width) {
+    switch (value_width) {
+    case 1: return uint32_t(runs_lds_bytes<uint8_t>());
+    case 2: return uint32_t(runs_lds_bytes<uint16_t>());
+    case 4: return uint32_t(runs_lds_bytes<uint32_t>());
+    case 8: return uint32_t(runs_lds_bytes<uint64_t>());
+    default: return uint32_t(runs_lds_bytes<uint4>());
+    }
+}
+
+vxg_status launch_k1_generic(const GenChunk* ext, uint32_t n, uint64_t groups, bool dict_lds, uint32_t packed_bytes,
+                             uint32_t dict_bytes, uint32_t runs_bytes, uint32_t* err, hipStream_t s) {
     static_assert(kGenVarBinDictMax * 16 <= uint64_t(kDictLdsBytes), "VarBin views must fit the dictionary stage");
     if (n == 0 || groups == 0) return VXG_OK;
     if (groups > 0xFFFFFFFFull) return set_error(VXG_ERR_INVALID_ARGUMENT, "array too long for one launch");
-    size_t shm = kGenPackedLds + (dict_lds || any_vb ? size_t(kDictLdsBytes) : 0);
-    if (any_runs) shm = std::max(shm, runs_lds_bytes<uint4>());
-    hipLaunchKernelGGL(k1_generic_kernel, dim3(unsigned(groups)), dim3(kGenThreads), shm, s, ext, n, dict_lds, err);
+    if (packed_bytes > kGenPackedLds || dict_bytes > uint32_t(kDictLdsBytes))
+        return set_error(VXG_ERR_INVALID_ARGUMENT, "K1g stage sizes");
+    // LDS = the largest packed stage + the largest dictionary stage, or a RunEnd expansion's
+    // (sized by the launch's jobs, so small jobs keep residency high)
+    const uint32_t dict_off = (packed_bytes + 15) & ~15u;
+    const size_t shm = std::max<size_t>({size_t(dict_off) + dict_bytes, size_t(runs_bytes), 16});
+    hipLaunchKernelGGL(k1_generic_kernel, dim3(unsigned(groups)), dim3(kGenThreads), shm, s, ext, n, dict_off, dict_lds,
+                       err);
     return hip_check(hipGetLastError(), "k1_generic_kernel launch");
 }
 

@@ -42,10 +42,13 @@ int gen_runs_kind(int value_width);
 constexpr uint64_t kGenVarBinDictMax = 1024;
 // Blocks per workgroup of a job (its packed words staged in <= 16 KiB of LDS).
 uint32_t gen_bpw(int T, int W);
-// One launch over a device table of n jobs (first_group filled in); `dict_lds` = every Dict job's
-// dictionary fits the LDS stage (16 KiB, 16-byte aligned); `any_vb` = some job builds VarBin
-// dictionary views (their stage is always allocated).
-vxg_status launch_k1_generic(const GenChunk* ext, uint32_t n, uint64_t groups, bool dict_lds, bool any_vb,
-                             bool any_runs, uint32_t* err, hipStream_t s);
+// LDS a short-run RunEnd expansion of `value_width`-byte values needs.
+uint32_t gen_runs_lds_bytes(int value_width);
+// One launch over a device table of n jobs (first_group filled in).  `dict_lds` = every Dict
+// job's dictionary fits the LDS stage (16 KiB, 16-byte aligned); packed_bytes / dict_bytes /
+// runs_bytes = the largest packed stage (bpw * 128 * W), dictionary stage (staged dictionaries,
+// VarBin views) and RunEnd expansion LDS of the launch's jobs.
+vxg_status launch_k1_generic(const GenChunk* ext, uint32_t n, uint64_t groups, bool dict_lds, uint32_t packed_bytes,
+                             uint32_t dict_bytes, uint32_t runs_bytes, uint32_t* err, hipStream_t s);
 
 }  // namespace vxg
