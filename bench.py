@@ -660,8 +660,9 @@ def main():
             e2e = run_e2e(arr, info, ctx) if args.e2e and not isinstance(arr, list) else None
             # one-array steps are one or two back-to-back kernel launches: direct calls overlap
             # the next submission with the running kernel (a graph replay measured 2-6 us slower
-            # per step on C1-C4); multi-array steps replay a graph
-            wl = Workload(arr, info, ctx, copies[key], graph=isinstance(arr, list) and not args.no_graph)
+            # per step on C1, C2, C4); multi-array steps and C3's 256-chunk table (one launch over
+            # a device chunk table instead of 8 kernel-argument tables) replay a plan
+            wl = Workload(arr, info, ctx, copies[key], graph=(isinstance(arr, list) or key == "c3") and not args.no_graph)
         del arr
         if rank == 0:
             log(f"[bench] {info['name']}: built in {time.perf_counter() - t0:.1f}s; timing...")
