@@ -1972,8 +1972,15 @@ struct vxg_plan {
     std::vector<hipKernelNodeParams> direct;
 };
 
-// Direct replay of short kernel chains (VXG_PLAN_DIRECT=0 disables; at most kPlanDirectMax nodes).
-constexpr size_t kPlanDirectMax = 8;
+// Direct replay of short kernel chains (VXG_PLAN_DIRECT=0 disables; at most
+// VXG_PLAN_DIRECT_MAX nodes, default 8).
+static size_t plan_direct_max() {
+    static const size_t v = [] {
+        const char* e = std::getenv("VXG_PLAN_DIRECT_MAX");
+        return e ? size_t(std::strtoull(e, nullptr, 10)) : size_t(8);
+    }();
+    return v;
+}
 static bool plan_direct_enabled() {
     static const bool on = [] {
         const char* e = std::getenv("VXG_PLAN_DIRECT");
@@ -1982,18 +1989,21 @@ static bool plan_direct_enabled() {
     return on;
 }
 
-// The kernel nodes of `g` in order if g is a chain of <= kPlanDirectMax kernel nodes, else empty.
+// The kernel nodes of `g` in order if g is a chain of <= plan_direct_max() kernel nodes, else empty.
 static std::vector<hipKernelNodeParams> kernel_chain(hipGraph_t g) {
     std::vector<hipKernelNodeParams> out;
     size_t nn = 0;
-    if (hipGraphGetNodes(g, nullptr, &nn) != hipSuccess || nn == 0 || nn > kPlanDirectMax) return out;
+    if (hipGraphGetNodes(g, nullptr, &nn) != hipSuccess || nn == 0 || nn > plan_direct_max()) return out;
     std::vector<hipGraphNode_t> nodes(nn);
     if (hipGraphGetNodes(g, nodes.data(), &nn) != hipSuccess) return out;
     std::vector<hipGraphNode_t> dep(nn, nullptr);
     size_t roots = 0, root = 0;
     for (size_t i = 0; i < nn; i++) {
         hipGraphNodeType t;
-        if (hipGraphNodeGetType(nodes[i], &t) != hipSuccess || t != hipGraphNodeTypeKernel) return out;
+        if (hipGraphNodeGetType(nodes[i], &t) != hipSuccess || t != hipGraphNodeTypeKernel) {
+            if (std::getenv("VXG_PLAN_DEBUG")) std::fprintf(stderr, "plan: node %zu of %zu has type %d\n", i, nn, int(t));
+            return out;
+        }
         size_t nd = 0;
         if (hipGraphNodeGetDependencies(nodes[i], nullptr, &nd) != hipSuccess || nd > 1) return out;
         if (nd == 1 && hipGraphNodeGetDependencies(nodes[i], &dep[i], &nd) != hipSuccess) return out;
