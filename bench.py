@@ -702,7 +702,7 @@ def main():
             "vs_baseline": None,
             "dtype": info["dtype"],
             "data": "synthetic (seeded; inputs resident in HBM, rotated across copies)",
-            "launch": "headline: direct vxg_canonicalize per step; multi-array steps (C5): vxg_plan HIP-graph replay"
+            "launch": "headline (C1), C2, C4: direct vxg_canonicalize per step; C3 (256-chunk table) and C5 (16 columns): vxg_plan replay (HIP graph, or direct launches of a short kernel chain)"
                       + (" disabled (--no-graph)" if args.no_graph else ""),
             "config": {"workload": f"{info['name']}: {info['encoding']}, {info['values']} values per GPU, "
                                    f"one chunk per GPU", "values_per_gpu": info["values"],
