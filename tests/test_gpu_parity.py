@@ -716,6 +716,26 @@ def test_plan_k1g_every_kind(ctx):
     plan.close()
 
 
+def test_plan_mixed_large_and_small_arrays(ctx):
+    """A plan with a large array (canonical output > the 16 MiB batching threshold: its own graph
+    branch, per-kernel launches) next to small ones (batched onto one more branch, K1g): both
+    paths in one graph, every replay equal to the oracle."""
+    import torch
+    rng = np.random.default_rng(91)
+    big = rng.integers(0, 1 << 13, 5_300_000, dtype=np.uint64).astype(np.uint32)  # 21 MB of u32
+    big_arr = A.chunked([E.encode_bitpacked(big[i:i + 1 << 20], bit_width=13, allow_patches=False)
+                         for i in range(0, big.size, 1 << 20)])
+    cols = _k1g_columns(rng)[:6]
+    arrs = [big_arr] + [c for c, _ in cols]
+    plan = V.Plan([a.to(torch.device("cuda", 0)) for a in arrs], ctx)
+    for _ in range(2):
+        res = plan.launch(sync=True)
+        assert res[0].numpy().tobytes() == big.tobytes()
+        for (a, exp), r in zip(cols, res[1:]):
+            assert r.numpy().tobytes() == exp.tobytes()
+    plan.close()
+
+
 # ------------------------------------------------------------------ edge cases: empty inputs
 def test_empty_arrays_every_encoding(ctx):
     """len = 0 through every encoding and container (the reference canonicalizes empty arrays
