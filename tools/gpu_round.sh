@@ -16,6 +16,8 @@ rc=$?; echo "pytest exit $rc"; tail -3 "$O/pytest_gpu_$TAG.log"
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke_$TAG.log" 2>&1 && \
 timeout -k 10 400 python -u bench.py > "$O/bench_$TAG.json" 2> "$O/bench_$TAG.err" && cat "$O/bench_$TAG.json" && \
 timeout -k 10 300 python -u bench.py --workloads c3,c5 --simulate-world 8 --no-cpu-baseline > "$O/bench_sim8_$TAG.json" 2> "$O/bench_sim8_$TAG.err" && \
+timeout -k 10 200 python -u tools/plan_probe.py 1 > "$O/plan_probe_$TAG.txt" 2>&1 && \
+timeout -k 10 200 python -u tools/plan_probe.py 8 >> "$O/plan_probe_$TAG.txt" 2>&1 && \
 cd /tmp && export TMPDIR=/tmp && \
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_$TAG" -o run -- python "$ROOTDIR/bench.py" --steps 20 --warmup 5 --no-cpu-baseline > "$O/prof_bench_$TAG.json" 2> "$O/prof_bench_$TAG.err" && \
 timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$O/pmc_fetch_$TAG" -o run -- python "$ROOTDIR/bench.py" --workloads c1,c2,c3,c4 --steps 5 --warmup 1 --no-cpu-baseline > /dev/null 2> "$O/pmc_fetch_$TAG.err" && \
