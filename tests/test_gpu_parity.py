@@ -723,7 +723,7 @@ def test_plan_mixed_large_and_small_arrays(ctx):
     import torch
     rng = np.random.default_rng(91)
     big = rng.integers(0, 1 << 13, 5_300_000, dtype=np.uint64).astype(np.uint32)  # 21 MB of u32
-    big_arr = A.chunked([E.encode_bitpacked(big[i:i + 1 << 20], bit_width=13, allow_patches=False)
+    big_arr = A.chunked([E.encode_bitpacked(big[i:i + (1 << 20)], bit_width=13, allow_patches=False)
                          for i in range(0, big.size, 1 << 20)])
     cols = _k1g_columns(rng)[:6]
     arrs = [big_arr] + [c for c, _ in cols]

@@ -33,7 +33,7 @@ constexpr int kRunsSpan = 4096;  // outputs per expansion window
 // LDS of one workgroup: run heads (kRunsSpan u32), run values (kRunEndRunsPerGroup V), scratch
 template <typename V>
 constexpr size_t runs_lds_bytes() {
-    return kRunsSpan * 4 + kRunEndRunsPerGroup * sizeof(V) + 128;
+    return kRunsSpan * 2 + kRunEndRunsPerGroup * sizeof(V) + 128;
 }
 
 // Workgroup g of the launch expands its 1024 runs of chunk c (c.first_group = its first
@@ -42,9 +42,12 @@ template <typename V>
 __device__ __forceinline__ void runend_runs_body(const RunEndChunk& c, uint64_t g, uint32_t* err, uint8_t* lds) {
     constexpr int kBlock = kRunsThreads;
     constexpr int SPAN = kRunsSpan, PER = SPAN / kBlock, RPG = int(kRunEndRunsPerGroup), RPT = RPG / kBlock;
-    uint32_t* const s_head = reinterpret_cast<uint32_t*>(lds);
-    V* const s_val = reinterpret_cast<V*>(lds + SPAN * 4);
-    uint8_t* const misc = lds + SPAN * 4 + RPG * sizeof(V);
+    // run heads as 16-bit run indices (<= 1024 runs per workgroup): 8 KiB instead of 16, so the
+    // LDS of a u64 expansion (16.6 KiB) allows 8 workgroups per CU instead of 6
+    static_assert(RPG < 65536, "run index must fit 16 bits");
+    uint16_t* const s_head = reinterpret_cast<uint16_t*>(lds);
+    V* const s_val = reinterpret_cast<V*>(lds + SPAN * 2);
+    uint8_t* const misc = lds + SPAN * 2 + RPG * sizeof(V);
     uint64_t* const s_wlast = reinterpret_cast<uint64_t*>(misc);           // kBlock / 64
     uint64_t& s_lo = reinterpret_cast<uint64_t*>(misc)[4];
     uint64_t& s_hi = reinterpret_cast<uint64_t*>(misc)[5];
@@ -96,12 +99,12 @@ __device__ __forceinline__ void runend_runs_body(const RunEndChunk& c, uint64_t 
     for (uint64_t wb = lo; wb < hi; wb += SPAN) {
         const int wn = int(hi - wb < uint64_t(SPAN) ? hi - wb : uint64_t(SPAN));
 #pragma unroll
-        for (int k = 0; k < PER / 4; k++) reinterpret_cast<uint4*>(s_head)[tid * (PER / 4) + k] = make_uint4(0, 0, 0, 0);
+        for (int k = 0; k < PER / 8; k++) reinterpret_cast<uint4*>(s_head)[tid * (PER / 8) + k] = make_uint4(0, 0, 0, 0);
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < RPT; k++)
             if (en[k] > st[k] && st[k] >= wb && st[k] < wb + uint64_t(wn))
-                s_head[st[k] - wb] = uint32_t(RPT * tid + k) + 1;
+                s_head[st[k] - wb] = uint16_t(RPT * tid + k + 1);
         __syncthreads();
         // inclusive max-scan of s_head (thread t owns entries [PER t, PER t + PER)), seeded
         // with the run carried over from the previous window
@@ -109,7 +112,7 @@ __device__ __forceinline__ void runend_runs_body(const RunEndChunk& c, uint64_t 
         uint32_t m = 0;
 #pragma unroll
         for (int k = 0; k < PER; k++) {
-            m = max(m, s_head[tid * PER + k]);
+            m = max(m, uint32_t(s_head[tid * PER + k]));
             vv[k] = m;
         }
         uint32_t x = m;
@@ -127,7 +130,7 @@ __device__ __forceinline__ void runend_runs_body(const RunEndChunk& c, uint64_t 
             if (w < (tid >> 6)) before = max(before, s_wmax[w]);
         before = max(before, carry);
 #pragma unroll
-        for (int k = 0; k < PER; k++) s_head[tid * PER + k] = max(vv[k], before);
+        for (int k = 0; k < PER; k++) s_head[tid * PER + k] = uint16_t(max(vv[k], before));
         __syncthreads();
         for (int i = tid; i < wn; i += kBlock) nt_store(out + wb + i, s_val[s_head[i] - 1]);
         if (tid == 0) s_carry = s_head[wn - 1];
