@@ -316,7 +316,8 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
                                                      const int64_t* __restrict__ tile_prefix_all,
                                                      const int64_t* __restrict__ block_totals_all,
                                                      const int64_t* __restrict__ tile_code_all,
-                                                     uint32_t* __restrict__ err) {
+                                                     uint32_t* __restrict__ err,
+                                                     const uint32_t* __restrict__ wg_chunk) {
     __shared__ uint64_t s_sym[256];
     __shared__ uint8_t s_len[256];
     __shared__ int ws_a[kTile / 64], ws_b[kTile / 64];
@@ -329,7 +330,9 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
     uint8_t* const s_heap = reinterpret_cast<uint8_t*>(s_heap32);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 
-    const FsstChunk& ch = fsst_chunk_of<false, EXT>(tab, blockIdx.x);
+    // a recorded plan's device table: the workgroup's chunk from the plan's per-workgroup map
+    // (one scalar load) instead of the wave-wide count over the table
+    const FsstChunk& ch = EXT ? tab.ext[wg_chunk[blockIdx.x]] : fsst_chunk_of<false, EXT>(tab, blockIdx.x);
     const uint64_t* __restrict__ symbols = ch.symbols;
     const uint8_t* __restrict__ sym_lens = ch.sym_lens;
     const unsigned n_symbols = ch.n_symbols;
@@ -718,6 +721,17 @@ vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint
             scans += (nt + kScanTiles - 1) / kScanTiles;
         }
         if (tab.n) {
+            const uint32_t* wg_chunk = nullptr;  // device table launches: chunk of every decode workgroup
+            if (tab.ext) {
+                uint32_t* host_map;
+                const vxg_status st = dt->table(tiles, &host_map, &wg_chunk);
+                if (st != VXG_OK) return st;
+                for (uint32_t k = 0; k < tab.n; k++) {
+                    const FsstChunk& c = cs[k];
+                    const uint64_t nt = (c.n + kTile - 1) / kTile;
+                    for (uint64_t t = 0; t < nt; t++) host_map[c.first_tile + t] = k;
+                }
+            }
             int64_t* tp = tiles_all;
             int64_t* bt = tiles_all + tiles;
             int64_t* tc = bt + scans;
@@ -737,7 +751,7 @@ vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint
                             hipLaunchKernelGGL((fsst_tile_scan<LA, X>), dim3(unsigned(scans)), dim3(kTile), 0, s, tab,
                                                tp, bt, tc);
                         hipLaunchKernelGGL((fsst_decode<OA, LA, X>), dim3(unsigned(tiles)), dim3(kTile), 0, s, tab,
-                                           tiles, tp, bt, tc, err);
+                                           tiles, tp, bt, tc, err, wg_chunk);
                     };
                     if (tab.ext) go(std::true_type{});
                     else go(std::false_type{});
