@@ -98,14 +98,24 @@ struct DevTables {
 // Index of the entry of a device-resident table (sorted by its first workgroup, entry 0 first
 // = 0) that covers workgroup g: every lane of the wave compares one entry per round (all loads
 // in flight together) and the ballot counts give the index -- wave-uniform, no dependent chain.
+// Four entries per lane per round, all four loads issued before any ballot: a table of up to 256
+// entries (C5's 92-chunk columns) costs one memory round trip, not one per 64 entries.
 template <class E, class Key>
 __device__ __forceinline__ uint32_t ext_chunk_index(const E* __restrict__ ext, uint32_t n, uint64_t g, Key key) {
     const uint32_t lane = threadIdx.x & 63u;
     uint32_t cnt = 0;
-    for (uint32_t base = 0; base < n; base += 64) {
-        const uint32_t i = base + lane;
-        const bool le = i < n && key(ext[i]) <= g;
-        cnt += uint32_t(__popcll(__ballot(le)));
+    for (uint32_t base = 0; base < n; base += 256) {
+        uint64_t kv[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t i = base + 64u * uint32_t(k) + lane;
+            kv[k] = uint64_t(key(ext[i < n ? i : n - 1]));  // clamped: no per-lane branch
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const bool le = base + 64u * uint32_t(k) + lane < n && kv[k] <= g;
+            cnt += uint32_t(__popcll(__ballot(le)));
+        }
     }
     return cnt ? cnt - 1 : 0;
 }
