@@ -717,9 +717,9 @@ def test_plan_k1g_every_kind(ctx):
 
 
 def test_plan_mixed_large_and_small_arrays(ctx):
-    """A plan with a large array (canonical output > the 16 MiB batching threshold: its own graph
-    branch, per-kernel launches) next to small ones (batched onto one more branch, K1g): both
-    paths in one graph, every replay equal to the oracle."""
+    """A plan with a 21 MB chunked array (22 K1 chunks) next to small columns of every K1g body:
+    batched together (K1 launch groups for the large group, one K1g launch for the rest), every
+    replay equal to the oracle."""
     import torch
     rng = np.random.default_rng(91)
     big = rng.integers(0, 1 << 13, 5_300_000, dtype=np.uint64).astype(np.uint32)  # 21 MB of u32

@@ -1944,15 +1944,22 @@ static uint32_t plan_branches_env() {
     return nb;
 }
 
-// Deferred launches of a plan's SMALL arrays (canonical output <= VXG_PLAN_BATCH_MAX_BYTES,
-// default 16 MiB; 0 disables) batched onto one branch.  A sharded scan's columns are all small
-// (C5 at 8 GPUs: 3-12 MB each, 0.120 -> 0.085-0.094 ms/step); a whole-table scan's columns keep
-// their own balanced branches (C5 at 1 GPU: batching them all onto one branch cost 6 %).
+// Plan batching (PlanBatch + K1g on one branch) is all-or-nothing: it is used when every array's
+// canonical output is <= VXG_PLAN_BATCH_MAX_BYTES (default 64 MiB; 0 disables) and the plan's total
+// is <= VXG_PLAN_BATCH_TOTAL_BYTES (default 400 MB).  C5 per GPU (tools/gpu_thresh.sh): 8-GPU
+// shard (140 MB) 0.120 -> 0.061 ms/step batched; 4-GPU shard (275 MB) 0.131 -> 0.106; 2-GPU
+// shard (550 MB) 0.179 unbatched vs 0.200 batched; mixing batched and unbatched arrays in one
+// plan measured slower than either.
+static uint64_t env_bytes(const char* name, uint64_t dflt) {
+    const char* e = std::getenv(name);
+    return e ? uint64_t(std::strtoull(e, nullptr, 10)) : dflt;
+}
 static uint64_t plan_batch_max_bytes() {
-    static const uint64_t v = [] {
-        const char* e = std::getenv("VXG_PLAN_BATCH_MAX_BYTES");
-        return e ? uint64_t(std::strtoull(e, nullptr, 10)) : uint64_t(16) << 20;
-    }();
+    static const uint64_t v = env_bytes("VXG_PLAN_BATCH_MAX_BYTES", uint64_t(64) << 20);
+    return v;
+}
+static uint64_t plan_batch_total_bytes() {
+    static const uint64_t v = env_bytes("VXG_PLAN_BATCH_TOTAL_BYTES", uint64_t(400) * 1000 * 1000);
     return v;
 }
 
@@ -2058,16 +2065,18 @@ vxg_status vxg_plan_create(vxg_ctx* ctx, const vxg_array* arrays, vxg_canonical*
     // The small arrays' deferrable launches (PlanBatch: K1 decodes, RunEnd expansions,
     // dictionary views of chunked columns) go to one more branch, recorded after all arrays were
     // visited.
-    bool batching = false, all_small = n > 0;
+    uint64_t total = 0;
+    bool all_small = n > 0;
     for (uint32_t i = 0; i < n; i++) {
-        const bool small = canonical_out_bytes(arrays[i]) <= plan_batch_max_bytes();
-        batching = batching || small;
-        all_small = all_small && small;
+        const uint64_t b = canonical_out_bytes(arrays[i]);
+        total += b;
+        all_small = all_small && b <= plan_batch_max_bytes();
     }
-    // Branches: 2 by default; ONE when every array is small (a sharded scan): each cross-branch
+    const bool batching = all_small && total <= plan_batch_total_bytes();
+    // Branches: 2 by default; ONE when the plan is batched (a sharded scan): each cross-branch
     // edge of a graph costs the replay several microseconds of queue synchronisation, more than
     // the small kernels gain from overlapping (C5 8-GPU shard: 82 -> 68 us per replay).
-    const uint32_t kPlanBranches = plan_branches_env() ? plan_branches_env() : (all_small ? 1u : 2u);
+    const uint32_t kPlanBranches = plan_branches_env() ? plan_branches_env() : (batching ? 1u : 2u);
     // (one branch requested: the batch follows the arrays on that branch -- a single-stream graph)
     const bool own = batching && kPlanBranches > 1;
     const uint32_t nb = (n < kPlanBranches ? (n ? n : 1) : kPlanBranches) + (own ? 1 : 0);
@@ -2103,8 +2112,7 @@ vxg_status vxg_plan_create(vxg_ctx* ctx, const vxg_array* arrays, vxg_canonical*
             const uint32_t i = order[k];
             const uint32_t b = uint32_t(std::min_element(load.begin(), load.end()) - load.begin());
             load[b] += cost[i];
-            const bool small = batching && canonical_out_bytes(arrays[i]) <= plan_batch_max_bytes();
-            Planner p(ctx, br[b], &pl->store, small ? &batch : nullptr);
+            Planner p(ctx, br[b], &pl->store, batching ? &batch : nullptr);
             st = p.canonical(arrays[i], outs[i]);
         }
         if (batching && st == VXG_OK) st = flush_plan_batch(batch, ctx->c.err_word, br[nb - 1], &pl->store);
