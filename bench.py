@@ -61,16 +61,21 @@ def c2_values(rng, n):
     return vals
 
 
-def c3_chunk(c: int):
-    """Chunk c of the C3 table (seeded by c so every rank agrees without communicating):
-    Dict(codes = BitPacked u64 W=10, values = 1024 random u64), Zipf(1.1) codes."""
-    import vortex_amd.arrays as A
-    import vortex_amd.encode as E
+def c3_chunk_plain(c: int):
+    """Plain data of chunk c of the C3 table (seeded by c so every rank agrees without
+    communicating): 1024 random u64 dictionary values and Zipf(1.1) codes."""
     r = np.random.default_rng(1000 + c)
     dv = r.integers(0, 2 ** 63, 1024, dtype=np.uint64)
     codes = (r.zipf(1.1, C3_CHUNK_VALUES) - 1) % 1024
-    return A.dict_array(A.primitive(dv), A.bitpacked(E.bitpack_buffer(codes.astype(np.uint64), 10), "u64", 10,
-                                                     C3_CHUNK_VALUES))
+    return dv, codes.astype(np.uint64)
+
+
+def c3_chunk(c: int, plain=None):
+    """Chunk c of the C3 table: Dict(codes = BitPacked u64 W=10, values = Primitive u64[1024])."""
+    import vortex_amd.arrays as A
+    import vortex_amd.encode as E
+    dv, codes = c3_chunk_plain(c) if plain is None else plain
+    return A.dict_array(A.primitive(dv), A.bitpacked(E.bitpack_buffer(codes, 10), "u64", 10, C3_CHUNK_VALUES))
 
 
 def c3_shard(world: int, rank: int) -> range:
@@ -111,22 +116,104 @@ def c4_heap(rng, n):
     return stream, offs
 
 
+# ------------------------------------------------------------------------------ output checks
+# Every timed workload's full-size output is checked after the timed region (never inside it):
+# against the generator's plain values (C1, C2, C3: xxh3 of the exact bytes; C4: the exact views
+# and heap, built here in numpy from the plain strings; C5: every numeric column's bytes and
+# every string row's logical value) - no oracle involved.  Rotated copies must produce the same
+# output bytes as the checked copy.
+def _xxh(*bufs) -> int:
+    import xxhash
+    h = xxhash.xxh3_64()
+    for b in bufs:
+        h.update(memoryview(np.ascontiguousarray(b)).cast("B"))
+    return h.intdigest()
+
+
+def expected_views(heap: np.ndarray, offs: np.ndarray, bidx: int = 0) -> np.ndarray:
+    """arrow-array 53.2 make_view over one data buffer: len <= 12 inline and
+    zero padded, else {len, 4-byte prefix, buffer_index, offset} -> u8[n, 16]."""
+    n = offs.size - 1
+    lens = np.diff(offs).astype(np.uint32)
+    starts = offs[:-1].astype(np.int64)
+    pad = np.concatenate([heap, np.zeros(16, np.uint8)])
+    first = pad[starts[:, None] + np.arange(12)[None, :]]
+    first[np.arange(12)[None, :] >= lens[:, None]] = 0
+    v = np.zeros((n, 16), np.uint8)
+    v[:, :4] = lens.view(np.uint8).reshape(n, 4)
+    inl = lens <= 12
+    v[inl, 4:16] = first[inl]
+    ni = ~inl
+    v[ni, 4:8] = first[ni, :4]
+    v[ni, 8:12] = np.frombuffer(np.uint32(bidx).tobytes(), np.uint8)
+    v[ni, 12:16] = starts[ni].astype(np.uint32).view(np.uint8).reshape(-1, 4)
+    return v
+
+
+def strings_of(views: np.ndarray, data: np.ndarray, bufs, width: int):
+    """Logical strings of canonical views (u8[n, 16]) over the data buffers (offset, len) in
+    `data`: (lengths, u8[n, width] zero padded)."""
+    n = views.shape[0]
+    lens = views[:, :4].copy().view(np.uint32).reshape(n).astype(np.int64)
+    if lens.size and lens.max() > width:
+        raise AssertionError(f"string longer than {width}")
+    out = np.zeros((n, width), np.uint8)
+    inl = lens <= 12
+    out[inl, : min(12, width)] = views[inl, 4: 4 + min(12, width)]
+    ni = np.nonzero(~inl)[0]
+    if ni.size:
+        bidx = views[ni, 8:12].copy().view(np.uint32).reshape(-1).astype(np.int64)
+        off = views[ni, 12:16].copy().view(np.uint32).reshape(-1).astype(np.int64)
+        base = np.array([o for o, _ in bufs], np.int64)[bidx]
+        blen = np.array([n_ for _, n_ in bufs], np.int64)[bidx]
+        if np.any(off + lens[ni] > blen):
+            raise AssertionError("view points past its data buffer")
+        idx = np.minimum(base[:, None] + off[:, None] + np.arange(width)[None, :], data.size - 1)
+        g = data[idx]
+        g[np.arange(width)[None, :] >= lens[ni][:, None]] = 0
+        out[ni] = g
+        if not np.array_equal(views[ni, 4:8], g[:, :4]):
+            raise AssertionError("view prefix differs from its bytes")
+    out[np.arange(width)[None, :] >= lens[:, None]] = 0
+    return lens, out
+
+
+def plain_strings(strs, width: int):
+    a = np.array(strs, dtype=f"S{width}")
+    return np.char.str_len(a).astype(np.int64), np.frombuffer(a.tobytes(), np.uint8).reshape(len(strs), width)
+
+
+def _host(t) -> np.ndarray:
+    return t.cpu().numpy() if t is not None else None
+
+
+def expect_hash(digest: int, what: str):
+    def check(results):
+        got = _xxh(_host(results[0].values))
+        if got != digest:
+            raise AssertionError(f"{what}: decoded bytes differ from the plain values")
+    return check
+
+
 def make_c1(rng, world, rank):
     """C1: 64 Mi u32 uniform in [0,128) -> BitPacked W=7, no patches (one chunk per GPU)."""
     import vortex_amd.encode as E
     vals = rng.integers(0, 128, 64 << 20, dtype=np.uint32)
     return E.encode_bitpacked(vals, bit_width=7, allow_patches=False), dict(
         name="C1", encoding="fastlanes.bitpacked u32 W=7", values=vals.size,
-        read_bytes=vals.size * 7 // 8, write_bytes=vals.nbytes, dtype="u32")
+        read_bytes=vals.size * 7 // 8, write_bytes=vals.nbytes, dtype="u32",
+        expect=expect_hash(_xxh(vals), "C1"))
 
 
 def make_c2(rng, world, rank):
     """C2: 64 Mi f64 prices -> ALP->FoR->BitPacked(u64, W=24) + Sparse patches (one chunk per GPU)."""
     import vortex_amd.encode as E
     n = 64 << 20
-    arr = E.encode_alp(c2_values(rng, n))
+    vals = c2_values(rng, n)
+    arr = E.encode_alp(vals)
     return arr, dict(name="C2", encoding="vortex.alp(fastlanes.for(fastlanes.bitpacked u64)) f64",
-                     values=n, read_bytes=arr.nbytes(), write_bytes=n * 8, dtype="f64")
+                     values=n, read_bytes=arr.nbytes(), write_bytes=n * 8, dtype="f64",
+                     expect=expect_hash(_xxh(vals), "C2"))
 
 
 def make_c3(rng, world, rank):
@@ -134,10 +221,16 @@ def make_c3(rng, world, rank):
     u64[1024])], 512 Ki values per chunk = 128 Mi values.  The table is the same at every N
     (strong scaling): this rank decodes the contiguous chunk range vortex_amd.shard.plan_shards
     gives it (balanced by compressed bytes; chunk_offsets, chunked/mod.rs:54-70), all 256 at N=1."""
+    import xxhash
     import vortex_amd.arrays as A
     mine = c3_shard(world, rank)
-    arr = A.chunked([c3_chunk(c) for c in mine])
-    return arr, dict(name="C3", encoding="vortex.chunked[vortex.dict(codes=fastlanes.bitpacked u64 W=10)] u64",
+    chunks, h = [], xxhash.xxh3_64()
+    for c in mine:
+        dv, codes = c3_chunk_plain(c)
+        chunks.append(c3_chunk(c, (dv, codes)))
+        h.update(memoryview(dv[codes]).cast("B"))  # take(values, codes), dict/array.rs:68-73
+    arr = A.chunked(chunks)
+    return arr, dict(expect=expect_hash(h.intdigest(), "C3"),name="C3", encoding="vortex.chunked[vortex.dict(codes=fastlanes.bitpacked u64 W=10)] u64",
                      values=len(mine) * C3_CHUNK_VALUES, read_bytes=arr.nbytes() - 8 * (len(mine) + 1),
                      write_bytes=len(mine) * C3_CHUNK_VALUES * 8, dtype="u64", chunks_per_gpu=len(mine),
                      chunk_range=[mine.start, mine.stop], global_chunks=C3_CHUNKS, strong_scaling=True)
@@ -150,8 +243,16 @@ def make_c4(rng, world, rank):
     n = 6_001_215
     heap, offs = c4_heap(rng, n)
     arr = E.encode_fsst_from_heap(heap, offs)
+    want_views, want_heap = _xxh(expected_views(heap, offs)), _xxh(heap)
+
+    def check(results):
+        r = results[0]
+        if _xxh(_host(r.views)) != want_views:
+            raise AssertionError("C4: views differ from make_view over the plain strings")
+        if len(r.data_buffers) != 1 or _xxh(_host(r.data)[: r.data_buffers[0][1]]) != want_heap:
+            raise AssertionError("C4: data buffer differs from the plain strings' bytes")
     return arr, dict(name="C4", encoding="vortex.fsst utf8 -> varbinview", values=n,
-                     read_bytes=arr.nbytes(), write_bytes=int(offs[-1]) + 16 * n, dtype="u8")
+                     read_bytes=arr.nbytes(), write_bytes=int(offs[-1]) + 16 * n, dtype="u8", expect=check)
 
 
 def c5_file(dist, rank: int) -> np.ndarray:
@@ -195,9 +296,10 @@ class FileWorkload:
     reader (vxg_file_*) parses footer, layouts and this rank's chunk messages; each column's
     message range is copied to HBM once (DeviceColumns); a step = one replay of the vxg_plan
     that canonicalizes the 16 reader-built ChunkedArray trees (struct_to_arrow,
-    canonical.rs:169-187: one canonicalize per field)."""
+    canonical.rs:169-187: one canonicalize per field).  `copies` device copies of the regions
+    (each with its own plan) are replayed in turn so the inputs come from HBM."""
 
-    def __init__(self, host, ctx, c0: int, c1: int):
+    def __init__(self, host, ctx, c0: int, c1: int, copies: int = 1):
         import torch
         import vortex_amd.arrays as A
         from vortex_amd.file import DeviceColumns, VortexFile
@@ -205,24 +307,38 @@ class FileWorkload:
         self.host = torch.from_numpy(host).pin_memory()
         t0 = time.perf_counter()
         self.f = VortexFile(self.host)
-        self.dc = DeviceColumns(self.f, ctx, None, c0, c1)
+        self.dcs = [DeviceColumns(self.f, ctx, None, c0, c1)]
         torch.cuda.synchronize()
         self.setup_s = time.perf_counter() - t0
-        self.plan = A.Plan(self.dc.nodes, ctx)
-        self.read_bytes = sum(_tree_buffer_bytes(n) for n in self.dc.nodes)
-        self.region_bytes = self.dc.nbytes()
+        self.dcs += [DeviceColumns(self.f, ctx, None, c0, c1) for _ in range(copies - 1)]
+        self.plans = [A.Plan(dc.nodes, ctx) for dc in self.dcs]
+        self.n_copies = copies
+        self.read_bytes = sum(_tree_buffer_bytes(n) for n in self.dcs[0].nodes)
+        self.region_bytes = self.dcs[0].nbytes()
+        self.input_bytes = self.region_bytes
         self.write_bytes = 0
-        for r in self.plan.results:
+        for r in self.plans[0].results:
             for t in (r.values, r.views, r.data):
                 if t is not None:
                     self.write_bytes += int(t.numel())
-        self.rows = int(self.dc.nodes[0].len)
+        self.rows = int(self.dcs[0].nodes[0].len)
+        self.i = 0
 
     def step(self):
-        self.plan.launch()
+        k = self.i
+        self.i += 1
+        self.plans[k % len(self.plans)].launch()
+
+    def results(self, k: int):
+        return self.plans[k].results
+
+    def run_copy(self, k: int):
+        self.i = k
+        self.step()
 
     def close(self):
-        self.plan.close()
+        for p in self.plans:
+            p.close()
         self.f.close()
 
 
@@ -275,7 +391,41 @@ def make_c5(rng, world, rank, dist=None):
     from tools import lineitem as L
     mine = c5_shard(world, rank)
     host = c5_file(dist, rank)
-    return ("file", host, mine.start, mine.stop), dict(
+
+    def check(results):
+        """Column by column against the generator's plain values of this rank's chunks:
+        numeric columns byte for byte, string columns row by row (logical value of each view)."""
+        host_res = []
+        for r in results:
+            if r.kind == "primitive":
+                host_res.append(("p", _host(r.values)))
+            else:
+                host_res.append(("s", _host(r.views).reshape(-1, 16), _host(r.data), r.data_buffers))
+            if r.validity is not None and not _host(r.validity).all():
+                raise AssertionError("C5: unexpected nulls")
+        row = 0
+        for c in mine:
+            vals = L.chunk_values(c)
+            n = vals["l_orderkey"].size
+            for (name, _), hr in zip(L.COLUMNS, host_res):
+                v = vals[name]
+                if hr[0] == "p":
+                    w = v.dtype.itemsize
+                    if hr[1][row * w: (row + n) * w].tobytes() != v.tobytes():
+                        raise AssertionError(f"C5 {name}: chunk {c} differs")
+                else:
+                    width = max(len(x) for x in v)
+                    gl, gs = strings_of(hr[1][row: row + n], hr[2], hr[3], max(width, 1))
+                    el, es = plain_strings(v, max(width, 1))
+                    if not (np.array_equal(gl, el) and np.array_equal(gs, es)):
+                        raise AssertionError(f"C5 {name}: chunk {c} strings differ")
+            row += n
+        for (name, kind), hr in zip(L.COLUMNS, host_res):
+            n_out = hr[1].size // {"i64": 8, "f64": 8, "i32": 4}[kind] if hr[0] == "p" else hr[1].shape[0]
+            if n_out != row:
+                raise AssertionError(f"C5 {name}: {n_out} rows out, {row} expected")
+
+    return ("file", host, mine.start, mine.stop), dict(expect=check,
         name="C5", encoding="lineitem scan from Vortex file bytes: 16 x vortex.chunked[<per-column cascades>] -> canonical",
         values=0, read_bytes=0, write_bytes=0, dtype="mixed", chunks_per_gpu=len(mine),
         chunk_range=[mine.start, mine.stop], global_chunks=L.n_chunks(), strong_scaling=True)
@@ -296,15 +446,28 @@ class Workload:
         arrs = arrs if isinstance(arrs, list) else [arrs]
         dev = torch.device("cuda", ctx.device)
         self.copies = [[arr.to(dev) for arr in arrs] for _ in range(copies)]
+        self.n_copies = copies
         if graph:
             self.plans = [A.Plan(trees, ctx) for trees in self.copies]
         else:
             self.keep = []
             self.cols = []
+            self.shared = []
             for j, arr in enumerate(arrs):
                 nodes = [A.flatten(trees[j], self.keep) for trees in self.copies]
-                self.cols.append((nodes, A.alloc_canonical(ctx, nodes[0], self.keep)[0]))
+                o, res = A.alloc_canonical(ctx, nodes[0], self.keep)
+                self.cols.append((nodes, o))
+                self.shared.append(res)
         self.i = 0
+        self.input_bytes = sum(a.nbytes() for a in arrs)
+
+    def results(self, k: int):
+        """Canonical outputs of copy k (direct calls share one output across copies)."""
+        return self.plans[k].results if self.graph else self.shared
+
+    def run_copy(self, k: int):
+        self.i = k
+        self.step()
 
     def step(self):
         k = self.i
@@ -367,6 +530,23 @@ def run_workload(wl, steps: int, warmup: int, dist):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     return elapsed, kmean, kmed
+
+
+def verify_workload(wl, expect) -> dict:
+    """After the timed region: replay every rotated copy once and check its output - copy 0
+    against the plain values (`expect`), every other copy byte-equal to copy 0."""
+    ref = None
+    for k in range(wl.n_copies):
+        wl.run_copy(k)
+        wl.ctx.sync()
+        res = wl.results(k)
+        hs = [_xxh(_host(t)) for r in res for t in (r.values, r.views, r.data, r.validity) if t is not None]
+        if k == 0:
+            expect(res)
+            ref = hs
+        elif hs != ref:
+            raise AssertionError(f"{wl.info['name'] if hasattr(wl, 'info') else 'C5'}: copy {k} output differs")
+    return {"verified": True, "copies_checked": wl.n_copies}
 
 
 def run_e2e(arr, info, ctx, reps: int = 5):
@@ -527,14 +707,15 @@ def cpu_baselines(budget_s: float, reps: int = 20) -> dict:
     t4, r4 = _median_time(lambda: canon(a4), reps, per_budget)
     out["C4"] = {"sample": "1 Mi synthetic l_comment strings, FSST",
                  "1core_GBps": round((int(offs[-1]) + 16 * (1 << 20)) / t4 / 1e9, 3), "reps": r4}
-    # C5: 8 of the 92 lineitem chunks x 16 columns
-    cols, plain = L.lineitem_columns(range(8))
-    c5 = [[cols[name].children[1 + i] for name, _ in L.COLUMNS] for i in range(8)]
+    # C5: 16 of the 92 lineitem chunks x 16 columns (>= the 16 cores of the all-core run)
+    n5 = max(16, cores)
+    cols, plain = L.lineitem_columns(range(n5))
+    c5 = [[cols[name].children[1 + i] for name, _ in L.COLUMNS] for i in range(n5)]
     c5_bytes = sum(L.canonical_bytes(v) for vs in plain.values() for v in vs)
     c3_bytes = 16 * C3_CHUNK_VALUES * 8
     global _POOL_ITEMS
     for key, items, nbytes, sample in (("C3", c3, c3_bytes, "16 of the 256 C3 chunks (8 Mi u64)"),
-                                       ("C5", c5, c5_bytes, "8 of the 92 lineitem chunks x 16 columns")):
+                                       ("C5", c5, c5_bytes, f"{n5} of the 92 lineitem chunks x 16 columns")):
         _POOL_ITEMS = items
         t1, r1 = _median_time(lambda: _pool_decode(range(len(items))), reps, per_budget)
         ent = {"sample": sample, "1core_GBps": round(nbytes / t1 / 1e9, 3), "reps": r1}
@@ -606,6 +787,10 @@ def main():
                     help="diagnostic: with one process, build rank 0's shard of an N-GPU run of C3/C5")
     ap.add_argument("--e2e", action="store_true",
                     help="also measure host->host (H2D + decode + D2H over PCIe); never the headline value")
+    ap.add_argument("--copies", type=int, default=0,
+                    help="diagnostic: rotated input copies for every workload (default: per config, > 256 MiB)")
+    ap.add_argument("--no-verify", action="store_true",
+                    help="skip the post-timing check of every output against the plain values")
     ap.add_argument("--launcher-selftest", action="store_true",
                     help="CPU check of the multi-process launch (gloo): print every rank's chunk ranges")
     args = ap.parse_args()
@@ -644,8 +829,12 @@ def main():
     # sharded configs, to read one GPU's share of the N-GPU work before an N-GPU node is used
     shard_world = args.simulate_world if args.simulate_world and world == 1 else world
     makers = {"c1": make_c1, "c2": make_c2, "c3": make_c3, "c4": make_c4, "c5": make_c5}
-    # C1: 8 rotated copies of its 58.7 MB input = 470 MB > the 256 MiB Infinity Cache
-    copies = {"c1": 8, "c2": 1, "c3": 1, "c4": 1, "c5": 1}
+    # Rotated HBM copies of every input, so the rotated total exceeds the 256 MiB Infinity Cache
+    # (MI355X_MICROARCH.md): C1 8 x 58.7 MB, C2 2 x 202 MB, C3 2 x 170 MB, C4 4 x 77 MB,
+    # C5 2 x 180 MB of file regions (one plan per copy)
+    copies = {"c1": 8, "c2": 2, "c3": 2, "c4": 4, "c5": 2}
+    if args.copies:
+        copies = {k: args.copies for k in copies}
     results = {}
     for key in [w.strip() for w in args.workloads.split(",") if w.strip()]:
         t0 = time.perf_counter()
@@ -653,7 +842,7 @@ def main():
         if isinstance(arr, tuple) and arr[0] == "file":
             _, host, c0, c1 = arr
             e2e = run_file_e2e(host, ctx, c0, c1) if args.e2e else None
-            wl = FileWorkload(host, ctx, c0, c1)
+            wl = FileWorkload(host, ctx, c0, c1, copies[key])
             info.update(values=wl.rows, read_bytes=wl.read_bytes, write_bytes=wl.write_bytes,
                         h2d_region_bytes=wl.region_bytes, reader_setup_ms=round(wl.setup_s * 1e3, 2))
         else:
@@ -668,6 +857,17 @@ def main():
             log(f"[bench] {info['name']}: built in {time.perf_counter() - t0:.1f}s; timing...")
         steps = args.steps if key == "c1" else max(3, args.steps // 2)
         elapsed, kmean, kmed = run_workload(wl, steps, args.warmup if key == "c1" else 2, dist)
+        check = None
+        if not args.no_verify:
+            t1 = time.perf_counter()
+            check = verify_workload(wl, info.pop("expect"))
+            check["verify_s"] = round(time.perf_counter() - t1, 1)
+            if rank == 0:
+                log(f"[bench] {info['name']}: output verified ({wl.n_copies} copies, {check['verify_s']} s)")
+        info.pop("expect", None)
+        rotation = {"copies": wl.n_copies, "input_bytes_per_copy": int(wl.input_bytes),
+                    "rotated_input_bytes": int(wl.n_copies * wl.input_bytes),
+                    "exceeds_infinity_cache": bool(wl.n_copies * wl.input_bytes > 256 * 2 ** 20)}
         per_step = elapsed / steps
         algo = info["read_bytes"] + info["write_bytes"]
         total_write = world * info["write_bytes"]
@@ -677,7 +877,7 @@ def main():
             total_write = float(t.item())
         results[key] = dict(info=info, elapsed=elapsed, ms_per_step=per_step * 1e3, kernel_ms_mean=kmean,
                             kernel_ms_median=kmed, algo_bytes=algo,
-                            value=total_write * steps / elapsed / 1e9, e2e=e2e)
+                            value=total_write * steps / elapsed / 1e9, e2e=e2e, check=check, rotation=rotation)
         wl.close()
         del wl
         torch.cuda.empty_cache()
@@ -715,6 +915,7 @@ def main():
                          "kernel_ms_mean": round(h["kernel_ms_mean"], 5),
                          "kernel_ms_median": round(h["kernel_ms_median"], 5),
                          "algorithmic_bytes_per_launch": h["algo_bytes"]},
+            "verified": bool(h["check"] and h["check"]["verified"]),
             "encodings": {},
         }
         for k, r in results.items():
@@ -732,6 +933,8 @@ def main():
             for extra in ("chunks_per_gpu", "chunk_range", "global_chunks", "h2d_region_bytes", "reader_setup_ms"):
                 if extra in i:
                     ent[extra] = i[extra]
+            ent["rotation"] = r["rotation"]
+            ent["verified"] = bool(r["check"] and r["check"]["verified"])
             if cpu is not None and i["name"] in cpu:
                 ent["cpu_baseline"] = cpu[i["name"]]
             if r.get("e2e"):

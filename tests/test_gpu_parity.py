@@ -736,6 +736,104 @@ def test_plan_mixed_large_and_small_arrays(ctx):
     plan.close()
 
 
+def _nested_chunked_arrays(rng):
+    """Trees whose ChunkedArray is NOT the root: a consumer kernel reads its decoded output right
+    after it (Dict values, FoR / ZigZag / ALP children, RunEnd ends and values, Sparse indices,
+    a string dictionary's values).  Under PlanBatch only a root ChunkedArray may defer its
+    launches to the end of the plan (nested deferral read unwritten temporaries)."""
+    def bp_chunks(v, W, sizes):
+        out, at = [], 0
+        for n in sizes:
+            out.append(E.encode_bitpacked(v[at:at + n], bit_width=W, allow_patches=False))
+            at += n
+        return A.chunked(out)
+
+    cases = []
+    # Dict(values = Chunked[u32], codes = BitPacked u16)
+    dv = rng.integers(0, 1 << 20, 3000, dtype=np.uint64).astype(np.uint32)
+    codes = rng.integers(0, dv.size, 40_000).astype(np.uint16)
+    cases.append((A.dict_array(bp_chunks(dv, 20, [1000, 1500, 500]),
+                               E.encode_bitpacked(codes, bit_width=12, allow_patches=False)), dv[codes]))
+    # FoR(i64) over Chunked[BitPacked u64]
+    raw = rng.integers(0, 1 << 9, 50_000, dtype=np.uint64)
+    ref = -123_456_789
+    cases.append((A.frame_of_reference(bp_chunks(raw, 9, [20_000, 1024, 28_976]), ref, 0, "i64"),
+                  raw.view(np.int64) + ref))
+    # ZigZag(i32) over Chunked[BitPacked u32]
+    zz = rng.integers(-500, 500, 30_000).astype(np.int32)
+    zu = ((zz.astype(np.int64) << 1) ^ (zz.astype(np.int64) >> 63)).astype(np.uint32)
+    cases.append((A.zigzag(bp_chunks(zu, 10, [10_000, 20_000])), zz))
+    # ALP(f64) over Chunked[FoR(BitPacked)] encoded ints
+    prices = np.round(rng.uniform(0, 1000, 20_000) * 100) / 100
+    e, f, enc, _, _ = E.alp_encode(prices)
+    assert enc.size == prices.size
+    enc = enc.astype(np.int64)
+    cases.append((A.alp(A.chunked([E.encode_for_bitpacked(enc[:7000], allow_patches=False),
+                                   E.encode_for_bitpacked(enc[7000:], allow_patches=False)]), e, f), None))
+    # RunEnd(ends = Chunked, values = Chunked)
+    runs = rng.integers(1, 9, 4000)
+    ends = np.cumsum(runs).astype(np.uint64)
+    rvals = rng.integers(0, 1 << 30, runs.size, dtype=np.uint64).astype(np.uint32)
+    cases.append((A.run_end(bp_chunks(ends, 15, [1500, 2500]), bp_chunks(rvals, 30, [2000, 2000]), int(ends[-1])),
+                  np.repeat(rvals, runs)))
+    # Sparse(u16) with Chunked indices
+    idx = np.sort(rng.choice(60_000, 700, replace=False)).astype(np.uint64)
+    sv = rng.integers(1, 1 << 16, idx.size, dtype=np.uint64).astype(np.uint16)
+    expect = np.zeros(60_000, np.uint16)
+    expect[idx] = sv
+    cases.append((A.sparse(bp_chunks(idx, 16, [300, 400]), A.primitive(sv), 60_000), expect))
+    return cases
+
+
+def test_plan_nested_chunked_not_deferred(ctx):
+    """A plan with a root ChunkedArray (batching on) and trees holding NESTED ChunkedArrays:
+    every replay equals the oracle and vxg_canonicalize, for primitive and string trees."""
+    import torch
+    rng = np.random.default_rng(2024)
+    cases = _nested_chunked_arrays(rng)
+    root = A.chunked([E.encode_bitpacked(rng.integers(0, 1 << 7, n, dtype=np.uint64).astype(np.uint32),
+                                         bit_width=7, allow_patches=False) for n in (5000, 3000)])
+    words = [b"DELIVER IN PERSON", b"NONE", b"TAKE BACK RETURN", b"COLLECT COD", b"x" * 40]
+    sdict = A.chunked([E.encode_dict_strings([words[i] for i in rng.integers(0, 5, n)]).children[0]
+                       for n in (3, 4)])  # Chunked[VarBin] dictionary values
+    scodes = rng.integers(0, sdict.len, 9000).astype(np.uint8)
+    sarr = A.dict_array(sdict, E.encode_bitpacked(scodes, bit_width=3, allow_patches=False))
+    arrs = [root] + [a for a, _ in cases] + [sarr]
+    plan = V.Plan([a.to(torch.device("cuda", 0)) for a in arrs], ctx)
+    for _ in range(3):
+        res = plan.launch(sync=True)
+        assert res[0].numpy().tobytes() == canon(root)[0].tobytes()
+        for k, ((a, exp), r) in enumerate(zip(cases, res[1:-1])):
+            got = r.numpy()
+            ref, _ = canon(a)
+            assert got.tobytes() == ref.tobytes(), k
+            assert got.tobytes() == gpu(a, ctx).numpy().tobytes(), k
+            if exp is not None:
+                assert got.tobytes() == np.ascontiguousarray(exp).tobytes(), k
+        (rviews, rbufs), _ = canon(sarr)
+        assert res[-1].numpy()[0].tobytes() == rviews.tobytes()
+        assert [b.tobytes() for b in res[-1].buffers()] == [b.tobytes() for b in rbufs]
+    plan.close()
+
+
+def test_varbin_bad_offsets_is_an_error(ctx):
+    """VarBin offsets that run backwards or past the bytes are rejected (zero view + error),
+    on the direct path and through a plan's batched dictionary views."""
+    import torch
+    heap = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz0123456789", np.uint8).copy()
+    offs = np.array([0, 5, 3, 20, 36, 40], np.int32)  # 5 -> 3 backwards; 36 -> 40 past the end
+    vb = A.varbin(A.primitive(offs), A.primitive(heap))
+    with pytest.raises(V.VortexGpuError, match="VarBin offsets"):
+        gpu(vb, ctx)
+    codes = np.array([0, 1, 2, 3, 4] * 100, np.uint8)
+    d = A.dict_array(vb, E.encode_bitpacked(codes, bit_width=3, allow_patches=False))
+    arr = A.chunked([d, d])
+    plan = V.Plan([arr.to(torch.device("cuda", 0))], ctx)
+    with pytest.raises(V.VortexGpuError, match="VarBin offsets"):
+        plan.launch(sync=True)
+    plan.close()
+
+
 # ------------------------------------------------------------------ edge cases: empty inputs
 def test_empty_arrays_every_encoding(ctx):
     """len = 0 through every encoding and container (the reference canonicalizes empty arrays

@@ -201,6 +201,41 @@ def test_region_must_cover_the_chunks():
     f.close()
 
 
+def test_region_must_cover_every_chunk():
+    """Chunk messages out of file order (a malformed or foreign writer): a region spanning the
+    first chunk's begin and the last chunk's end does not cover a middle chunk written elsewhere,
+    and no buffer pointer may leave the region."""
+    cols, _ = _lineitem(rows=3000, chunk_rows=1024)
+    cols = cols[:2]
+    order = [(0, 0), (0, 2), (1, 0), (1, 1), (1, 2), (0, 1)]
+    data = X.write_file(cols, message_order=order)
+    f = VortexFile(data)
+    c0, c1, c2 = (f.chunk(0, k) for k in range(3))
+    assert c0.message_begin < c2.message_begin < c1.message_begin
+    b, e = c0.message_begin, c2.message_end
+    with pytest.raises(L.VortexGpuError) as ei:
+        f.column_tree(0, 0, 3, region=1 << 40, region_offset=b, region_len=e - b)
+    assert ei.value.kind in ("InvalidArgument", "InvalidSerde")
+    # covering all three messages is fine, and the out-of-order file still reads correctly
+    node = f.column_tree(0, 0, 3, region=1 << 40, region_offset=b, region_len=c1.message_end - b)
+    lo, hi = 1 << 40, (1 << 40) + c1.message_end - b
+    for k in range(3):
+        for leaf in _leaf_buffers(node.children[1 + k]):
+            assert lo <= leaf[0] and leaf[0] + leaf[1] <= hi
+    raw = np.frombuffer(data, np.uint8)
+    node = f.column_tree(0, 0, 3)
+    for k, ch in enumerate(cols[0][1]):
+        _check_tree(node.children[1 + k], ch, raw)
+    f.close()
+
+
+def _leaf_buffers(node):
+    out = [(int(node.buffers[i].ptr or 0), int(node.buffers[i].len)) for i in range(node.n_buffers)]
+    for i in range(node.n_children):
+        out += _leaf_buffers(node.children[i])
+    return out
+
+
 def test_flatbuffer_postscript_is_32_bytes():
     # writer.rs:248-262 postscript_size: a Postscript flatbuffer is exactly 32 bytes
     fbb = X.FBB()

@@ -236,6 +236,36 @@ __global__ __launch_bounds__(256) void k_copy(const uint4* __restrict__ in, uint
     }
 }
 
+// burst copy reference: a workgroup reads its 32 blocks' packed bytes (28 KiB) into LDS in one
+// burst, then writes its 128 KiB of output, each wave 32 KiB with 1 KiB contiguous instructions
+// (plain or NT stores) -- do phase-separated reads and writes beat interleaved ones?
+template <int NT>
+__global__ __launch_bounds__(256) void k_burst(const uint4* __restrict__ in, uint4* __restrict__ out, uint64_t n_blocks) {
+    __shared__ uint4 s_in[32 * 56];  // 32 blocks x 896 B
+    const uint64_t b0 = uint64_t(blockIdx.x) * 32;
+    if (b0 >= n_blocks) return;
+    const uint4* src = in + b0 * 56;
+    for (int q = threadIdx.x; q < 32 * 56; q += 256) s_in[q] = src[q];
+    __syncthreads();
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint4 acc = s_in[wave * 448 + lane];
+    uint4* dst = out + (b0 + wave * 8) * 256;
+#pragma unroll
+    for (int k = 0; k < 32; k++) {
+        uint4 v = make_uint4(acc.x + k, acc.y, acc.z, acc.w);
+        store_bytes<16, NT>(reinterpret_cast<uint8_t*>(dst + k * 64 + lane), &v);
+    }
+}
+
+// write-only, wave-contiguous: each wave writes 32 KiB, 1 KiB per instruction, plain stores
+__global__ __launch_bounds__(256) void k_write_wave(uint4* __restrict__ out, uint64_t n16) {
+    const uint64_t wave = (uint64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    if (wave * 2048 >= n16) return;
+#pragma unroll
+    for (int k = 0; k < 32; k++) out[wave * 2048 + k * 64 + lane] = make_uint4(unsigned(k), 1u, 2u, 3u);
+}
+
 // write-only reference: 268 MB of NT stores, nothing read
 __global__ __launch_bounds__(256) void k_write(uint4* __restrict__ out, uint64_t n16) {
     using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
@@ -284,7 +314,9 @@ int main(int argc, char** argv) {
                              {"split2_nt", 5}, {"split4_nt", 6}, {"copy_ref_nt", 7}, {"write_only_nt", 8},
                              {"base_plain", 11}, {"copy_ref_plain", 12},
                              {"memord_nt", 13}, {"memord_plain", 14}, {"xcd_nt", 15}, {"xcd_memord_nt", 16},
-                             {"copy_pipe_x4_plain", 17}, {"copy_pipe_x8_plain", 18}, {"copy_pipe_x8_nt", 19}};
+                             {"copy_pipe_x4_plain", 17}, {"copy_pipe_x8_plain", 18}, {"copy_pipe_x8_nt", 19},
+                             {"tr_plain", 9}, {"tr_nt", 10}, {"burst_plain", 20}, {"burst_nt", 21},
+                             {"write_wave_plain", 22}};
     auto launch = [&](int id, const uint8_t* src) {
         switch (id) {
         case 1: hipLaunchKernelGGL(k_base<1>, dim3(grid_base), dim3(256), 0, 0, src, out, n_blocks); break;
@@ -305,13 +337,16 @@ int main(int argc, char** argv) {
         case 17: hipLaunchKernelGGL(k_copy_pipe<0>, dim3(cus * 4), dim3(256), 0, 0, (const uint4*)src, (uint4*)out, n_blocks); break;
         case 18: hipLaunchKernelGGL(k_copy_pipe<0>, dim3(cus * 8), dim3(256), 0, 0, (const uint4*)src, (uint4*)out, n_blocks); break;
         case 19: hipLaunchKernelGGL(k_copy_pipe<1>, dim3(cus * 8), dim3(256), 0, 0, (const uint4*)src, (uint4*)out, n_blocks); break;
+        case 20: hipLaunchKernelGGL(k_burst<0>, dim3(unsigned(n_blocks / 32)), dim3(256), 0, 0, (const uint4*)src, (uint4*)out, n_blocks); break;
+        case 21: hipLaunchKernelGGL(k_burst<1>, dim3(unsigned(n_blocks / 32)), dim3(256), 0, 0, (const uint4*)src, (uint4*)out, n_blocks); break;
+        case 22: hipLaunchKernelGGL(k_write_wave, dim3(unsigned(out_bytes / 16 / 2048 / 4)), dim3(256), 0, 0, (uint4*)out, out_bytes / 16); break;
         case 8: hipLaunchKernelGGL(k_write, dim3(cus * 8), dim3(256), 0, 0, (uint4*)out, out_bytes / 16); break;
         }
     };
     std::vector<uint32_t> h_ref(n_vals), h_out(n_vals);
     CK(hipMemcpy(h_ref.data(), ref, out_bytes, hipMemcpyDeviceToHost));
     for (auto& v : vars) {
-        if (v.id == 7 || v.id == 8 || v.id == 12 || v.id >= 17) continue;
+        if (v.id == 7 || v.id == 8 || v.id == 12 || (v.id >= 17 && v.id != 9 && v.id != 10)) continue;
         CK(hipMemset(out, 0, out_bytes));
         launch(v.id, in[0]);
         CK(hipDeviceSynchronize());
@@ -345,7 +380,7 @@ int main(int argc, char** argv) {
         auto v = t[vi];
         std::sort(v.begin(), v.end());
         const double med = v[v.size() / 2], mn = v[0];
-        const double by = vars[vi].id == 8 ? double(out_bytes) : bytes;
+        const double by = (vars[vi].id == 8 || vars[vi].id == 22) ? double(out_bytes) : bytes;
         printf("%-16s median %8.2f us  min %8.2f us  algo %7.1f GB/s (%.1f%% of 8 TB/s)\n",
                vars[vi].name, med * 1e3, mn * 1e3, by / (med * 1e-3) / 1e9, 100.0 * by / (med * 1e-3) / 8e12);
     }

@@ -604,28 +604,38 @@ def _write_layout(fbb: FBB, l: Layout) -> int:
     return fbb.end()
 
 
-def write_file(columns: Sequence[tuple], row_count: Optional[int] = None) -> bytes:
+def write_file(columns: Sequence[tuple], row_count: Optional[int] = None,
+               message_order: Optional[Sequence[tuple]] = None) -> bytes:
     """LayoutWriter::write_array_columns + finalize for a StructArray whose fields are
     ChunkedArrays (bench-vortex tpch/mod.rs:249-307): `columns` = [(name, [chunk Array, ...])].
-    Each chunk is one Batch message; every column's chunks are written consecutively."""
+    Each chunk is one Batch message; every column's chunks are written consecutively, unless
+    `message_order` (a permutation of (column, chunk) pairs) says otherwise (test input for
+    readers that must not assume ascending, contiguous chunk messages)."""
     out = bytearray()
+    order = list(message_order) if message_order is not None else \
+        [(ci, k) for ci, (_, chunks) in enumerate(columns) for k in range(len(chunks))]
+    if sorted(order) != [(ci, k) for ci, (_, chunks) in enumerate(columns) for k in range(len(chunks))]:
+        raise ValueError("message_order must be a permutation of the (column, chunk) pairs")
+    spans = {}
+    for ci, k in order:
+        b = len(out)
+        out += batch_message(columns[ci][1][k])
+        spans[(ci, k)] = (b, len(out))
     col_ranges = []
     nrows = None
-    for name, chunks in columns:
-        offs, rows = [len(out)], [0]
+    for ci, (name, chunks) in enumerate(columns):
+        rows = [0]
         for c in chunks:
-            out += batch_message(c)
-            offs.append(len(out))
             rows.append(rows[-1] + c.len)
-        col_ranges.append((offs, rows))
+        col_ranges.append(([spans[(ci, k)] for k in range(len(chunks))], rows))
         nrows = rows[-1] if nrows is None else nrows
         if rows[-1] != nrows:
             raise ValueError("columns of different lengths")
     # per-column metadata tables (writer.rs:120-157)
     layouts = []
     meta_dtype = DType("struct", names=("row_offset",), fields=(DType("primitive", "u64"),))
-    for offs, rows in col_ranges:
-        flats = [Layout(FLAT, buffers=[(b, e)]) for b, e in zip(offs[:-1], offs[1:])]
+    for spans_c, rows in col_ranges:
+        flats = [Layout(FLAT, buffers=[(b, e)]) for b, e in spans_c]
         row_offsets = np.array(rows[:-1], dtype=np.uint64)
         table = Array(ENC_STRUCT, len(row_offsets), DTYPE["NULL"], "u8", False, VALIDITY["NON_NULLABLE"], {}, [],
                       [Array(ENC["PRIMITIVE"], len(row_offsets), DTYPE["PRIMITIVE"], "u64", False,

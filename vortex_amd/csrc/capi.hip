@@ -363,10 +363,11 @@ struct PlanBatch {
     bool empty() const { return dicts.empty() && jobs.empty() && runs.empty(); }
 };
 
-vxg_status launch_varbin_dicts(const std::vector<VarBinChunk>& dicts, hipStream_t s, DevTables* dt) {
+vxg_status launch_varbin_dicts(const std::vector<VarBinChunk>& dicts, uint32_t* err, hipStream_t s, DevTables* dt) {
     const size_t per = dt && dicts.size() > size_t(kVarBinArgChunks) ? dicts.size() : size_t(kVarBinArgChunks);
     for (size_t i = 0; i < dicts.size(); i += per) {
         VarBinTable tab{};
+        tab.err = err;
         VarBinChunk* cs = tab.c;
         if (per > size_t(kVarBinArgChunks)) {
             VarBinChunk* host;
@@ -386,7 +387,7 @@ vxg_status launch_varbin_dicts(const std::vector<VarBinChunk>& dicts, hipStream_
 }
 
 vxg_status flush_plan_batch(PlanBatch& b, uint32_t* err, hipStream_t s, DevTables* dt) {
-    VXG_TRY_S(launch_varbin_dicts(b.dicts, s, dt));
+    VXG_TRY_S(launch_varbin_dicts(b.dicts, err, s, dt));
     // short-run expansions that read their children in place join the K1g launch; the others
     // follow the K1 decodes that produce their children
     std::vector<std::pair<int, RunEndChunk>> gen_runs;
@@ -440,6 +441,13 @@ class Planner {
     // holds become device tables (one launch per kernel group).
     DevTables* plan_ = nullptr;
     PlanBatch* batch_ = nullptr;  // a plan's deferred launches (all its arrays), or null
+    // The array canonical() was called on.  Only a ChunkedArray that IS this root defers its
+    // launches into batch_: its chunks write straight into the caller's output and nothing
+    // recorded after it reads them.  A nested ChunkedArray (Dict values, FoR/ZigZag/ALP child,
+    // Sparse/RunEnd children, views of a string dictionary) feeds a consumer recorded right
+    // after it, so it launches immediately.
+    const vxg_array* root_ = nullptr;
+    bool defer(const vxg_array& a) const { return batch_ && &a == root_; }
     // Deferred K1 decodes of the chunks of a ChunkedArray (grouped into shared launches) and
     // the patch scatters that must follow them; null = launch immediately.
     struct PatchJob {
@@ -823,7 +831,7 @@ vxg_status Planner::decode_chunked_primitive(const vxg_array& a, void* dst) {
         off += c.len;
     }
     if (off != a.len) return set_error(VXG_ERR_INVALID_ARGUMENT, "Chunked len != sum of chunk lens");
-    if (batch_ && patches.empty()) {  // a plan: launched with the other arrays' jobs (PlanBatch)
+    if (defer(a) && patches.empty()) {  // a plan's root: launched with the other arrays' jobs (PlanBatch)
         batch_->jobs.insert(batch_->jobs.end(), jobs.begin(), jobs.end());
         for (size_t k = 0; k < runs.size(); k++) batch_->runs.push_back(PlanBatch::Run{w, runs[k], runs_indep[k] != 0});
         return VXG_OK;
@@ -1505,7 +1513,7 @@ vxg_status Planner::strings_into(const vxg_array& a, uint8_t* views, uint8_t* da
         uint8_t* heap = data + bufs[0].offset;
         if (bufs[0].len)
             VXG_TRY(hip_check(hipMemcpyAsync(heap, pb, bufs[0].len, hipMemcpyDeviceToDevice, s_), "heap copy"));
-        return launch_varbin_views(heap, width(*offs), po, a.len, validity, bidx, views, s_);
+        return launch_varbin_views(heap, bufs[0].len, width(*offs), po, a.len, validity, bidx, views, ctx_->c.err_word, s_);
     }
     case VXG_ENC_VARBINVIEW: {
         // already canonical: views (rebased) and buffers copied into the output layout
@@ -1639,7 +1647,7 @@ vxg_status Planner::strings_into(const vxg_array& a, uint8_t* views, uint8_t* da
                 // a plan batch with a small dictionary: K1g builds its views in LDS (no views
                 // launch); otherwise the views are built into dviews first
                 const vxg_array& codes = c.children[1];
-                const bool vb = batch_ && v.len <= kGenVarBinDictMax && v.len > 0 && codes.len > 0 &&
+                const bool vb = defer(a) && v.len <= kGenVarBinDictMax && v.len > 0 && codes.len > 0 &&
                                 !codes.meta.bitpacked.has_patches;
                 if (!vb) dicts.push_back(d);
                 UnpackArgs ua{};
@@ -1683,12 +1691,12 @@ vxg_status Planner::strings_into(const vxg_array& a, uint8_t* views, uint8_t* da
             VXG_TRY(temp(fsst_batch_scratch_bytes(fssts.data(), fssts.size()), &scratch));
             VXG_TRY(launch_fsst_batch(fssts, scratch, ctx_->c.err_word, s_, plan_));
         }
-        if (batch_ && patches.empty()) {  // a plan: launched with the other arrays' jobs (PlanBatch)
+        if (defer(a) && patches.empty()) {  // a plan's root: launched with the other arrays' jobs (PlanBatch)
             batch_->dicts.insert(batch_->dicts.end(), dicts.begin(), dicts.end());
             batch_->jobs.insert(batch_->jobs.end(), jobs.begin(), jobs.end());
             return VXG_OK;
         }
-        VXG_TRY(launch_varbin_dicts(dicts, s_, plan_));
+        VXG_TRY(launch_varbin_dicts(dicts, ctx_->c.err_word, s_, plan_));
         VXG_TRY(launch_k1_jobs(jobs, ctx_->c.err_word, s_, plan_));
         for (const PatchJob& p : patches) VXG_TRY(apply_sparse_patches(*p.sp, p.T, p.epi, p.vw, p.a, p.dst, p.out_len));
         return VXG_OK;
@@ -1751,6 +1759,7 @@ vxg_status Planner::canonical_size(const vxg_array& a, uint64_t& vb, uint64_t& d
 }
 
 vxg_status Planner::canonical(const vxg_array& a, vxg_canonical& out) {
+    root_ = &a;
     out.len = a.len;
     out.dtype = a.dtype;
     out.ptype = a.ptype;
@@ -1871,6 +1880,7 @@ vxg_status vxg_stream_sync(vxg_ctx* ctx, void* stream) {
             return set_error(VXG_ERR_INVALID_ARGUMENT, "FSST codes do not decode to uncompressed_lengths");
         if (err & kErrRoaring)
             return set_error(VXG_ERR_INVALID_SERDE, "RoaringBool buffer is not a croaring Native bitmap");
+        if (err & kErrVarBin) return set_error(VXG_ERR_INVALID_ARGUMENT, "VarBin offsets out of range of the bytes");
     }
     return VXG_OK;
 }
@@ -2006,7 +2016,7 @@ static std::vector<hipKernelNodeParams> kernel_chain(hipGraph_t g) {
     std::vector<hipGraphNode_t> dep(nn, nullptr);
     size_t roots = 0, root = 0;
     for (size_t i = 0; i < nn; i++) {
-        hipGraphNodeType t;
+        hipGraphNodeType t{};
         if (hipGraphNodeGetType(nodes[i], &t) != hipSuccess || t != hipGraphNodeTypeKernel) {
             if (std::getenv("VXG_PLAN_DEBUG")) std::fprintf(stderr, "plan: node %zu of %zu has type %d\n", i, nn, int(t));
             return out;

@@ -83,7 +83,12 @@ __device__ __forceinline__ void gen_body(const GenChunk& gc, uint64_t g, uint8_t
         for (uint32_t k = tid; k < c.dict_len; k += kGenThreads) {
             const uint64_t a = vb_offset(gc.vb_offs, gc.vb_offs_width, k);
             const uint64_t e = vb_offset(gc.vb_offs, gc.vb_offs_width, k + 1);
-            s_views[k] = vb_view(gc.vb_src, a, uint32_t(e - a), gc.vb_bidx);
+            if (a > e || e > gc.vb_bytes) {  // malformed offsets: zero view + error bit
+                __hip_atomic_fetch_or(err, kErrVarBin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                s_views[k] = make_uint4(0, 0, 0, 0);
+            } else {
+                s_views[k] = vb_view(gc.vb_src, a, uint32_t(e - a), gc.vb_bidx);
+            }
         }
         ep.dict = s_views;
     } else if constexpr (EPI == Epi::Dict) {

@@ -766,10 +766,20 @@ __device__ __forceinline__ uint4 make_view(const uint8_t* __restrict__ heap, uin
     return make_uint4(len, w1, w2, w3);
 }
 
-__global__ __launch_bounds__(kBlock) void varbin_views_kernel(const uint8_t* __restrict__ heap, const void* offs,
-                                                              int offs_width, uint64_t n,
+// A row whose offsets are not a <= e <= heap_len gets an all-zero view and sets kErrVarBin.
+__device__ __forceinline__ uint4 checked_view(const uint8_t* __restrict__ heap, uint64_t heap_len, uint64_t a,
+                                              uint64_t e, uint32_t bidx, uint32_t* err) {
+    if (a > e || e > heap_len) {
+        __hip_atomic_fetch_or(err, kErrVarBin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return make_uint4(0, 0, 0, 0);
+    }
+    return make_view(heap, a, uint32_t(e - a), bidx);
+}
+
+__global__ __launch_bounds__(kBlock) void varbin_views_kernel(const uint8_t* __restrict__ heap, uint64_t heap_len,
+                                                              const void* offs, int offs_width, uint64_t n,
                                                               const uint8_t* __restrict__ validity,
-                                                              uint32_t bidx, uint4* __restrict__ views) {
+                                                              uint32_t bidx, uint4* __restrict__ views, uint32_t* err) {
     const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
     for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
         if (validity && !((validity[i >> 3] >> (i & 7)) & 1)) {
@@ -778,15 +788,15 @@ __global__ __launch_bounds__(kBlock) void varbin_views_kernel(const uint8_t* __r
         }
         const uint64_t a = load_uint(offs, offs_width, offs_width < 8, i);
         const uint64_t b = load_uint(offs, offs_width, offs_width < 8, i + 1);
-        views[i] = make_view(heap, a, uint32_t(b - a), bidx);
+        views[i] = checked_view(heap, heap_len, a, b, bidx, err);
     }
 }
 
-vxg_status launch_varbin_views(const uint8_t* heap, int offs_width, const void* offsets, uint64_t n,
-                               const uint8_t* validity, uint32_t bidx, uint8_t* views, hipStream_t s) {
+vxg_status launch_varbin_views(const uint8_t* heap, uint64_t heap_len, int offs_width, const void* offsets, uint64_t n,
+                               const uint8_t* validity, uint32_t bidx, uint8_t* views, uint32_t* err, hipStream_t s) {
     if (n == 0) return VXG_OK;
-    hipLaunchKernelGGL(varbin_views_kernel, dim3(grid_for(n)), dim3(kBlock), 0, s, heap, offsets,
-                       offs_width, n, validity, bidx, reinterpret_cast<uint4*>(views));
+    hipLaunchKernelGGL(varbin_views_kernel, dim3(grid_for(n)), dim3(kBlock), 0, s, heap, heap_len, offsets,
+                       offs_width, n, validity, bidx, reinterpret_cast<uint4*>(views), err);
     return hip_check(hipGetLastError(), "varbin_views_kernel");
 }
 
@@ -813,7 +823,7 @@ __global__ __launch_bounds__(kBlock) void varbin_chunks_kernel(VarBinTable tab) 
     if (i < c.n) {
         const uint64_t a = load_uint(c.offsets, int(c.offs_width), c.offs_width < 8, i);
         const uint64_t e = load_uint(c.offsets, int(c.offs_width), c.offs_width < 8, i + 1);
-        reinterpret_cast<uint4*>(c.views)[i] = make_view(c.src, a, uint32_t(e - a), c.bidx);
+        reinterpret_cast<uint4*>(c.views)[i] = checked_view(c.src, c.bytes, a, e, c.bidx, tab.err);
     }
 }
 

@@ -485,6 +485,7 @@ struct Builder {
     const BatchBuffers* bb;
     const uint8_t* region;    // caller's copy of the file bytes
     uint64_t region_off;
+    uint64_t region_len;
     Pool* pool;
 
     Flex meta(const FbTable& a, bool required) const {
@@ -501,6 +502,10 @@ struct Builder {
         if (!a.has(1)) return;  // buffer_index = null
         const uint64_t i = a.get<uint64_t>(1, 0);
         if (i >= bb->off.size()) bad("buffer_index out of range");
+        // every buffer must lie inside the caller's region (chunk messages of a malformed file
+        // need not be in ascending, non-overlapping order)
+        if (bb->off[i] < region_off || bb->len[i] > region_len || bb->off[i] - region_off > region_len - bb->len[i])
+            bad("buffer lies outside the region copied to the device");
         vxg_buffer* b = pool->alloc_buf();
         b->ptr = reinterpret_cast<const void*>(reinterpret_cast<uintptr_t>(region) + uintptr_t(bb->off[i] - region_off));
         b->len = bb->len[i];
@@ -1132,7 +1137,10 @@ vxg_status vxg_file_column_array(vxg_file* file, uint32_t column, uint32_t chunk
             read_batch_geometry(*file, c.begin, c.end, &batch, &bb);
             FbTable arr;
             if (!batch.table(0, &arr)) bad("Chunk missing Array");
-            Builder b{file->bytes, file->len, &bb, static_cast<const uint8_t*>(region), region_file_offset, &file->pool};
+            if (c.begin < region_file_offset || c.end > region_file_offset + region_len)
+                bad("region does not cover chunk " + std::to_string(chunk_begin + i) + "'s message");
+            Builder b{file->bytes, file->len, &bb, static_cast<const uint8_t*>(region), region_file_offset, region_len,
+                      &file->pool};
             b.build(arr, dt, c.rows, kids[i + 1], 0);
         }
         vxg_array& r = root[0];

@@ -55,7 +55,7 @@ extern const double kF10d[24];
 extern const double kIF10d[24];
 
 // Device error word bits (set by kernels, read by vxg_check via vxg_stream_sync).
-enum : uint32_t { kErrTakeOOB = 1u, kErrPatchOOB = 2u, kErrRunEnd = 4u, kErrFsst = 8u, kErrRoaring = 16u };
+enum : uint32_t { kErrTakeOOB = 1u, kErrPatchOOB = 2u, kErrRunEnd = 4u, kErrFsst = 8u, kErrRoaring = 16u, kErrVarBin = 32u };
 
 struct Ctx {
     int device = 0;
@@ -280,6 +280,7 @@ struct VarBinTable {
     VarBinChunk c[kVarBinArgChunks];
     uint32_t n;
     const VarBinChunk* ext;  // device table of n entries (plans), or null
+    uint32_t* err;           // kErrVarBin: offsets not monotonic inside the bytes
 };
 vxg_status launch_varbin_chunks(const VarBinTable& t, uint64_t groups, hipStream_t s);
 
@@ -316,8 +317,8 @@ uint64_t fsst_batch_scratch_bytes(const FsstChunk* chunks, size_t n_chunks);
 vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint32_t* err, hipStream_t s,
                              DevTables* dt = nullptr);
 // Views carry `bidx` as the buffer_index of non-inlined rows.
-vxg_status launch_varbin_views(const uint8_t* heap, int offs_width, const void* offsets, uint64_t n,
-                               const uint8_t* validity, uint32_t bidx, uint8_t* views, hipStream_t s);
+vxg_status launch_varbin_views(const uint8_t* heap, uint64_t heap_len, int offs_width, const void* offsets, uint64_t n,
+                               const uint8_t* validity, uint32_t bidx, uint8_t* views, uint32_t* err, hipStream_t s);
 vxg_status launch_views_rebase(const uint8_t* src, uint64_t n, uint32_t add, uint8_t* dst, hipStream_t s);
 
 }  // namespace vxg
