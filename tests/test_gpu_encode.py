@@ -232,3 +232,97 @@ def test_alp_many_exceptions_regrows_capacity(ctx):
     vals = rng.standard_normal(20_000)  # nearly every value is an exception
     vals[::2] = np.round(vals[::2] * 100) / 100
     assert_alp_same(ctx, vals, "f64")
+
+
+# ------------------------------------------------------------------ K17 FSST compress
+FSST_SENTENCES = [  # encodings/fsst/tests/fsst_tests.rs:19-35
+    b"The Greeks never said that the limit could not he overstepped",
+    b"They said it existed and that whoever dared to exceed it was mercilessly struck down",
+    b"Nothing in present history can contradict them",
+]
+
+
+def _dev(x):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(x).view(np.uint8).reshape(-1).copy()).cuda()
+
+
+def _fsst_gpu_vs_host(ctx, strings, offs_ptype="i64"):
+    """GPU FSST (host-trained table from the device column's sample + K17 compress) against the
+    host encoder (encode.encode_fsst_from_heap, plain children): the same table, byte-equal
+    codes, i32 code offsets and i32 uncompressed lengths; then decode(encode(x)) == x through
+    the K6/K7 canonicalize."""
+    import torch
+    heap, offs, valid = E.strings_to_heap(strings)
+    has_nulls = not valid.all()
+    host = E.encode_fsst_from_heap(heap, offs, valid if has_nulls else None, compress_children=False)
+    n = len(strings)
+    vbits = np.packbits(valid, bitorder="little") if has_nulls else None
+    d_offs = _dev(offs.astype(A.NP_OF_PTYPE[offs_ptype]))
+    d_heap = _dev(heap if heap.size else np.zeros(1, np.uint8))[: heap.size]
+    arr = G.encode_fsst(ctx, d_offs, offs_ptype, d_heap, n, validity=_dev(vbits) if has_nulls else None)
+    syms, slen, codes_vb, ulens = arr.children
+    hsyms, hslen, hcodes_vb, hulens = host.children
+    assert syms.buffers[0].cpu().numpy().tobytes() == np.ascontiguousarray(hsyms.buffers[0]).tobytes()
+    assert slen.buffers[0].cpu().numpy().tobytes() == np.ascontiguousarray(hslen.buffers[0]).tobytes()
+    assert codes_vb.children[0].buffers[0].cpu().numpy().tobytes() == \
+        np.ascontiguousarray(hcodes_vb.children[0].buffers[0]).astype(np.int32).tobytes()
+    assert codes_vb.children[1].buffers[0].cpu().numpy().tobytes() == \
+        np.ascontiguousarray(hcodes_vb.children[1].buffers[0]).tobytes()
+    assert ulens.buffers[0].cpu().numpy().tobytes() == np.ascontiguousarray(hulens.buffers[0]).astype(np.int32).tobytes()
+    assert codes_vb.nullable == hcodes_vb.nullable
+    res = V.canonicalize(arr.to(torch.device("cuda", 0)), ctx)
+    views, _ = res.numpy()
+    bufs = res.buffers()
+    from oracle_tree import view_bytes
+    for i in range(0, n, max(1, n // 5000)):
+        if strings[i] is not None:
+            assert view_bytes(views, bufs, i) == strings[i], i
+    return arr
+
+
+def test_fsst_compress_reference_sentences(ctx):
+    """The reference's FSST test input (fsst_tests.rs:19-35), i32 and i64 offsets."""
+    for op in ("i32", "i64"):
+        _fsst_gpu_vs_host(ctx, FSST_SENTENCES, op)
+
+
+def test_fsst_compress_comments_1m(ctx):
+    """1 Mi synthetic l_comment strings (bench C4's generator), plus escapes: bytes no symbol
+    covers, empty strings and nulls."""
+    import sys
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+    import bench
+    rng = np.random.default_rng(17)
+    heap, offs = bench.c4_heap(rng, 1 << 20)
+    strings = [heap[offs[i]:offs[i + 1]].tobytes() for i in range(offs.size - 1)]
+    for i in range(0, len(strings), 997):
+        strings[i] = None
+    for i in range(5, len(strings), 1009):
+        strings[i] = b""
+    for i in range(7, len(strings), 4999):
+        strings[i] = bytes(rng.integers(0, 256, int(rng.integers(1, 90)), dtype=np.uint8))
+    _fsst_gpu_vs_host(ctx, strings)
+
+
+def test_fsst_compress_edge_cases(ctx):
+    """Empty input, one string, all-null, long strings, every byte value, strings shorter than
+    the symbols that would match them."""
+    _fsst_gpu_vs_host(ctx, [])
+    _fsst_gpu_vs_host(ctx, [b"a"])
+    _fsst_gpu_vs_host(ctx, [None, None, None])
+    rng = np.random.default_rng(5)
+    long = [bytes(rng.integers(97, 100, int(rng.integers(100, 5000)), dtype=np.uint8)) for _ in range(50)]
+    _fsst_gpu_vs_host(ctx, long + [bytes(range(256))] + [b"ab", b"abc", b"a"] * 30)
+
+
+def test_fsst_compress_bad_offsets(ctx):
+    """Offsets that run backwards or past the bytes are rejected, not read."""
+    heap = np.frombuffer(b"hello world", np.uint8).copy()
+    offs = np.array([0, 5, 3, 11], np.int64)
+    syms, lens = np.array([int.from_bytes(b"lo", "little")], np.uint64), np.array([2], np.uint8)
+    with pytest.raises(V.VortexGpuError, match="offsets"):
+        G.fsst_compress(ctx, _dev(offs), "i64", _dev(heap), 3, syms, lens)
+    with pytest.raises(V.VortexGpuError, match="symbol length"):
+        G.fsst_compress(ctx, _dev(np.array([0, 5], np.int64)), "i64", _dev(heap), 1, syms,
+                        np.array([9], np.uint8))

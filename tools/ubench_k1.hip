@@ -257,6 +257,51 @@ __global__ __launch_bounds__(256) void k_burst(const uint4* __restrict__ in, uin
     }
 }
 
+// K1 with burst reads + wave-contiguous stores: the workgroup reads its 32 blocks' packed bytes
+// into LDS in one burst; then every wave decodes whole blocks, all 64 lanes on one block: in
+// store k, lane group g (8 lanes) produces the row whose 128 output bytes sit at k*1 KiB + g*128
+// of the block, lane t its 16-byte slice -- so each store instruction writes 1 KiB contiguous.
+// The row index (hence the shift) is lane-dependent: runtime shifts on words read from LDS.
+__device__ __forceinline__ int inv_row32(int seg128) {
+    // byte offset of row r (T=32) = FL_ORDER[r/8]*64 + (r%8)*512 -> inverse over 128-B slots
+    const int s = seg128 >> 2, q = seg128 & 3;        // 512-B segment s, 128-B quarter q
+    const int o = (q == 0) ? 0 : (q == 1) ? 2 : (q == 2) ? 1 : 3;  // FL_ORDER[o]*64/128 == q
+    return o * 8 + s;
+}
+template <int NT>
+__global__ __launch_bounds__(256) void k_lds(const uint8_t* __restrict__ packed, uint32_t* __restrict__ out,
+                                             uint64_t n_blocks) {
+    constexpr int BPW = 32;
+    __shared__ __attribute__((aligned(16))) uint8_t s_in[BPW * 128 * W];
+    const uint64_t b0 = uint64_t(blockIdx.x) * BPW;
+    if (b0 >= n_blocks) return;
+    const uint4* src = reinterpret_cast<const uint4*>(packed + b0 * (128 * W));
+    for (int q = threadIdx.x; q < BPW * 8 * W; q += 256) reinterpret_cast<uint4*>(s_in)[q] = src[q];
+    __syncthreads();
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 3, t = lane & 7;
+    for (int b = wave; b < BPW; b += 4) {
+        const uint8_t* blk = s_in + b * 128 * W;
+        uint8_t* dst = reinterpret_cast<uint8_t*>(out) + (b0 + b) * 4096;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int r = inv_row32(k * 8 + g);
+            const int start = r * W, w0 = start >> 5, sh = start & 31;
+            const uint4 lo = *reinterpret_cast<const uint4*>(blk + w0 * 128 + 16 * t);
+            uint4 v;
+            const uint32_t m = (1u << W) - 1u;
+            if (sh + W <= 32) {
+                v = make_uint4((lo.x >> sh) & m, (lo.y >> sh) & m, (lo.z >> sh) & m, (lo.w >> sh) & m);
+            } else {
+                const uint4 hi = *reinterpret_cast<const uint4*>(blk + (w0 + 1) * 128 + 16 * t);
+                const int c = 32 - sh;
+                v = make_uint4(((lo.x >> sh) | (hi.x << c)) & m, ((lo.y >> sh) | (hi.y << c)) & m,
+                               ((lo.z >> sh) | (hi.z << c)) & m, ((lo.w >> sh) | (hi.w << c)) & m);
+            }
+            store_bytes<16, NT>(dst + k * 1024 + 16 * lane, &v);
+        }
+    }
+}
+
 // write-only, wave-contiguous: each wave writes 32 KiB, 1 KiB per instruction, plain stores
 __global__ __launch_bounds__(256) void k_write_wave(uint4* __restrict__ out, uint64_t n16) {
     const uint64_t wave = (uint64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
@@ -316,7 +361,7 @@ int main(int argc, char** argv) {
                              {"memord_nt", 13}, {"memord_plain", 14}, {"xcd_nt", 15}, {"xcd_memord_nt", 16},
                              {"copy_pipe_x4_plain", 17}, {"copy_pipe_x8_plain", 18}, {"copy_pipe_x8_nt", 19},
                              {"tr_plain", 9}, {"tr_nt", 10}, {"burst_plain", 20}, {"burst_nt", 21},
-                             {"write_wave_plain", 22}};
+                             {"write_wave_plain", 22}, {"lds_plain", 23}, {"lds_nt", 24}};
     auto launch = [&](int id, const uint8_t* src) {
         switch (id) {
         case 1: hipLaunchKernelGGL(k_base<1>, dim3(grid_base), dim3(256), 0, 0, src, out, n_blocks); break;
@@ -340,13 +385,15 @@ int main(int argc, char** argv) {
         case 20: hipLaunchKernelGGL(k_burst<0>, dim3(unsigned(n_blocks / 32)), dim3(256), 0, 0, (const uint4*)src, (uint4*)out, n_blocks); break;
         case 21: hipLaunchKernelGGL(k_burst<1>, dim3(unsigned(n_blocks / 32)), dim3(256), 0, 0, (const uint4*)src, (uint4*)out, n_blocks); break;
         case 22: hipLaunchKernelGGL(k_write_wave, dim3(unsigned(out_bytes / 16 / 2048 / 4)), dim3(256), 0, 0, (uint4*)out, out_bytes / 16); break;
+        case 23: hipLaunchKernelGGL(k_lds<0>, dim3(unsigned(n_blocks / 32)), dim3(256), 0, 0, src, out, n_blocks); break;
+        case 24: hipLaunchKernelGGL(k_lds<1>, dim3(unsigned(n_blocks / 32)), dim3(256), 0, 0, src, out, n_blocks); break;
         case 8: hipLaunchKernelGGL(k_write, dim3(cus * 8), dim3(256), 0, 0, (uint4*)out, out_bytes / 16); break;
         }
     };
     std::vector<uint32_t> h_ref(n_vals), h_out(n_vals);
     CK(hipMemcpy(h_ref.data(), ref, out_bytes, hipMemcpyDeviceToHost));
     for (auto& v : vars) {
-        if (v.id == 7 || v.id == 8 || v.id == 12 || (v.id >= 17 && v.id != 9 && v.id != 10)) continue;
+        if (v.id == 7 || v.id == 8 || v.id == 12 || (v.id >= 17 && v.id != 9 && v.id != 10 && v.id < 23)) continue;
         CK(hipMemset(out, 0, out_bytes));
         launch(v.id, in[0]);
         CK(hipDeviceSynchronize());

@@ -202,6 +202,7 @@ GPU_SIGNATURES = {
     "vxg_gather_patches": (ST, [VP, INT, UINT, VP, U64, VP, VP, U64, C.POINTER(U64), VP]),
     "vxg_alp_encode": (ST, [VP, INT, VP, U64, C.POINTER(C.c_uint8), C.POINTER(C.c_uint8), VP, VP, VP, U64,
                             C.POINTER(U64), VP]),
+    "vxg_fsst_compress": (ST, [VP, VP, VP, C.c_uint32, INT, VP, VP, U64, VP, U64, VP, U64, VP, VP, C.POINTER(U64), VP]),
 }
 
 class VxgFileColumn(C.Structure):

@@ -452,6 +452,7 @@ def flatten(a: Array, keep: list) -> _lib.VxgArray:
         bufs = (_lib.VxgBuffer * len(a.buffers))()
         for i, b in enumerate(a.buffers):
             bufs[i].ptr, bufs[i].len = _buf_ptr(b)
+            keep.append(b)  # the device tensor must outlive the node (a Plan replays it)
         keep.append(bufs)
         node.buffers = C.cast(bufs, C.POINTER(_lib.VxgBuffer))
         node.n_buffers = len(a.buffers)

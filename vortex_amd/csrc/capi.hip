@@ -287,6 +287,9 @@ vxg_status make_k1_job(int T, unsigned W, unsigned offset, uint64_t len, const v
     if (reinterpret_cast<uintptr_t>(out) % uint64_t(ow))
         return set_error(VXG_ERR_INVALID_ARGUMENT, "output buffer must be aligned to the value width");
     if (epi == Epi::Dict && W > unsigned(kDictFusedMaxW)) return VXG_ERR_NOT_IMPLEMENTED;
+    // every code is out of bounds of an empty dictionary (whose buffer may be null)
+    if (epi == Epi::Dict && a.dict_len == 0 && len > 0)
+        return set_error(VXG_ERR_OUT_OF_BOUNDS, "take: index out of bounds");
     j.T = T;
     j.W = int(W);
     j.epi = epi;
@@ -2421,6 +2424,20 @@ vxg_status vxg_alp_encode(vxg_ctx* ctx, int float_ptype, const void* values, uin
         return set_error(VXG_ERR_INVALID_ARGUMENT, "null argument");
     return launch_alp_encode(float_ptype, values, n, e, f, encoded, patch_indices, patch_values, cap, n_patches,
                              S(stream));
+}
+
+vxg_status vxg_fsst_compress(vxg_ctx* ctx, const uint64_t* symbols, const uint8_t* symbol_lengths, uint32_t n_symbols,
+                             int offsets_ptype, const void* offsets, const uint8_t* bytes, uint64_t bytes_len,
+                             const uint8_t* validity, uint64_t n, uint8_t* codes, uint64_t codes_cap,
+                             int32_t* code_offsets, int32_t* uncompressed_lengths, uint64_t* codes_len, void* stream) {
+    VXG_TRY(use_device(ctx));
+    if (!codes_len || !code_offsets || (n_symbols && (!symbols || !symbol_lengths)) ||
+        (n && (!offsets || !uncompressed_lengths)) || (bytes_len && !bytes) || (codes_cap && !codes))
+        return set_error(VXG_ERR_INVALID_ARGUMENT, "null argument");
+    if (!ptype_is_int(offsets_ptype)) return set_error(VXG_ERR_MISMATCHED_TYPES, "VarBin offsets must be integers");
+    return launch_fsst_compress(symbols, symbol_lengths, n_symbols, ptype_width(offsets_ptype),
+                                ptype_is_signed(offsets_ptype), offsets, bytes, bytes_len, validity, n, codes, codes_cap,
+                                code_offsets, uncompressed_lengths, codes_len, S(stream));
 }
 
 vxg_status vxg_filter_array(vxg_ctx* ctx, const vxg_array* a, const vxg_array* predicate, vxg_canonical* out,

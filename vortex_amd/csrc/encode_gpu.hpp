@@ -38,4 +38,12 @@ vxg_status launch_gather_patches_gpu(int width, unsigned W, const void* v, uint6
 vxg_status launch_alp_encode(int float_ptype, const void* v, uint64_t n, uint8_t* e, uint8_t* f, void* enc,
                              uint64_t* idx, void* vals, uint64_t cap, uint64_t* count, hipStream_t s);
 
+// K17 (fsst_encode.hip), synchronous: FSST-compress n strings (VarBin offsets of offs_width bytes
+// + bytes, optional LSB validity) with a trained table into codes (i32 offsets, n + 1) and i32
+// uncompressed lengths; *codes_len = code bytes written (at most codes_cap).
+vxg_status launch_fsst_compress(const uint64_t* symbols, const uint8_t* sym_lens, uint32_t n_symbols, int offs_width,
+                                bool offs_signed, const void* offsets, const uint8_t* bytes, uint64_t bytes_len,
+                                const uint8_t* validity, uint64_t n, uint8_t* codes, uint64_t codes_cap,
+                                int32_t* code_offsets, int32_t* ulens, uint64_t* codes_len, hipStream_t s);
+
 }  // namespace vxg

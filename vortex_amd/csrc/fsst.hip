@@ -32,6 +32,8 @@
 
 namespace vxg {
 
+__device__ const uint64_t kNoSymbol[1] = {0};
+
 namespace {
 
 constexpr int kTile = 256;            // strings per tile = threads per workgroup
@@ -333,9 +335,11 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
     // a recorded plan's device table: the workgroup's chunk from the plan's per-workgroup map
     // (one scalar load) instead of the wave-wide count over the table
     const FsstChunk& ch = EXT ? tab.ext[wg_chunk[blockIdx.x]] : fsst_chunk_of<false, EXT>(tab, blockIdx.x);
-    const uint64_t* __restrict__ symbols = ch.symbols;
-    const uint8_t* __restrict__ sym_lens = ch.sym_lens;
     const unsigned n_symbols = ch.n_symbols;
+    // an empty table (no symbols: e.g. trained on null strings only) may have null buffers; the
+    // clamped load below then reads a zero entry here instead
+    const uint64_t* __restrict__ symbols = n_symbols ? ch.symbols : kNoSymbol;
+    const uint8_t* __restrict__ sym_lens = n_symbols ? ch.sym_lens : reinterpret_cast<const uint8_t*>(kNoSymbol);
     const uint8_t* __restrict__ codes = ch.codes;
     const OffAcc code_offs(ch.offs);
     const LenAcc lens(ch.lens);

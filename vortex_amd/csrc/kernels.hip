@@ -260,6 +260,8 @@ static vxg_status take_c(int vw, const void* values, uint64_t nv, const void* co
 vxg_status launch_take(int value_width, const void* values, uint64_t n_values, int code_width, bool code_signed,
                        const void* codes, uint64_t n, void* out, uint32_t* err, hipStream_t s) {
     if (n == 0) return VXG_OK;
+    // every index is out of bounds of an empty array (and its values buffer may be null)
+    if (n_values == 0) return set_error(VXG_ERR_OUT_OF_BOUNDS, "take: index out of bounds");
     switch (code_width * (code_signed ? -1 : 1)) {
     case 1: return take_c<uint8_t>(value_width, values, n_values, codes, n, out, err, s);
     case 2: return take_c<uint16_t>(value_width, values, n_values, codes, n, out, err, s);

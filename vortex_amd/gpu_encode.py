@@ -13,10 +13,16 @@ equal to, byte for byte) and the reference algorithm it cites:
   * `encode_for_bitpacked` -- for_compress (for/compress.rs:13-85) -> BitPacked, fused into one
                               K15 pass when no patches are taken;
   * `encode_alp`           -- ALPFloat::encode with find_best_exponents (alp/mod.rs:51-140) ->
-                              FoR -> BitPacked, exceptions as Sparse patches (alp/compress.rs:38-59).
+                              FoR -> BitPacked, exceptions as Sparse patches (alp/compress.rs:38-59);
+  * `fsst_train`           -- fsst_train_compressor (fsst/compress.rs:46-81): training stays on the
+                              host, as Compressor::train does; only the trainer's sample of the
+                              device column is gathered and copied back;
+  * `encode_fsst`          -- fsst_compress_iter (fsst/compress.rs:83-129): K17 compresses every
+                              string against the table on the GPU (codes VarBin with i32 offsets,
+                              i32 uncompressed lengths).
 
-The only host work is the choice of parameters from the statistics the GPU returns; no value
-passes through host memory.  There is no CPU fallback: without the HIP library this raises.
+The only host work is the choice of parameters from the statistics the GPU returns (and FSST's
+table training on a bounded sample); no value passes through host memory.  There is no CPU fallback: without the HIP library this raises.
 """
 from __future__ import annotations
 
@@ -238,3 +244,81 @@ def encode_alp(ctx, values, ptype: str) -> Array:
         patches = A.sparse(_patch_indices(ctx, idx, m, n), _primitive(pv, ptype, m, "ALL_VALID"), n)
     ip = {"f32": "i32", "f64": "i64"}[ptype]
     return A.alp(encode_for_bitpacked(ctx, enc, ip, allow_patches=True), e, f, patches)
+
+
+def _offsets_host(offsets, offs_ptype: str, n: int) -> np.ndarray:
+    b = _bytes(offsets)[: (n + 1) * ptype_width(offs_ptype)]
+    return b.cpu().numpy().view(NP_OF_PTYPE[offs_ptype]).astype(np.int64)
+
+
+def fsst_train(ctx, offsets, offs_ptype: str, data, n: int):
+    """The host trainer (encode.cpp vxe_fsst_train) over exactly the strings it samples: every
+    (n // 20000)-th string until 1 MiB is read.  Only those strings are gathered on the device
+    and copied back; the table equals the one trained on the whole column in host memory.
+    -> (symbols u64[k], lengths u8[k]) host arrays."""
+    torch = _torch()
+    from .encode import _lib_enc, _p
+    offs = _offsets_host(offsets, offs_ptype, n)
+    step = n // 20000 if n > 20000 else 1
+    picks, sampled = [], 0
+    for i in range(0, n, step):
+        if sampled >= (1 << 20):
+            break
+        picks.append(i)
+        sampled += int(offs[i + 1] - offs[i])
+    picks = np.array(picks, dtype=np.int64)
+    lens = (offs[picks + 1] - offs[picks]) if picks.size else np.zeros(0, np.int64)
+    new_offs = np.zeros(picks.size + 1, np.int64)
+    np.cumsum(lens, out=new_offs[1:])
+    if new_offs[-1]:
+        idx = np.repeat(offs[picks] - new_offs[:-1], lens) + np.arange(new_offs[-1])
+        heap = _bytes(data)[torch.from_numpy(idx).to(_bytes(data).device)].cpu().numpy()
+    else:
+        heap = np.zeros(1, np.uint8)
+    t = _lib.VxeFsstTable()
+    _lib_enc().vxe_fsst_train(_p(heap), _p(new_offs), picks.size, C.byref(t))
+    k = int(t.n_symbols)
+    return np.array(list(t.symbols)[:k], dtype=np.uint64), np.array(list(t.lens)[:k], dtype=np.uint8)
+
+
+def fsst_compress(ctx, offsets, offs_ptype: str, data, n: int, symbols, lengths, validity=None):
+    """vxg_fsst_compress (K17): -> (codes, code_offsets i32[n + 1], uncompressed_lengths i32[n]),
+    device tensors (codes trimmed to the bytes written)."""
+    torch = _torch()
+    d = _bytes(data)
+    syms = np.ascontiguousarray(symbols, dtype=np.uint64)
+    slen = np.ascontiguousarray(lengths, dtype=np.uint8)
+    cap = 2 * d.numel()
+    codes = _empty(ctx, cap)
+    coffs = _empty(ctx, 4 * (n + 1))
+    ulens = _empty(ctx, 4 * n)
+    got = C.c_uint64()
+    vb = _ptr(_bytes(validity)) if validity is not None else C.c_void_p(0)
+    _lib.check(ctx.lib.vxg_fsst_compress(ctx.handle, syms.ctypes.data_as(C.c_void_p), slen.ctypes.data_as(C.c_void_p),
+                                         syms.size, PTYPE[offs_ptype], _ptr(_bytes(offsets)), _ptr(d), d.numel(), vb,
+                                         n, _ptr(codes), cap, _ptr(coffs), _ptr(ulens), C.byref(got), ctx.stream_ptr()))
+    return codes[: got.value], coffs, ulens
+
+
+def encode_fsst(ctx, offsets, offs_ptype: str, data, n: int, validity=None, table=None, utf8: bool = True) -> Array:
+    """fsst_compress (fsst/compress.rs:19-44) of a device-resident VarBin (offsets + bytes,
+    optional LSB validity bits): the table is trained on the host (fsst_train) unless given,
+    every string is compressed on the GPU.  -> FSSTArray(symbols, symbol_lengths,
+    codes = VarBin(i32 offsets, binary), uncompressed_lengths i32) with device buffers, the
+    tree encode.encode_fsst_from_heap(compress_children=False) builds on the host."""
+    torch = _torch()
+    dev = torch.device("cuda", ctx.device)
+    symbols, lengths = table if table is not None else fsst_train(ctx, offsets, offs_ptype, data, n)
+    codes, coffs, ulens = fsst_compress(ctx, offsets, offs_ptype, data, n, symbols, lengths, validity)
+    k = int(np.asarray(symbols).size)
+    sym_t = torch.from_numpy(np.ascontiguousarray(symbols, dtype=np.uint64).view(np.uint8).copy()).to(dev)
+    len_t = torch.from_numpy(np.ascontiguousarray(lengths, dtype=np.uint8).copy()).to(dev)
+    code_vb = A.varbin(_primitive(coffs, "i32", n + 1), _primitive(codes, "u8", int(codes.numel())), utf8=False)
+    if validity is not None:
+        vbits = _bytes(validity)
+        mask = np.unpackbits(vbits.cpu().numpy(), bitorder="little")[:n].astype(bool)
+        if not mask.all():
+            code_vb = A.varbin(_primitive(coffs, "i32", n + 1), _primitive(codes, "u8", int(codes.numel())),
+                               utf8=False, validity=mask)
+    return A.fsst(_primitive(sym_t, "u64", k), _primitive(len_t, "u8", k), code_vb, _primitive(ulens, "i32", n),
+                  utf8=utf8)
