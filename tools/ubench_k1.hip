@@ -302,6 +302,70 @@ __global__ __launch_bounds__(256) void k_lds(const uint8_t* __restrict__ packed,
     }
 }
 
+// lds2: as k_lds, but each wave decodes 8 CONSECUTIVE blocks (32 KiB of contiguous output per
+// wave, like the burst copy) and the row extraction is branch-free: both words are always read
+// and funnel-shifted (v_alignbit), the per-lane row parameters computed once.
+template <int NT>
+__global__ __launch_bounds__(256) void k_lds2(const uint8_t* __restrict__ packed, uint32_t* __restrict__ out,
+                                              uint64_t n_blocks) {
+    constexpr int BPW = 32;
+    __shared__ __attribute__((aligned(16))) uint8_t s_in[BPW * 128 * W + 128];
+    const uint64_t b0 = uint64_t(blockIdx.x) * BPW;
+    if (b0 >= n_blocks) return;
+    const uint4* src = reinterpret_cast<const uint4*>(packed + b0 * (128 * W));
+    for (int q = threadIdx.x; q < BPW * 8 * W; q += 256) reinterpret_cast<uint4*>(s_in)[q] = src[q];
+    __syncthreads();
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, g = lane >> 3, t = lane & 7;
+    int off0[4], sh[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int r = inv_row32(k * 8 + g), start = r * W;
+        off0[k] = (start >> 5) * 128 + 16 * t;
+        sh[k] = start & 31;
+    }
+    const uint32_t m = (1u << W) - 1u;
+#pragma unroll 2
+    for (int j = 0; j < 8; j++) {
+        const int b = wave * 8 + j;
+        const uint8_t* blk = s_in + b * 128 * W;
+        uint8_t* dst = reinterpret_cast<uint8_t*>(out) + (b0 + b) * 4096;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint4 lo = *reinterpret_cast<const uint4*>(blk + off0[k]);
+            const uint4 hi = *reinterpret_cast<const uint4*>(blk + off0[k] + 128);
+            const uint32_t c = uint32_t(sh[k]);
+            uint4 v;
+            v.x = __builtin_amdgcn_alignbit(hi.x, lo.x, c) & m;
+            v.y = __builtin_amdgcn_alignbit(hi.y, lo.y, c) & m;
+            v.z = __builtin_amdgcn_alignbit(hi.z, lo.z, c) & m;
+            v.w = __builtin_amdgcn_alignbit(hi.w, lo.w, c) & m;
+            store_bytes<16, NT>(dst + k * 1024 + 16 * lane, &v);
+        }
+    }
+}
+
+// lds_k1: burst read into LDS, then the engine's K1 decode (8 threads per block, compile-time
+// row extraction, K1 store shape) with the packed words read from LDS instead of HBM
+template <int NT>
+__global__ __launch_bounds__(256) void k_lds_k1(const uint8_t* __restrict__ packed, uint32_t* __restrict__ out,
+                                                uint64_t n_blocks) {
+    constexpr int BPW = 32;
+    __shared__ __attribute__((aligned(16))) uint8_t s_in[BPW * 128 * W];
+    const uint64_t b0 = uint64_t(blockIdx.x) * BPW;
+    if (b0 >= n_blocks) return;
+    const uint4* src = reinterpret_cast<const uint4*>(packed + b0 * (128 * W));
+    for (int q = threadIdx.x; q < BPW * 8 * W; q += 256) reinterpret_cast<uint4*>(s_in)[q] = src[q];
+    __syncthreads();
+    const int b = threadIdx.x >> 3, t = threadIdx.x & 7;
+    Vec16<T> p[W];
+#pragma unroll
+    for (int w = 0; w < W; w++) p[w] = load16<T>(s_in + b * 128 * W + 128 * w + 16 * t);
+    EpiParams ep{};
+    bool oob = false;
+    process_rows<T, W, Epi::Plain, 0, NT, true>(p, t * 4, out, int64_t((b0 + b) * 1024), 1ull << 40, ep, oob,
+                                                std::make_integer_sequence<int, T>{});
+}
+
 // write-only, wave-contiguous: each wave writes 32 KiB, 1 KiB per instruction, plain stores
 __global__ __launch_bounds__(256) void k_write_wave(uint4* __restrict__ out, uint64_t n16) {
     const uint64_t wave = (uint64_t(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
@@ -361,7 +425,8 @@ int main(int argc, char** argv) {
                              {"memord_nt", 13}, {"memord_plain", 14}, {"xcd_nt", 15}, {"xcd_memord_nt", 16},
                              {"copy_pipe_x4_plain", 17}, {"copy_pipe_x8_plain", 18}, {"copy_pipe_x8_nt", 19},
                              {"tr_plain", 9}, {"tr_nt", 10}, {"burst_plain", 20}, {"burst_nt", 21},
-                             {"write_wave_plain", 22}, {"lds_plain", 23}, {"lds_nt", 24}};
+                             {"write_wave_plain", 22}, {"lds_plain", 23}, {"lds_nt", 24},
+                             {"lds2_plain", 25}, {"lds2_nt", 26}, {"lds_k1_plain", 27}, {"lds_k1_nt", 28}};
     auto launch = [&](int id, const uint8_t* src) {
         switch (id) {
         case 1: hipLaunchKernelGGL(k_base<1>, dim3(grid_base), dim3(256), 0, 0, src, out, n_blocks); break;
@@ -387,6 +452,10 @@ int main(int argc, char** argv) {
         case 22: hipLaunchKernelGGL(k_write_wave, dim3(unsigned(out_bytes / 16 / 2048 / 4)), dim3(256), 0, 0, (uint4*)out, out_bytes / 16); break;
         case 23: hipLaunchKernelGGL(k_lds<0>, dim3(unsigned(n_blocks / 32)), dim3(256), 0, 0, src, out, n_blocks); break;
         case 24: hipLaunchKernelGGL(k_lds<1>, dim3(unsigned(n_blocks / 32)), dim3(256), 0, 0, src, out, n_blocks); break;
+        case 25: hipLaunchKernelGGL(k_lds2<0>, dim3(unsigned(n_blocks / 32)), dim3(256), 0, 0, src, out, n_blocks); break;
+        case 26: hipLaunchKernelGGL(k_lds2<1>, dim3(unsigned(n_blocks / 32)), dim3(256), 0, 0, src, out, n_blocks); break;
+        case 27: hipLaunchKernelGGL(k_lds_k1<0>, dim3(unsigned(n_blocks / 32)), dim3(256), 0, 0, src, out, n_blocks); break;
+        case 28: hipLaunchKernelGGL(k_lds_k1<1>, dim3(unsigned(n_blocks / 32)), dim3(256), 0, 0, src, out, n_blocks); break;
         case 8: hipLaunchKernelGGL(k_write, dim3(cus * 8), dim3(256), 0, 0, (uint4*)out, out_bytes / 16); break;
         }
     };
