@@ -104,6 +104,66 @@ def test_bitunpack_with_patches(ctx, T):
     assert_primitive_parity(arr, ctx, vals)
 
 
+# K1w (the large-launch K1: burst LDS staging + wave-contiguous stores) is chosen by launch size;
+# VXG_K1_WAVE=force takes it for every launch so every width, epilogue, offset and tail is
+# compared with the oracle at test sizes.
+@pytest.mark.parametrize("T", [8, 16, 32, 64])
+def test_k1w_every_width(ctx, T, monkeypatch):
+    monkeypatch.setenv("VXG_K1_WAVE", "force")
+    rng = np.random.default_rng(100 + T)
+    dt = UT[T]
+    for W in range(T + 1) if T < 64 else list(range(0, 64, 3)) + [63]:
+        if W == T:
+            continue
+        n = int(rng.integers(1, 40_000))
+        vals = (rng.integers(0, 1 << W, n, dtype=np.uint64) if W else np.zeros(n, np.uint64)).astype(dt)
+        off = int(rng.integers(0, 1024)) if W % 2 else 0
+        assert_primitive_parity(E.encode_bitpacked(vals, bit_width=W, allow_patches=False, offset=off), ctx, vals)
+
+
+def test_k1w_epilogues_and_chunks(ctx, monkeypatch):
+    """FoR / ZigZag / ALP / Dict epilogues, patches, chunked tables (ragged, sliced, unaligned
+    slices) and a plan's device table through K1w."""
+    import torch
+    monkeypatch.setenv("VXG_K1_WAVE", "force")
+    rng = np.random.default_rng(7)
+    cases = []
+    for dt in (np.int8, np.int16, np.int32, np.int64, np.uint32):
+        info = np.iinfo(dt)
+        base = int(info.min) // 2 + 8 if info.min < 0 else 1000
+        cases.append(E.encode_for_bitpacked((base + 4 * rng.integers(0, 25, 9000)).astype(dt)))
+    cases.append(E.encode_zigzag(rng.integers(-500, 500, 20_000).astype(np.int32)))
+    cases.append(E.encode_alp(c_prices(rng, 30_000)))
+    cases.append(E.encode_alp(c_prices(rng, 30_000).astype(np.float32)))
+    for vdt in (np.uint8, np.uint16, np.uint32, np.uint64):
+        pool = rng.integers(0, 200, 300).astype(vdt)
+        cases.append(E.encode_dict(pool[rng.integers(0, pool.size, 25_000)]))
+    cases.append(E.encode_dict_strings([b"row-%d" % (i % 37) for i in range(20_000)]))
+    big = rng.integers(0, 16, 70_000, dtype=np.uint64).astype(np.uint32)
+    big[rng.choice(big.size, 700, replace=False)] = np.iinfo(np.uint32).max
+    cases.append(E.encode_bitpacked(big))
+    cases.append(A.chunked([E.encode_bitpacked(rng.integers(0, 1 << 9, n, dtype=np.uint64).astype(np.uint16),
+                                               bit_width=9, allow_patches=False) for n in (1000, 3, 4097, 70_000)]))
+    cases.append(A.chunked([E.encode_for_bitpacked(rng.integers(-99, 99, n).astype(np.int64)) for n in (5, 2048, 33_333)]))
+    for a in cases:
+        if a.dtype == A.DTYPE["PRIMITIVE"]:
+            assert_primitive_parity(a, ctx)
+        else:
+            assert_string_parity(a, ctx)
+    plan = V.Plan([a.to(torch.device("cuda", 0)) for a in cases[-2:]], ctx)
+    for _ in range(2):
+        res = plan.launch(sync=True)
+        for a, r in zip(cases[-2:], res):
+            assert r.numpy().tobytes() == canon(a)[0].tobytes()
+    plan.close()
+
+
+def c_prices(rng, n):
+    v = np.round(rng.uniform(1, 100000, n) * 100) / 100
+    v[rng.choice(n, n // 500, replace=False)] = rng.uniform(1, 100000, n // 500) + 1e-7
+    return v
+
+
 def test_bitpacked_reference_kat_patch_max(ctx):
     vals = np.array([1, 0, 1, 0, 1, 0, 2 ** 64 - 1], np.uint64)
     arr = E.encode_bitpacked(vals, bit_width=1, validity=[True, False, True, False, True, False, True])
@@ -478,15 +538,70 @@ def test_direct_bitunpack_entry(ctx):
     assert st == 3 and b"packed bytes" in lib.vxg_last_error()
 
 
+def _bench():
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+    import bench
+    return bench
+
+
 def test_full_size_c1_roundtrip(ctx):
-    """BASELINE config 1 at full size (64 Mi u32, W=7): size-independent property checks
-    (exact roundtrip + checksum) on top of a bit-exact oracle comparison."""
+    """BASELINE config 1 at full size (64 Mi u32, W=7, the bench's generator): bit-exact against
+    the oracle's decode of the same packed bytes, plus the size-independent properties
+    (exact roundtrip to the plain values, checksum)."""
     rng = np.random.default_rng(42)
     vals = rng.integers(0, 128, 64 << 20, dtype=np.uint32)
     arr = E.encode_bitpacked(vals, bit_width=7, allow_patches=False)
     got = gpu(arr, ctx).numpy()
+    ref, _ = canon(arr)
+    assert got.tobytes() == ref.tobytes()
     assert got.tobytes() == vals.tobytes()
     assert int(got.astype(np.uint64).sum()) == int(vals.astype(np.uint64).sum())
+
+
+def test_full_size_c2_alp(ctx):
+    """BASELINE config 2 at full size: 64 Mi f64 prices + 0.1 % exceptions (bench generator),
+    ALP -> FoR -> BitPacked(u64) + patches: bit-exact against the oracle and the plain values."""
+    b = _bench()
+    vals = b.c2_values(np.random.default_rng(42), 64 << 20)
+    arr = E.encode_alp(vals)
+    got = gpu(arr, ctx).numpy()
+    assert got.tobytes() == vals.tobytes()
+    assert got.tobytes() == canon(arr)[0].tobytes()
+
+
+def test_full_size_c3_dict_chunks(ctx):
+    """BASELINE config 3 at full size: the 256-chunk Dict(BitPacked u64 W=10) table (128 Mi
+    values), decoded as one plan over a device chunk table and directly; each chunk equals
+    take(values, codes) of its plain data."""
+    import torch
+    b = _bench()
+    plains = [b.c3_chunk_plain(c) for c in range(b.C3_CHUNKS)]
+    arr = A.chunked([b.c3_chunk(c, p) for c, p in enumerate(plains)])
+    dev = arr.to(torch.device("cuda", 0))
+    plan = V.Plan([dev], ctx)
+    got = plan.launch(sync=True)[0].numpy()
+    plan.close()
+    n = b.C3_CHUNK_VALUES
+    for c, (dv, codes) in enumerate(plains):
+        assert got[c * n:(c + 1) * n].tobytes() == dv[codes].tobytes(), c
+    assert V.canonicalize(dev, ctx).numpy().tobytes() == got.tobytes()
+
+
+def test_full_size_c4_fsst(ctx):
+    """BASELINE config 4 at full size: 6 001 215 l_comment-like strings, FSST: the data buffer
+    equals the plain heap, views equal make_view over it (bench.expected_views), and the oracle."""
+    b = _bench()
+    heap, offs = b.c4_heap(np.random.default_rng(42), 6_001_215)
+    arr = E.encode_fsst_from_heap(heap, offs)
+    res = gpu(arr, ctx)
+    views, _ = res.numpy()
+    bufs = res.buffers()
+    assert len(bufs) == 1 and bufs[0].tobytes() == heap.tobytes()
+    assert views.tobytes() == b.expected_views(heap, offs).tobytes()
+    (rviews, rheap), _ = canon(arr)
+    assert views.tobytes() == rviews.tobytes()
 
 
 # ------------------------------------------------------------------ C5: TPC-H lineitem scan

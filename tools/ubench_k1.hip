@@ -305,10 +305,9 @@ __global__ __launch_bounds__(256) void k_lds(const uint8_t* __restrict__ packed,
 // lds2: as k_lds, but each wave decodes 8 CONSECUTIVE blocks (32 KiB of contiguous output per
 // wave, like the burst copy) and the row extraction is branch-free: both words are always read
 // and funnel-shifted (v_alignbit), the per-lane row parameters computed once.
-template <int NT>
+template <int NT, int BPW = 32>
 __global__ __launch_bounds__(256) void k_lds2(const uint8_t* __restrict__ packed, uint32_t* __restrict__ out,
                                               uint64_t n_blocks) {
-    constexpr int BPW = 32;
     __shared__ __attribute__((aligned(16))) uint8_t s_in[BPW * 128 * W + 128];
     const uint64_t b0 = uint64_t(blockIdx.x) * BPW;
     if (b0 >= n_blocks) return;
@@ -325,8 +324,8 @@ __global__ __launch_bounds__(256) void k_lds2(const uint8_t* __restrict__ packed
     }
     const uint32_t m = (1u << W) - 1u;
 #pragma unroll 2
-    for (int j = 0; j < 8; j++) {
-        const int b = wave * 8 + j;
+    for (int j = 0; j < BPW / 4; j++) {
+        const int b = wave * (BPW / 4) + j;
         const uint8_t* blk = s_in + b * 128 * W;
         uint8_t* dst = reinterpret_cast<uint8_t*>(out) + (b0 + b) * 4096;
 #pragma unroll
@@ -419,14 +418,19 @@ int main(int argc, char** argv) {
     }
 
     struct Var { const char* name; int id; };
-    std::vector<Var> vars = {{"base_nt", 1}, {"pipe_nt_x2", 2}, {"pipe_nt_x4", 3}, {"pipe_nt_x8", 4},
+    std::vector<Var> vars_all = {{"base_nt", 1}, {"pipe_nt_x2", 2}, {"pipe_nt_x4", 3}, {"pipe_nt_x8", 4},
                              {"split2_nt", 5}, {"split4_nt", 6}, {"copy_ref_nt", 7}, {"write_only_nt", 8},
                              {"base_plain", 11}, {"copy_ref_plain", 12},
                              {"memord_nt", 13}, {"memord_plain", 14}, {"xcd_nt", 15}, {"xcd_memord_nt", 16},
                              {"copy_pipe_x4_plain", 17}, {"copy_pipe_x8_plain", 18}, {"copy_pipe_x8_nt", 19},
                              {"tr_plain", 9}, {"tr_nt", 10}, {"burst_plain", 20}, {"burst_nt", 21},
                              {"write_wave_plain", 22}, {"lds_plain", 23}, {"lds_nt", 24},
-                             {"lds2_plain", 25}, {"lds2_nt", 26}, {"lds_k1_plain", 27}, {"lds_k1_nt", 28}};
+                             {"lds2_plain", 25}, {"lds2_nt", 26}, {"lds_k1_plain", 27}, {"lds_k1_nt", 28},
+                             {"lds2_nt_bpw16", 29}, {"lds2_nt_bpw64", 30}, {"lds2_nt_bpw8", 31}};
+    std::vector<Var> vars;
+    for (auto& v : vars_all)
+        if (std::getenv("UB_ALL") || v.id == 1 || v.id == 7 || v.id == 20 || v.id == 21 || v.id == 22 || v.id >= 25)
+            vars.push_back(v);
     auto launch = [&](int id, const uint8_t* src) {
         switch (id) {
         case 1: hipLaunchKernelGGL(k_base<1>, dim3(grid_base), dim3(256), 0, 0, src, out, n_blocks); break;
@@ -456,6 +460,9 @@ int main(int argc, char** argv) {
         case 26: hipLaunchKernelGGL(k_lds2<1>, dim3(unsigned(n_blocks / 32)), dim3(256), 0, 0, src, out, n_blocks); break;
         case 27: hipLaunchKernelGGL(k_lds_k1<0>, dim3(unsigned(n_blocks / 32)), dim3(256), 0, 0, src, out, n_blocks); break;
         case 28: hipLaunchKernelGGL(k_lds_k1<1>, dim3(unsigned(n_blocks / 32)), dim3(256), 0, 0, src, out, n_blocks); break;
+        case 29: hipLaunchKernelGGL((k_lds2<1, 16>), dim3(unsigned(n_blocks / 16)), dim3(256), 0, 0, src, out, n_blocks); break;
+        case 30: hipLaunchKernelGGL((k_lds2<1, 64>), dim3(unsigned(n_blocks / 64)), dim3(256), 0, 0, src, out, n_blocks); break;
+        case 31: hipLaunchKernelGGL((k_lds2<1, 8>), dim3(unsigned(n_blocks / 8)), dim3(256), 0, 0, src, out, n_blocks); break;
         case 8: hipLaunchKernelGGL(k_write, dim3(cus * 8), dim3(256), 0, 0, (uint4*)out, out_bytes / 16); break;
         }
     };

@@ -524,7 +524,9 @@ uint64_t vxe_runend_encode(int vw, const void* values, uint64_t n, uint64_t* end
 
 void vxe_fsst_train(const uint8_t* heap, const int64_t* offsets, uint64_t n, vxe_fsst_table* t) {
     // Count substrings of length 1..8 over a bounded sample of strings; pick the 255 with the
-    // largest (count * (len - 1) + count) benefit, greedily discounting overlaps is skipped.
+    // largest gain = count * len, single bytes promoted x8 (the FSST trainer's heuristic that
+    // fsst-rs follows: "promoting single-byte symbols (*8) helps reduce exception rates and
+    // increases [de]compression speed"); greedily discounting overlaps is skipped.
     std::unordered_map<uint64_t, uint64_t> cnt;  // key = len<<56 | bytes (len <= 7) ; len 8 hashed
     std::unordered_map<uint64_t, uint64_t> cnt8;
     uint64_t sampled = 0;
@@ -546,7 +548,7 @@ void vxe_fsst_train(const uint8_t* heap, const int64_t* offsets, uint64_t n, vxe
     std::vector<Cand> c;
     for (auto& kv : cnt) {
         const uint8_t len = uint8_t(kv.first >> 56);
-        c.push_back({kv.first & ((1ull << 56) - 1), len, kv.second * len});
+        c.push_back({kv.first & ((1ull << 56) - 1), len, kv.second * len * (len == 1 ? 8u : 1u)});
     }
     for (auto& kv : cnt8) c.push_back({kv.first, 8, kv.second * 8});
     std::sort(c.begin(), c.end(), [](const Cand& a, const Cand& b) {

@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <type_traits>
 #include <utility>
 
@@ -385,6 +386,171 @@ __device__ __forceinline__ void unpack_chunk(const ChunkDev& c, uint64_t g, uint
     }
 }
 
+// ---------------------------------------------------------------------------- K1w
+// The large-launch K1: burst read + wave-contiguous stores.  Measured on C1 (tools/ubench_k1.hip,
+// profiles/r03_ubench_k1.txt): a copy of C1's bytes whose workgroups first read their whole
+// input into LDS and then write their output 1 KiB per store instruction runs 54.6 us against
+// 59.6 us for the same copy with reads and writes interleaved per wave, and K1 with this shape
+// ran 57.1 us against 60.5 us for the register-resident K1 (whose store instruction writes
+// 8 x 128 B at a 4 KiB stride).  So:
+//   * a workgroup stages the packed words of BPW consecutive blocks of one chunk (~32 KiB) into
+//     LDS with coalesced 16-byte loads, then decodes them: wave v takes BPW/4 consecutive
+//     blocks (a contiguous output range);
+//   * all 64 lanes of a wave work on ONE block at a time: in store k, lane group g (8 lanes)
+//     produces the row whose 128 output bytes are slot 8k + g of the block and lane t its
+//     16-byte slice, so every store instruction writes 1 KiB contiguous (T/8 stores per block);
+//   * the row -- hence the bit offset -- differs per lane group: each 16-byte slice is funnel-
+//     shifted out of the two LDS word rows holding it (runtime shift, per-lane SWAR masks).
+//   * the packed words live in LDS, not VGPRs: T = 64, W = 24 (C2) drops from 110 VGPRs
+//     (4 waves/SIMD) to a few dozen.
+// blocks per workgroup: ~32 KiB of packed words (16 KiB when a dictionary shares the LDS)
+constexpr int kw_bpw(int W, bool lds_dict = false) {
+    const int b = ((lds_dict ? 16 : 32) * 1024) / (128 * (W > 0 ? W : 1));
+    const int b4 = (b / 4) * 4;
+    return b4 < 4 ? 4 : (b4 > 32 ? 32 : b4);
+}
+
+// Row whose 128 output bytes are 128-byte slot q of a block: row r = o*8 + s sits at slot
+// FL_ORDER[o] * T/64 + s * T/8 (fl_index in bytes / 128), and FL_ORDER is its own inverse.
+template <int T>
+__device__ __forceinline__ int kw_row(int q) {
+    constexpr int P = T / 8;
+    const int s = q / P, f = (q % P) * (64 / T);
+    const int o = ((f & 1) << 2) | (f & 2) | (f >> 2);
+    return o * 8 + s;
+}
+
+template <typename U>
+__device__ __forceinline__ U kw_mask(int n) {
+    return n >= int(8 * sizeof(U)) ? ~U(0) : ((U(1) << n) - U(1));
+}
+
+// Row r of this lane's 16-byte lane slice t from a block's packed words in LDS.
+template <int T, int W>
+__device__ __forceinline__ Vec16<T> kw_extract(const uint8_t* blk, int r, int t) {
+    using U = typename Fl<T>::U;
+    constexpr int NV = Vec16<T>::NV;
+    Vec16<T> v;
+    if constexpr (W == 0) {
+#pragma unroll
+        for (int k = 0; k < NV; k++) v.w[k] = 0;
+    } else {
+        const int start = r * W, w0 = start / T, sh = start % T;
+        const Vec16<T> lo = load16<T>(blk + w0 * 128 + 16 * t);  // ds_read_b128
+        if constexpr (W == T) {
+            v = lo;
+        } else {
+            // word w0 + 1 may be the next block's (or the LDS slack): its bits are masked off
+            const Vec16<T> hi = load16<T>(blk + (w0 + 1) * 128 + 16 * t);
+            const int cur = T - sh;                  // bits of the value held by word w0
+            const int nlo = cur < W ? cur : W, nhi = W - nlo;
+            const U mlo = Fl<T>::rep(kw_mask<U>(nlo)), mhi = Fl<T>::rep(kw_mask<U>(nhi));
+            const int hs = cur & (int(8 * sizeof(U)) - 1);  // == cur whenever mhi != 0
+#pragma unroll
+            for (int k = 0; k < NV; k++) v.w[k] = ((lo.w[k] >> sh) & mlo) | ((hi.w[k] & mhi) << hs);
+        }
+    }
+    return v;
+}
+
+template <int T, int W, Epi EPI, int VW, int NT>
+__device__ __forceinline__ void kw_block(const uint8_t* pk, int gq, int t, typename EpiOut<T, EPI, VW>::type* __restrict__ out,
+                                         int64_t out_base, bool full, uint64_t len, const EpiParams& ep, bool& oob) {
+    using E = typename Fl<T>::E;
+    using O = typename EpiOut<T, EPI, VW>::type;
+    constexpr int EPV = 16 / int(sizeof(E));
+#pragma unroll
+    for (int k = 0; k < T / 8; k++) {
+        const int q = 8 * k + gq;
+        const Vec16<T> v = kw_extract<T, W>(pk, kw_row<T>(q), t);
+        const int idx = q * (1024 / T) + t * EPV;  // element index of the slice in the block
+        if (full) {
+            O* dst = out + (out_base + idx);
+            if constexpr (EPI == Epi::Plain) {
+                store_bytes<16, NT>(reinterpret_cast<uint8_t*>(dst), v.w);
+            } else {
+                O o[EPV];
+#pragma unroll
+                for (int j = 0; j < EPV; j++) o[j] = apply_epi<T, EPI, VW>(v.elem(j), ep, oob);
+                store_bytes<EPV * int(sizeof(O)), NT>(reinterpret_cast<uint8_t*>(dst), o);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < EPV; j++) {
+                const int64_t o = out_base + idx + j;
+                if (o >= 0 && uint64_t(o) < len) out[o] = apply_epi<T, EPI, VW>(v.elem(j), ep, oob);
+            }
+        }
+    }
+}
+
+// LDS of a K1w workgroup: the packed words (+ one word row of slack), then (LDSD) the dictionary
+// -- dynamic, sized by the launch to the largest dictionary of its table.
+template <int W, bool LDSD>
+constexpr int kw_packed_lds() {
+    return (W > 0 ? kw_bpw(W, LDSD) * 128 * W : 0) + 128;
+}
+
+template <int T, int W, Epi EPI, int VW, bool LDSD>
+__device__ __forceinline__ void unpack_chunk_w(const ChunkDev& c, uint64_t g, uint32_t* err) {
+    using O = typename EpiOut<T, EPI, VW>::type;
+    constexpr int BPW = kw_bpw(W, LDSD);
+    extern __shared__ __attribute__((aligned(16))) uint8_t k1w_lds[];
+    uint8_t* const s_pk = k1w_lds;
+    EpiParams ep;
+    ep.reference = c.reference;
+    ep.shift = c.shift;
+    ep.alp_a = c.alp_a;
+    ep.alp_b = c.alp_b;
+    ep.dict = c.dict;
+    ep.dict_len = c.dict_len;
+    ep.err = err;
+    if constexpr (LDSD) {  // the whole workgroup is in this chunk
+        uint8_t* const s_dict = k1w_lds + kw_packed_lds<W, LDSD>();
+        stage_dict<VW>(s_dict, c.dict, c.dict_len);
+        ep.dict = s_dict;
+    }
+    const uint64_t blk0 = (g - c.first_group) * BPW;
+    const int nb = c.n_blocks - blk0 < uint64_t(BPW) ? int(c.n_blocks - blk0) : BPW;
+    if constexpr (W > 0) {  // burst: the workgroup's packed words, coalesced 16-byte loads
+        const uint4* src = reinterpret_cast<const uint4*>(c.packed + blk0 * (128 * W));
+        for (int q = threadIdx.x; q < nb * 8 * W; q += 256) reinterpret_cast<uint4*>(s_pk)[q] = src[q];
+    }
+    __syncthreads();
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, gq = lane >> 3, t = lane & 7;
+    O* const out = static_cast<O*>(c.out);
+    const bool aligned = (reinterpret_cast<uintptr_t>(c.out) & 15) == 0;
+    bool oob = false;
+    constexpr int PER = BPW / 4;
+    for (int j = 0; j < PER; j++) {
+        const int b = wave * PER + j;
+        if (b >= nb) break;  // wave-uniform
+        const uint64_t blk = blk0 + b;
+        const int64_t out_base = int64_t(blk * 1024) - int64_t(c.offset);
+        const bool full = c.offset == 0 && (blk + 1) * 1024 <= c.len && aligned;
+        kw_block<T, W, EPI, VW, kOutNT>(s_pk + b * 128 * W, gq, t, out, out_base, full, c.len, ep, oob);
+    }
+    if constexpr (EPI == Epi::Dict)
+        if (oob) __hip_atomic_fetch_or(err, kErrTakeOOB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int T, int W, Epi EPI, int VW, bool LDSD, bool EXT>
+__global__ __launch_bounds__(256) void fl_unpack_w_kernel(ChunkTable tab) {
+    const uint64_t g = blockIdx.x;
+    if constexpr (EXT) {
+        const ChunkDev& c =
+            tab.ext[ext_chunk_index(tab.ext, tab.n, g, [](const ChunkDev& d) { return d.first_group; })];
+        unpack_chunk_w<T, W, EPI, VW, LDSD>(c, g, tab.err);
+    } else {
+        uint32_t lo = 0, hi = tab.n;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (tab.c[mid].first_group <= g) lo = mid; else hi = mid;
+        }
+        unpack_chunk_w<T, W, EPI, VW, LDSD>(tab.c[lo], g, tab.err);
+    }
+}
+
 // EXT: the chunk table is a recorded plan's device table (any length; one wave-wide count
 // finds the chunk) instead of the kernel argument -- a separate instantiation, so the kernarg
 // path keeps its scalar-load code (a runtime branch cost C1 1 %).
@@ -407,6 +573,32 @@ __global__ __launch_bounds__(256) void fl_unpack_kernel(ChunkTable tab) {
 
 // A launch with fewer 32-block workgroups than this uses the row split (S = 4).
 constexpr uint64_t kSplitBelowGroups = 512;
+
+template <int T, int W, Epi EPI, int VW, bool LDSD, bool EXT>
+vxg_status launch_w(ChunkTable tab, hipStream_t s) {
+    constexpr int BPW = kw_bpw(W, LDSD);
+    ChunkDev* cs = tab.ext ? tab.host : tab.c;
+    uint64_t groups = 0, dict_bytes = 0;
+    for (uint32_t k = 0; k < tab.n; k++) {
+        cs[k].first_group = groups;
+        groups += (cs[k].n_blocks + BPW - 1) / BPW;
+        const uint64_t db = (cs[k].dict_len * uint64_t(VW > 0 ? VW : 1) + 15) & ~15ull;
+        dict_bytes = db > dict_bytes ? db : dict_bytes;
+    }
+    if (groups == 0) return VXG_OK;
+    if (groups > 0xFFFFFFFFull) return set_error(VXG_ERR_INVALID_ARGUMENT, "array too long for one launch");
+    const size_t shm = size_t(kw_packed_lds<W, LDSD>()) + (LDSD ? size_t(dict_bytes) : 0);
+    hipLaunchKernelGGL((fl_unpack_w_kernel<T, W, EPI, VW, LDSD, EXT>), dim3(unsigned(groups)), dim3(256), shm, s, tab);
+    return hip_check(hipGetLastError(), "fl_unpack_w_kernel launch");
+}
+
+// VXG_K1_WAVE (diagnostics, read at every launch): "0" keeps the register-resident K1 for large
+// launches too; "force" takes K1w for small launches as well (parity tests of every width).
+inline int k1_wave_mode() {
+    const char* e = std::getenv("VXG_K1_WAVE");
+    if (!e) return 1;
+    return e[0] == '0' ? 0 : (e[0] == 'f' ? 2 : 1);
+}
 
 template <int T, int W, Epi EPI, int VW, bool LDSD, int S, bool EXT = false>
 vxg_status launch_s(ChunkTable tab, hipStream_t s) {
@@ -438,7 +630,17 @@ vxg_status launch_one(const ChunkTable& tab, uint64_t groups32, hipStream_t s) {
             lds = lds && cs[k].dict_len * VW <= uint64_t(kDictLdsBytes) &&
                   (reinterpret_cast<uintptr_t>(cs[k].dict) & 15) == 0;
     }
-    if (tab.ext) {  // device table (plans): one variant, row split where it exists
+    // Dict gathers keep the register-resident K1 by default: C3 (u64 codes W=10, 8-byte values,
+    // dictionary in LDS) measured 0.65 of 8 TB/s with K1w against 0.70 with the row split
+    const int mode = k1_wave_mode();
+    const bool wave = mode == 2 || (mode == 1 && !split && EPI != Epi::Dict);  // large launches: K1w
+    if (tab.ext) {  // device table (plans): K1w, or the row split for small T = 32/64 launches
+        if (wave) {
+            if constexpr (EPI == Epi::Dict) {
+                if (lds) return launch_w<T, W, EPI, VW, true, true>(tab, s);
+            }
+            return launch_w<T, W, EPI, VW, false, true>(tab, s);
+        }
         constexpr int SX = kSplit ? 4 : 1;
         if constexpr (EPI == Epi::Dict) {
             if (lds) return launch_s<T, W, EPI, VW, true, SX, true>(tab, s);
@@ -446,7 +648,13 @@ vxg_status launch_one(const ChunkTable& tab, uint64_t groups32, hipStream_t s) {
         return launch_s<T, W, EPI, VW, false, SX, true>(tab, s);
     }
     if constexpr (kSplit) {
-        if (split) return lds ? launch_s<T, W, EPI, VW, true, 4>(tab, s) : launch_s<T, W, EPI, VW, false, 4>(tab, s);
+        if (split && !wave) return lds ? launch_s<T, W, EPI, VW, true, 4>(tab, s) : launch_s<T, W, EPI, VW, false, 4>(tab, s);
+    }
+    if (wave) {
+        if constexpr (EPI == Epi::Dict) {
+            if (lds) return launch_w<T, W, EPI, VW, true, false>(tab, s);
+        }
+        return launch_w<T, W, EPI, VW, false, false>(tab, s);
     }
     if constexpr (EPI == Epi::Dict) {
         if (lds) return launch_s<T, W, EPI, VW, true, 1>(tab, s);
