@@ -60,7 +60,7 @@ impl Drop for DeviceOutputs {
     }
 }
 
-fn to_host(s: &GpuSession, dptr: *mut c_void, bytes: u64) -> VortexResult<ArrowBuffer> {
+pub(crate) fn to_host(s: &GpuSession, dptr: *mut c_void, bytes: u64) -> VortexResult<ArrowBuffer> {
     let mut h = ptr::null_mut();
     check(unsafe { ffi::vxg_host_alloc(s.raw(), bytes.max(1), &mut h) })?;
     let owner = Arc::new(PinnedHost { ctx: s.raw(), ptr: h });
@@ -73,7 +73,7 @@ fn to_host(s: &GpuSession, dptr: *mut c_void, bytes: u64) -> VortexResult<ArrowB
     Ok(unsafe { ArrowBuffer::from_custom_allocation(nn, bytes as usize, owner) })
 }
 
-fn validity(dtype: &DType, bits: Option<ArrowBuffer>, len: usize) -> VortexResult<Validity> {
+pub(crate) fn validity(dtype: &DType, bits: Option<ArrowBuffer>, len: usize) -> VortexResult<Validity> {
     if !dtype.is_nullable() {
         return Ok(Validity::NonNullable);
     }
@@ -83,7 +83,7 @@ fn validity(dtype: &DType, bits: Option<ArrowBuffer>, len: usize) -> VortexResul
     })
 }
 
-fn bytes_array(b: ArrowBuffer) -> Array {
+pub(crate) fn bytes_array(b: ArrowBuffer) -> Array {
     PrimitiveArray::new(Buffer::from(b), PType::U8, Validity::NonNullable).into_array()
 }
 

@@ -17,6 +17,10 @@
 //! `vxg_meta`) and calls `vxg_canonicalize`.  The outputs come back into pinned host memory and
 //! are handed to Vortex as zero-copy Arrow buffers (`Buffer::from_custom_allocation`).
 //!
+//! A whole-file scan (the reference's `LayoutBatchStream` + `struct_to_arrow`) goes through
+//! [`scan_file`]: the engine's own file reader, one H2D copy per column range, and ONE plan
+//! (HIP graph) canonicalizing every column, instead of per-chunk, per-buffer calls.
+//!
 //! There is no CPU fallback: without a GPU the registered encodings return an error.
 //!
 //! UNTESTED: the build image of this project has no Rust toolchain.  `src/ffi.rs` is generated
@@ -28,12 +32,14 @@ mod encodings;
 pub mod ffi;
 mod flatten;
 mod meta;
+mod scan;
 
 use std::ffi::CStr;
 use std::ptr;
 use std::sync::OnceLock;
 
 pub use encodings::{gpu_context, gpu_encodings, GpuEncoding};
+pub use scan::{scan_file, ColumnInfo, GpuFile};
 use vortex::{Array, Canonical};
 use vortex_error::{vortex_bail, vortex_err, VortexResult};
 

@@ -30,6 +30,24 @@ pub(crate) fn ptype_code(p: PType) -> u8 {
     }
 }
 
+/// Inverse of [`ptype_code`] (the reader's column ptypes).
+pub(crate) fn ptype_of_code(c: u8) -> VortexResult<PType> {
+    Ok(match c {
+        0 => PType::U8,
+        1 => PType::U16,
+        2 => PType::U32,
+        3 => PType::U64,
+        4 => PType::I8,
+        5 => PType::I16,
+        6 => PType::I32,
+        7 => PType::I64,
+        8 => PType::F16,
+        9 => PType::F32,
+        10 => PType::F64,
+        _ => vortex_bail!(InvalidSerde: "unknown ptype code {}", c),
+    })
+}
+
 fn ptype_width(p: PType) -> usize {
     match p {
         PType::U8 | PType::I8 => 1,

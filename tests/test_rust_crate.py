@@ -48,3 +48,20 @@ def test_meta_rs_covers_every_decoded_encoding():
         if name == "VXG_ENC_STRUCT":  # canonical: not decoded by the engine
             continue
         assert f"ffi::{name}" in meta, name
+
+
+def test_scan_rs_uses_the_reader_and_plan_entry_points():
+    """scan.rs (scan_file) drives the batched path: the file reader, one region copy per column,
+    the layout query, and one plan for all columns -- every entry point exists in ffi.rs."""
+    scan = (CRATE / "src" / "scan.rs").read_text()
+    ffi = (CRATE / "src" / "ffi.rs").read_text()
+    needed = ["vxg_file_open", "vxg_file_close", "vxg_file_info", "vxg_file_column_info", "vxg_file_chunk_info",
+              "vxg_file_chunk_offsets", "vxg_file_column_array", "vxg_alloc", "vxg_memcpy_h2d",
+              "vxg_canonical_layout", "vxg_plan_create", "vxg_plan_launch", "vxg_plan_destroy", "vxg_stream_sync"]
+    for name in needed:
+        assert f"ffi::{name}(" in scan, name
+        assert f"pub fn {name}(" in ffi, name
+    lib = (CRATE / "src" / "lib.rs").read_text()
+    assert "mod scan;" in lib and "scan_file" in lib
+    meta = (CRATE / "src" / "meta.rs").read_text()
+    assert "fn ptype_of_code" in meta

@@ -7,5 +7,5 @@ TAG="$1"; WL="$2"; shift 2
 mkdir -p "$ROOTDIR/gpurun_out"
 cd /tmp && export TMPDIR=/tmp
 timeout -s KILL 120 rocprofv3 --pmc "$@" --output-format csv -d "$ROOTDIR/gpurun_out/pmc_$TAG" -o run -- \
-    python "$ROOTDIR/bench.py" --workloads "$WL" --steps 3 --warmup 1 --no-cpu-baseline \
+    python "$ROOTDIR/bench.py" --workloads "$WL" --steps 3 --warmup 1 --no-cpu-baseline --no-verify \
     > "$ROOTDIR/gpurun_out/pmc_$TAG.out" 2> "$ROOTDIR/gpurun_out/pmc_$TAG.err"

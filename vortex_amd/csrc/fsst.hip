@@ -36,13 +36,24 @@ __device__ const uint64_t kNoSymbol[1] = {0};
 
 namespace {
 
-constexpr int kTile = 256;            // strings per tile = threads per workgroup
-// LDS images sized for short strings (TPC-H l_comment: 10-43 bytes, a 256-string tile is
-// ~6.9 KB decoded / ~2.3 KB of codes).  ~18.9 KB of LDS per workgroup keeps 8 workgroups
-// resident per CU.  Larger tiles take the direct path.
-constexpr int kCodeLds = 6 * 1024;    // staged code bytes per tile
-constexpr int kHeapLds = 10 * 1024;   // staged output bytes per tile
-constexpr int kScanTiles = 128;       // tiles per pre-pass workgroup (= 32 FastLanes blocks)
+constexpr int kTile = 256;            // threads per workgroup
+#ifndef FSST_SPT
+#define FSST_SPT 1
+#endif
+// Strings per thread: a tile of kTS strings is one workgroup.  The decode of a tile is a chain
+// of dependent phases (prologue loads, length scan, staging, two code passes with a scan between,
+// copy-out); C4's SQ counters park 64 % of wave cycles on waits / barriers.  Two strings per
+// thread (twice the work per chain, 27 KiB of LDS) measured 112 us on C4 against 109 us for one,
+// so one it is (profiles/r03_fsst_spt.md); the generalisation stays for other string shapes.
+constexpr int kSPT = FSST_SPT;
+constexpr int kTS = kTile * kSPT;     // strings per tile
+// LDS images sized for short strings (TPC-H l_comment: 10-43 bytes, a 512-string tile is
+// ~13.6 KB decoded / ~4.5 KB of codes).  Larger tiles take the direct path.
+constexpr int kCodeLds = kSPT == 1 ? 6 * 1024 : 8 * 1024;    // staged code bytes per tile
+constexpr int kHeapLds = kSPT == 1 ? 10 * 1024 : 16 * 1024;  // staged output bytes per tile
+constexpr int kTPB = 1024 / kTS;      // tiles per FastLanes block of lengths (kSPT <= 4)
+constexpr int kScanTiles = 32 * kTPB; // tiles per pre-pass workgroup (= 32 FastLanes blocks)
+static_assert(kSPT == 1 || kSPT == 2 || kSPT == 4, "1, 2 or 4 strings per thread");
 constexpr int kMaxDw = (kCodeLds / kTile + 3) / 4;  // code dwords per thread in the decode
 static_assert(kMaxDw * 4 * kTile >= kCodeLds, "segments must cover the staged codes");
 
@@ -174,9 +185,9 @@ __device__ __forceinline__ int block_excl_scan32(int v, int* ws, int& total) {
 // first kScanTiles threads, read before the pre-pass's barrier.
 __device__ __forceinline__ int64_t tile_code_end(const FsstChunk& c, uint64_t sb) {
     const uint64_t tt = sb * kScanTiles + threadIdx.x;
-    const uint64_t n_tiles = (c.n + kTile - 1) / kTile;
+    const uint64_t n_tiles = (c.n + kTS - 1) / kTS;
     if (threadIdx.x >= kScanTiles || tt >= n_tiles) return 0;
-    const uint64_t e = (tt + 1) * kTile < c.n ? (tt + 1) * kTile : c.n;
+    const uint64_t e = (tt + 1) * kTS < c.n ? (tt + 1) * kTS : c.n;
     return intcol_get(c.offs, e);
 }
 
@@ -214,7 +225,7 @@ __device__ __forceinline__ const FsstChunk& fsst_chunk_of(const FsstTable& tab, 
     }
 }
 
-// Any length column: wave w sums tile 4r + w in round r (4 consecutive lengths per lane).
+// Any length column: wave w sums tile 4r + w in round r (kTS / 64 consecutive lengths per lane).
 template <class LenAcc, bool EXT>
 __global__ __launch_bounds__(kTile) void fsst_tile_scan(FsstTable tab, int64_t* __restrict__ tile_prefix_all,
                                                         int64_t* __restrict__ block_totals_all,
@@ -224,19 +235,20 @@ __global__ __launch_bounds__(kTile) void fsst_tile_scan(FsstTable tab, int64_t* 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const FsstChunk& c = fsst_chunk_of<true, EXT>(tab, blockIdx.x);
     const LenAcc lens(c.lens);
-    const uint64_t n = c.n, n_tiles = (n + kTile - 1) / kTile, sb = blockIdx.x - c.first_scan;
+    const uint64_t n = c.n, n_tiles = (n + kTS - 1) / kTS, sb = blockIdx.x - c.first_scan;
     int64_t* const tile_prefix = tile_prefix_all + c.first_tile;
     int64_t* const block_totals = block_totals_all + c.first_scan;
     const int64_t code_end = tile_code_end(c, sb);
     const uint64_t t0 = sb * kScanTiles;
+    constexpr int PL = kTS / 64;  // lengths per lane per tile
     for (int r0 = 0; r0 < kScanTiles / 4; r0 += 8) {
         int64_t v[8];
 #pragma unroll
         for (int r = 0; r < 8; r++) {  // 32 independent loads in flight per lane
-            const uint64_t base = (t0 + 4 * (r0 + r) + wave) * kTile + 4 * lane;
+            const uint64_t base = (t0 + 4 * (r0 + r) + wave) * kTS + PL * lane;
             int64_t acc = 0;
 #pragma unroll
-            for (int e = 0; e < 4; e++) {
+            for (int e = 0; e < PL; e++) {
                 const uint64_t i = base + e;
                 const int64_t x = lens(i < n ? i : n - 1);
                 acc += i < n ? x : 0;
@@ -255,8 +267,8 @@ __global__ __launch_bounds__(kTile) void fsst_tile_scan(FsstTable tab, int64_t* 
 
 // Patch-free FoR(BitPacked u32/i32) lengths with offset 0 (the reference cascade): decode
 // whole FastLanes blocks K1-style (8 threads per block, W x 16-byte loads, SWAR rows).  Row R
-// of a block holds strings (R % 8) * 128 + ..., i.e. tile (R % 8) / 2 of the block, so each
-// thread accumulates 4 tile partial sums, reduced across its 8 threads.
+// of a block holds strings (R % 8) * 128 + ..., i.e. tile (R % 8) * 128 / kTS of the block, so
+// each thread accumulates kTPB tile partial sums, reduced across its 8 threads.
 template <int W, int... Rs>
 __device__ __forceinline__ void fl32_tile_rows(const Vec16<32>* p, int t, uint64_t blk0, uint64_t n, uint32_t shift,
                                                uint32_t reference, bool sgn, int64_t* acc,
@@ -269,7 +281,7 @@ __device__ __forceinline__ void fl32_tile_rows(const Vec16<32>* p, int t, uint64
         for (int j = 0; j < 4; j++) {
             const uint32_t u = uint32_t(v.elem(j) << shift) + reference;
             const int64_t x = sgn ? int64_t(int32_t(u)) : int64_t(u);
-            acc[(R % 8) / 2] += blk0 + uint64_t(idx0 + j) < n ? x : 0;
+            acc[(R % 8) * 128 / kTS] += blk0 + uint64_t(idx0 + j) < n ? x : 0;
         }
     };
     (row(std::integral_constant<int, Rs>{}), ...);
@@ -286,12 +298,14 @@ __global__ __launch_bounds__(kTile) void fsst_tile_scan_fl32(FsstTable tab, int6
     const uint8_t* __restrict__ packed = static_cast<const uint8_t*>(c.lens.p);
     const uint32_t shift = c.lens.shift, reference = uint32_t(c.lens.reference);
     const bool sgn = c.lens.sgn;
-    const uint64_t n = c.n, n_tiles = (n + kTile - 1) / kTile, sb = blockIdx.x - c.first_scan;
+    const uint64_t n = c.n, n_tiles = (n + kTS - 1) / kTS, sb = blockIdx.x - c.first_scan;
     int64_t* const tile_prefix = tile_prefix_all + c.first_tile;
     int64_t* const block_totals = block_totals_all + c.first_scan;
-    const uint64_t blk = sb * (kScanTiles / 4) + (tid >> 3);
+    const uint64_t blk = sb * 32 + (tid >> 3);
     const int64_t code_end = tile_code_end(c, sb);
-    int64_t acc[4] = {0, 0, 0, 0};
+    int64_t acc[kTPB];
+#pragma unroll
+    for (int k = 0; k < kTPB; k++) acc[k] = 0;
     if (blk * 1024 < n) {
         Vec16<32> p[W > 0 ? W : 1];
         if constexpr (W > 0) {
@@ -301,13 +315,13 @@ __global__ __launch_bounds__(kTile) void fsst_tile_scan_fl32(FsstTable tab, int6
         fl32_tile_rows<W>(p, t, blk * 1024, n, shift, reference, sgn, acc, std::make_integer_sequence<int, 32>{});
     }
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
+    for (int k = 0; k < kTPB; k++) {
 #pragma unroll
         for (int d = 1; d < 8; d <<= 1) acc[k] += __shfl_xor(acc[k], d, 64);
     }
     if (t == 0) {
 #pragma unroll
-        for (int k = 0; k < 4; k++) s_ts[(tid >> 3) * 4 + k] = acc[k];
+        for (int k = 0; k < kTPB; k++) s_ts[(tid >> 3) * kTPB + k] = acc[k];
     }
     __syncthreads();
     scan_tile_sums(s_ts, ws, n_tiles, sb, tile_prefix, block_totals, tile_code_all + c.first_tile, code_end);
@@ -366,12 +380,14 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
     }
     // Prologue: every global load is unconditional (indices clamped, results selected
     // afterwards) so they retire under one wait.
-    const uint64_t first = uint64_t(tile) * kTile;
-    const uint64_t i = first + tid;
-    const bool live = i < n;
-    const uint64_t ii = live ? i : n - 1;
-    const int64_t len_v = lens(ii);
-    const uint8_t vbyte = validity ? validity[ii >> 3] : uint8_t(0xFF);
+    // thread tid owns strings i0 .. i0 + kSPT - 1 of the tile
+    const uint64_t first = uint64_t(tile) * kTS;
+    const uint64_t i0 = first + uint64_t(tid) * kSPT;
+    int64_t len_v[kSPT];
+#pragma unroll
+    for (int j = 0; j < kSPT; j++) len_v[j] = lens(i0 + j < n ? i0 + j : n - 1);
+    // kSPT divides 8 and i0 is a multiple of kSPT: the thread's validity bits share one byte
+    const uint8_t vbyte = validity ? validity[(i0 < n ? i0 : n - 1) >> 3] : uint8_t(0xFF);
     const int64_t tp = tile_prefix[tile];
     // the tile's code range [cf, cl) (absolute offsets into `codes`) from the pre-pass records
     // (uniform loads, L2-resident), so the code bytes below are requested in this same round
@@ -385,12 +401,19 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
     const int span = span_ok ? int(span64) : 0;  // tile codes at s_codes[0, span) once staged
     const uint4* const a0 = reinterpret_cast<const uint4*>(ga - uintptr_t(cshift));
     const int nchunk = (span + 15) >> 4;
-    // chunk `tid` of the staged image: two aligned 16-byte loads (an aligned chunk that holds a
-    // tile byte never crosses a page, so it is read whole), funnel-shifted when written
-    uint4 cx = make_uint4(0, 0, 0, 0), cy = make_uint4(0, 0, 0, 0);
-    if (tid < nchunk) {
-        cx = a0[tid];
-        if (cshift != 0 && 16 * (tid + 1) - cshift < span) cy = a0[tid + 1];
+    // chunks tid + 256 p (p < kSPT) of the staged image: two aligned 16-byte loads each (an
+    // aligned chunk that holds a tile byte never crosses a page, so it is read whole),
+    // funnel-shifted when written
+    uint4 cx[kSPT], cy[kSPT];
+#pragma unroll
+    for (int p = 0; p < kSPT; p++) {
+        const int q = tid + kTile * p;
+        cx[p] = make_uint4(0, 0, 0, 0);
+        cy[p] = make_uint4(0, 0, 0, 0);
+        if (q < nchunk) {
+            cx[p] = a0[q];
+            if (cshift != 0 && 16 * (q + 1) - cshift < span) cy[p] = a0[q + 1];
+        }
     }
     if (wave == 0) {  // prefix of the preceding scan blocks (<= a few hundred totals), one wave
         // four loads per lane in flight per round (clamped index, no per-element branch), so a
@@ -410,22 +433,27 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
         acc = wave_sum(acc);
         if (lane == 0) s_block_prefix = acc;
     }
-    const int64_t my_len = live ? len_v : 0;
+    int64_t my_len[kSPT];
+    int64_t my_sum = 0;
+    bool bad = false;
+#pragma unroll
+    for (int j = 0; j < kSPT; j++) {
+        my_len[j] = i0 + j < n ? len_v[j] : 0;
+        bad |= my_len[j] < 0 || my_len[j] > kHeapLds;
+        my_sum += my_len[j];
+    }
 
     // (a) length scan: int32 with DPP when every length is in [0, kHeapLds] (then a staged
     // tile is possible), int64 otherwise (direct path).
-    const bool bad = my_len < 0 || my_len > kHeapLds;
+    bad |= my_sum > kHeapLds;
     const unsigned long long bm = __ballot(bad);
     if (lane == 0) ws_bad[wave] = bm != 0;
     int t32;
-    const int rel32 = block_excl_scan32(bad ? 0 : int(my_len), ws_a, t32);
+    const int rel32 = block_excl_scan32(bad ? 0 : int(my_sum), ws_a, t32);
     const bool any_bad = (ws_bad[0] | ws_bad[1] | ws_bad[2] | ws_bad[3]) != 0;
     int64_t my_rel = rel32, tile_total = t32;
-    if (any_bad) my_rel = block_exclusive_scan<kTile / 64>(my_len, ws64, tile_total);  // uniform branch
+    if (any_bad) my_rel = block_exclusive_scan<kTile / 64>(my_sum, ws64, tile_total);  // uniform branch
     const int64_t tile_out0 = tp + s_block_prefix;
-
-    const bool valid = live && ((vbyte >> (ii & 7)) & 1);
-    const uint32_t vlen = valid ? uint32_t(my_len) : 0u;
     const bool stage = !any_bad && span_ok && tile_total <= kHeapLds;
 
     if (stage) {
@@ -435,8 +463,11 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
         const int hshift = int((reinterpret_cast<uintptr_t>(heap) + tile_out0) & 15);  // image byte hshift = heap[tile_out0]
         const int ttot = int(tile_total);
         {
-            if (tid < nchunk) *reinterpret_cast<uint4*>(s_codes + 16 * tid) = funnel16(cx, cy, cshift);
-            for (int q = tid + kTile; q < nchunk; q += kTile) {
+#pragma unroll
+            for (int p = 0; p < kSPT; p++)
+                if (tid + kTile * p < nchunk)
+                    *reinterpret_cast<uint4*>(s_codes + 16 * (tid + kTile * p)) = funnel16(cx[p], cy[p], cshift);
+            for (int q = tid + kTile * kSPT; q < nchunk; q += kTile) {
                 const uint4 x = a0[q];
                 uint4 y = make_uint4(0, 0, 0, 0);
                 if (cshift != 0 && 16 * (q + 1) - cshift < span) y = a0[q + 1];
@@ -603,44 +634,59 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
                 }
             }
         }
-        if (live)
-            views[i] = valid ? lds_view(s_heap32, hshift + int(my_rel), vlen, uint32_t(tile_out0 + my_rel), bidx)
-                             : make_uint4(0, 0, 0, 0);
+        int64_t rel = my_rel;
+#pragma unroll
+        for (int j = 0; j < kSPT; j++) {
+            const uint64_t i = i0 + j;
+            if (i < n) {
+                const bool valid = (vbyte >> (i & 7)) & 1;
+                views[i] = valid ? lds_view(s_heap32, hshift + int(rel), uint32_t(my_len[j]), uint32_t(tile_out0 + rel), bidx)
+                                 : make_uint4(0, 0, 0, 0);
+            }
+            rel += my_len[j];
+        }
     } else {
         // direct path: per-string decode straight into HBM (codes of string i are
         // [offs[i], offs[i+1]); each must decode to exactly lengths[i] bytes)
-        const int64_t my_c0 = live ? code_offs(ii) : 0;
-        const int64_t my_c1 = live ? code_offs(ii + 1) : 0;
-        const uint8_t* gcodes = codes;
         int64_t o = tile_out0 + my_rel;
-        const int64_t o_start = o, o_end = o + my_len;
-        for (int64_t k = my_c0; k < my_c1; k++) {
-            const uint8_t c = gcodes[k];
-            if (c == 255) {
-                ++k;
-                if (o < o_end) heap[o] = gcodes[k];
-                o++;
-            } else {
-                const uint64_t sym = s_sym[c];
-                const int L = s_len[c];
-                for (int b = 0; b < L; b++)
-                    if (o + b < o_end) heap[o + b] = uint8_t(sym >> (8 * b));
-                o += L;
+        for (int j = 0; j < kSPT; j++) {
+            const uint64_t i = i0 + j;
+            const bool live = i < n;
+            const int64_t my_c0 = live ? code_offs(i) : 0;
+            const int64_t my_c1 = live ? code_offs(i + 1) : 0;
+            const uint8_t* gcodes = codes;
+            const int64_t o_start = o, o_end = o + my_len[j];
+            for (int64_t k = my_c0; k < my_c1; k++) {
+                const uint8_t c = gcodes[k];
+                if (c == 255) {
+                    ++k;
+                    if (o < o_end) heap[o] = gcodes[k];
+                    o++;
+                } else {
+                    const uint64_t sym = s_sym[c];
+                    const int L = s_len[c];
+                    for (int b = 0; b < L; b++)
+                        if (o + b < o_end) heap[o + b] = uint8_t(sym >> (8 * b));
+                    o += L;
+                }
             }
-        }
-        if (o != o_end) __hip_atomic_fetch_or(err, kErrFsst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (live) {
-            const uint8_t* hp = heap + o_start;
-            views[i] = valid ? build_view(vlen, uint32_t(o_start), bidx,
-                                          [&](int j) { return uint32_t(j) < vlen ? hp[j] : uint8_t(0); })
-                             : make_uint4(0, 0, 0, 0);
+            if (o != o_end) __hip_atomic_fetch_or(err, kErrFsst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            o = o_end;
+            if (live) {
+                const bool valid = (vbyte >> (i & 7)) & 1;
+                const uint32_t vlen = valid ? uint32_t(my_len[j]) : 0u;
+                const uint8_t* hp = heap + o_start;
+                views[i] = valid ? build_view(vlen, uint32_t(o_start), bidx,
+                                              [&](int b) { return uint32_t(b) < vlen ? hp[b] : uint8_t(0); })
+                                 : make_uint4(0, 0, 0, 0);
+            }
         }
     }
 }
 
 uint64_t fsst_scratch_bytes(uint64_t n) {
     // tile prefixes + scan-block totals + tile code ends
-    const uint64_t n_tiles = (n + kTile - 1) / kTile;
+    const uint64_t n_tiles = (n + kTS - 1) / kTS;
     return (2 * n_tiles + (n_tiles + kScanTiles - 1) / kScanTiles + 2) * sizeof(int64_t);
 }
 
@@ -689,7 +735,7 @@ vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint
                              DevTables* dt) {
     for (const FsstChunk& c : chunks) {
         if (c.n_symbols > 255) return set_error(VXG_ERR_INVALID_ARGUMENT, "FSST symbol table > 255 entries");
-        if ((c.n + kTile - 1) / kTile > 0xFFFFFFFFull) return set_error(VXG_ERR_INVALID_ARGUMENT, "FSST array too long");
+        if ((c.n + kTS - 1) / kTS > 0xFFFFFFFFull) return set_error(VXG_ERR_INVALID_ARGUMENT, "FSST array too long");
         if (acc_kind(c.offs) == 0 || acc_kind(c.lens) == 0 || (c.offs.packed && c.offs.width != 4 && c.offs.width != 8) ||
             (c.lens.packed && c.lens.width != 4 && c.lens.width != 8))
             return set_error(VXG_ERR_MISMATCHED_TYPES, "FSST offsets/lengths must be 1/2/4/8-byte integers "
@@ -718,7 +764,7 @@ vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint
             if (chunks[k].n == 0) continue;
             FsstChunk& c = cs[tab.n++];
             c = chunks[k];
-            const uint64_t nt = (c.n + kTile - 1) / kTile;
+            const uint64_t nt = (c.n + kTS - 1) / kTS;
             c.first_tile = tiles;
             c.first_scan = scans;
             tiles += nt;
@@ -732,7 +778,7 @@ vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint
                 if (st != VXG_OK) return st;
                 for (uint32_t k = 0; k < tab.n; k++) {
                     const FsstChunk& c = cs[k];
-                    const uint64_t nt = (c.n + kTile - 1) / kTile;
+                    const uint64_t nt = (c.n + kTS - 1) / kTS;
                     for (uint64_t t = 0; t < nt; t++) host_map[c.first_tile + t] = k;
                 }
             }
