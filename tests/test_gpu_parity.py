@@ -512,6 +512,27 @@ def test_fsst_inconsistent_lengths_is_an_error(ctx):
     assert ei.value.kind == "InvalidArgument"
 
 
+@pytest.mark.parametrize("escapes", [False, True])
+def test_fsst_segment_sizes(ctx, escapes):
+    # one-byte symbols: tile t's code span is 256 x its string length, so the staged tiles cover
+    # every segment size of the decode (1..6 dwords per thread, spans 0.5..5.6 KB); with escapes
+    # some tiles take the general path, and tails that end inside a segment are padded
+    rng = np.random.default_rng(5 + escapes)
+    alphabet = b"abcdefghij "
+    strings = []
+    for t, L in enumerate([2, 6, 10, 14, 18, 22, 3, 21, 0, 7]):
+        for i in range(256):
+            s = bytes(rng.choice(np.frombuffer(alphabet, np.uint8), L))
+            if escapes and t % 2 == 1 and i % 37 == 5 and L:
+                s = s[:-1] + b"\xf7"  # not a symbol: escaped
+            strings.append(None if (i % 53 == 11) else s)
+    strings += [b"jade"] * 77  # a partial last tile
+    arr = _fsst_handmade(strings, [bytes([c]) for c in alphabet])
+    codes = arr.children[2].children[1].buffers[0]
+    assert ((codes == 255).any()) == escapes
+    assert_string_parity(arr, ctx, strings)
+
+
 def test_fsst_long_strings_direct_path(ctx):
     # strings large enough that a 256-string tile overflows the LDS images
     rng = np.random.default_rng(1)

@@ -1,24 +1,28 @@
 #!/bin/bash
-# One iteration on the GPU box: the -m gpu suite, then bench workloads ($2, default c5) and the
-# per-column C5 isolation.  Usage: tools/gpu_iter.sh TAG [workloads]
+# Iteration session: a subset of the -m gpu suite (pytest -k EXPR), bench over the given workloads
+# (N=1 and the simulated 8-GPU shard), then one SQ counter pass over the same workloads.
+#   tools/gpu_iter.sh TAG "pytest -k expr" c4,c5 [sq]
 set -o pipefail
 ROOTDIR="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+cd "$ROOTDIR"
 O="$ROOTDIR/gpurun_out"; mkdir -p "$O"
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-TAG="${1:-iter}"; WL="${2:-c5}"
-cd "$ROOTDIR" && \
-timeout -k 10 400 python -u -m pytest tests -x -q --timeout 120 --timeout-method thread -m gpu -p no:cacheprovider > "$O/${TAG}_gpu.log" 2>&1; rc=$?
-echo "gpu suite exit $rc"; tail -3 "$O/${TAG}_gpu.log"
-[ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python -u bench.py --workloads "$WL" --no-cpu-baseline > "$O/${TAG}_bench.jsonl" 2> "$O/${TAG}_bench.err" || { echo "bench failed"; tail -5 "$O/${TAG}_bench.err"; exit 1; }
-timeout -k 10 300 python -u tools/c5_columns.py --reps 20 > "$O/${TAG}_cols.jsonl" 2> "$O/${TAG}_cols.err" || { echo "cols failed"; exit 1; }
-python - "$O/${TAG}_bench.jsonl" "$O/${TAG}_cols.jsonl" <<'PY'
+TAG="$1"; K="$2"; WL="$3"; SQ="${4:-}"
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q -k "$K" --timeout 120 --timeout-method thread -p no:cacheprovider > "$O/pytest_$TAG.log" 2>&1
+rc=$?; echo "pytest exit $rc"; tail -3 "$O/pytest_$TAG.log"
+[ $rc -eq 0 ] || exit 3
+timeout -k 10 300 python -u bench.py --workloads "$WL" --no-cpu-baseline > "$O/bench_$TAG.json" 2> "$O/bench_$TAG.err" || exit 4
+timeout -k 10 300 python -u bench.py --workloads "$WL" --no-cpu-baseline --simulate-world 8 > "$O/bench_sim8_$TAG.json" 2> "$O/bench_sim8_$TAG.err" || exit 5
+python - "$O/bench_$TAG.json" "$O/bench_sim8_$TAG.json" <<'PY'
 import json, sys
-for l in open(sys.argv[1]):
-    try: d = json.loads(l)
-    except Exception: continue
-    for k, v in (d.get("encodings") or {}).items():
-        print("bench", k, v.get("ms_per_step"), v.get("kernel_ms_median"), v.get("hbm_frac_algorithmic"))
-for l in open(sys.argv[2]):
-    d = json.loads(l); print(d["column"], d.get("ms"), d.get("plan_ms"), d.get("plan_hbm_frac"))
+for f in sys.argv[1:]:
+    d = json.loads(open(f).read().strip().splitlines()[-1])
+    for k, v in d["encodings"].items():
+        print(f"{f.split('/')[-1]:28s} {k} kernel_ms {v['kernel_ms_mean']:.4f} frac {v['hbm_frac_algorithmic']} verified {v.get('verified')}")
 PY
+if [ -n "$SQ" ]; then
+  cd /tmp && export TMPDIR=/tmp
+  timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE --output-format csv -d "$O/pmc_sq_$TAG" -o run -- python "$ROOTDIR/bench.py" --workloads "$WL" --steps 3 --warmup 1 --no-cpu-baseline --no-verify > /dev/null 2> "$O/pmc_sq_$TAG.err" || exit 6
+  timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_$TAG" -o run -- python "$ROOTDIR/bench.py" --workloads "$WL" --steps 20 --warmup 5 --no-cpu-baseline --no-verify > /dev/null 2> "$O/prof_$TAG.err" || exit 7
+fi
+echo "iter done"

@@ -24,7 +24,7 @@ def main():
     ctx = V.Context(0)
     (_, host, c0, c1), info = bench.make_c5(np.random.default_rng(42), world, 0)
     wl = bench.FileWorkload(host, ctx, c0, c1)  # C5 as bench runs it: reader-built trees, one plan
-    plan = wl.plan
+    plan = wl.plans[0]
     for _ in range(5):
         plan.launch()
     ctx.sync()

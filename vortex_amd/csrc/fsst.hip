@@ -12,13 +12,14 @@
 //   kernel 2 (scan_blocks): exclusive tile prefix inside 1024-tile blocks + one total per block
 //   kernel 3 (decode):      per tile, in LDS:
 //     (a) block prefix (one wave) + block scan of the lengths -> each string's offset;
-//     (b) the tile's code bytes staged with aligned 16-byte loads;
-//     (c) CODE-parallel decode: thread t takes 16-byte-aligned segments of the code bytes
-//         (not one string: per-string loops ran as long as the longest of 64 strings and were
-//         VALU-issue bound).  Pass 1 sums the decoded length of the codes starting in the
-//         segment, a block scan places every segment, pass 2 ORs each code's <= 8 bytes into a
-//         zeroed LDS image (ds_or_b32 into <= 3 dwords).  An escape (255) emits the next byte;
-//         a segment that starts inside a run of 255s finds its parity by counting back;
+//     (b) the tile's code bytes staged with aligned 16-byte loads, 0xFF-padded, escapes flagged;
+//     (c) CODE-parallel decode: thread t takes a segment of ND dwords of the code bytes (not
+//         one string: per-string loops ran as long as the longest of 64 strings and were
+//         VALU-issue bound; ND per tile, the segment code templated on it, branch-free).
+//         Pass 1 sums the decoded length of the codes starting in the segment, a block scan
+//         places every segment, pass 2 ORs each code's <= 8 bytes into a zeroed LDS image
+//         (ds_or_b32 into <= 3 dwords).  An escape (255) emits the next byte; a segment that
+//         starts inside a run of 255s finds its parity by counting back;
 //     (d) aligned 16-byte copy-out of the image, 16-byte views read from the image with
 //         aligned dword reads + v_alignbyte.
 //   A tile whose codes do not decode to exactly the sum of its lengths raises an error (the
@@ -36,26 +37,16 @@ __device__ const uint64_t kNoSymbol[1] = {0};
 
 namespace {
 
-constexpr int kTile = 256;            // threads per workgroup
-#ifndef FSST_SPT
-#define FSST_SPT 1
-#endif
-// Strings per thread: a tile of kTS strings is one workgroup.  The decode of a tile is a chain
-// of dependent phases (prologue loads, length scan, staging, two code passes with a scan between,
-// copy-out); C4's SQ counters park 64 % of wave cycles on waits / barriers.  Two strings per
-// thread (twice the work per chain, 27 KiB of LDS) measured 112 us on C4 against 109 us for one,
-// so one it is (profiles/r03_fsst_spt.md); the generalisation stays for other string shapes.
-constexpr int kSPT = FSST_SPT;
-constexpr int kTS = kTile * kSPT;     // strings per tile
-// LDS images sized for short strings (TPC-H l_comment: 10-43 bytes, a 512-string tile is
-// ~13.6 KB decoded / ~4.5 KB of codes).  Larger tiles take the direct path.
-constexpr int kCodeLds = kSPT == 1 ? 6 * 1024 : 8 * 1024;    // staged code bytes per tile
-constexpr int kHeapLds = kSPT == 1 ? 10 * 1024 : 16 * 1024;  // staged output bytes per tile
-constexpr int kTPB = 1024 / kTS;      // tiles per FastLanes block of lengths (kSPT <= 4)
+constexpr int kTile = 256;            // threads per workgroup = strings per tile
+// (Two strings per thread -- twice the work per tile, 27 KiB of LDS -- measured 112 us on C4
+// against 109 us for one: profiles/r03_fsst_spt.md.)
+constexpr int kTS = kTile;            // strings per tile
+// LDS images sized for short strings (TPC-H l_comment: 10-43 bytes, a 256-string tile is
+// ~6.8 KB decoded / ~2.2 KB of codes).  Larger tiles take the direct path.
+constexpr int kCodeLds = 6 * 1024;    // staged code bytes per tile
+constexpr int kHeapLds = 10 * 1024;   // staged output bytes per tile
+constexpr int kTPB = 1024 / kTS;      // tiles per FastLanes block of lengths
 constexpr int kScanTiles = 32 * kTPB; // tiles per pre-pass workgroup (= 32 FastLanes blocks)
-static_assert(kSPT == 1 || kSPT == 2 || kSPT == 4, "1, 2 or 4 strings per thread");
-constexpr int kMaxDw = (kCodeLds / kTile + 3) / 4;  // code dwords per thread in the decode
-static_assert(kMaxDw * 4 * kTile >= kCodeLds, "segments must cover the staged codes");
 
 __device__ __forceinline__ int64_t wave_sum(int64_t x) {
 #pragma unroll
@@ -327,21 +318,187 @@ __global__ __launch_bounds__(kTile) void fsst_tile_scan_fl32(FsstTable tab, int6
     scan_tile_sums(s_ts, ws, n_tiles, sb, tile_prefix, block_totals, tile_code_all + c.first_tile, code_end);
 }
 
+// Length of string first + k of a tile (k clamped by the caller).  A packed (FastLanes) length
+// column's tile lies in at most two blocks: the block base is uniform and the in-block index
+// 32-bit, so the per-lane work is the unpack_single arithmetic only (intcol.hpp fl_get).
+template <class LenAcc>
+struct TileLen {
+    __device__ static __forceinline__ int64_t get(const LenAcc& a, uint64_t first, uint32_t k) { return a(first + k); }
+};
+template <int T>
+struct TileLen<PackedCol<T>> {
+    __device__ static __forceinline__ int64_t get(const PackedCol<T>& a, uint64_t first, uint32_t k) {
+        using E = std::conditional_t<T == 32, uint32_t, uint64_t>;
+        constexpr uint32_t LANES = 1024 / T;
+        E v = 0;
+        if (a.W != 0) {
+            const uint64_t g0 = first + a.offset;  // uniform
+            const E* __restrict__ base = static_cast<const E*>(a.p) + (g0 >> 10) * (uint64_t(LANES) * a.W);
+            const uint32_t local = uint32_t(g0 & 1023) + k;
+            const uint32_t idx = local & 1023;
+            const uint32_t lane = idx % LANES, s = idx >> 7;
+            const uint32_t fl = ((idx & 127) - lane) >> 4;
+            const uint32_t row = (((fl & 1) << 2) | (fl & 2) | (fl >> 2)) * 8 + s;  // FL_ORDER[fl] * 8 + s
+            const uint32_t start = row * a.W, word = start / T, sh = start % T;
+            const uint32_t word2 = word + 1 < a.W ? word + 1 : word;
+            const uint32_t blk = (local >> 10) * (LANES * a.W);
+            const E lo = base[blk + LANES * word + lane], hi = base[blk + LANES * word2 + lane];
+            v = lo >> sh;
+            if (sh + a.W > uint32_t(T)) v |= hi << (T - sh);
+            if (a.W < uint32_t(T)) v &= (E(1) << a.W) - 1;
+        }
+        const E r = E(E(v << a.shift) + E(a.reference));
+        if constexpr (T == 64) return int64_t(r);
+        else return a.sgn ? int64_t(int32_t(r)) : int64_t(r);
+    }
+};
+
+__device__ __forceinline__ bool has_ff(uint32_t x) { return (((x & 0x7F7F7F7Fu) + 0x01010101u) & x & 0x80808080u) != 0; }
+
+// One staged 16-byte chunk of a tile's code bytes, `nvb` of them the tile's (>= 16: all, <= 0: a
+// padding chunk).  Bytes past the tile become 0xFF -- in the escape-free fast path that code has
+// length 0 and an all-zero symbol, so segments need no tail masks.  Returns whether a tile byte
+// is an escape (255).
+__device__ __forceinline__ bool stage_chunk(uint4& v, int nvb) {
+    if (nvb >= 16) return has_ff(v.x) || has_ff(v.y) || has_ff(v.z) || has_ff(v.w);
+    uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    bool e = false;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int k = nvb - 4 * j;
+        const uint32_t keep = k >= 4 ? 0xFFFFFFFFu : (k <= 0 ? 0u : (1u << (8 * k)) - 1u);
+        e |= has_ff(w[j] & keep);
+        w[j] = (w[j] & keep) | ~keep;
+    }
+    v = make_uint4(w[0], w[1], w[2], w[3]);
+    return e;
+}
+
+// (c) CODE-parallel decode of a staged tile: thread t takes code bytes [4 ND t, 4 ND (t + 1)) of
+// the tile (ND dwords; ND uniform per tile = ceil(span / 1 KiB)).  Pass 1 packs each code's
+// decoded length x 8 into one byte lane per dword (v_sad_u8 sums them), a block scan places every
+// segment, pass 2 ORs each code's zero-padded symbol into <= 3 dwords of the zeroed LDS image.
+// Fast path (no escape byte in the tile): no per-code selects; the 0xFF padding past the tile
+// decodes to nothing.  General path: an escape (255) emits the next byte; a segment that starts
+// inside a run of 255s finds its parity by counting back; bytes past the tile do not count.
+// Threads whose segment starts past the tile do nothing (their ORs would all hit one address).
+template <int ND>
+__device__ __forceinline__ void fsst_segments(const uint8_t* __restrict__ s_codes, int span, bool fast,
+                                              const uint64_t* __restrict__ s_sym, const uint8_t* __restrict__ s_len,
+                                              uint32_t* __restrict__ s_heap32, int hshift, int ttot, int* ws_b,
+                                              uint32_t* __restrict__ err, uint32_t abl) {
+    const int tid = threadIdx.x;
+    const int s0 = tid * 4 * ND;
+    const bool act = s0 < span;
+    const uint32_t* __restrict__ c32 = reinterpret_cast<const uint32_t*>(s_codes);
+    uint32_t pk[ND];  // (the code dwords are re-read in pass 2: fewer registers live across the scan)
+    uint32_t sum8 = 0;
+#pragma unroll
+    for (int d = 0; d < ND; d++) pk[d] = 0;
+    if (act) {
+        uint32_t wd[ND];
+#pragma unroll
+        for (int d = 0; d < ND; d++) wd[d] = c32[(s0 >> 2) + d];
+        if (fast) {
+#pragma unroll
+            for (int d = 0; d < ND; d++) {
+                const uint32_t x = wd[d];
+                uint32_t ls[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) ls[j] = s_len[(x >> (8 * j)) & 0xFFu];
+                uint32_t k = 0;
+#pragma unroll
+                for (int j = 0; j < 4; j++) k |= ls[j] << (8 * j + 3);
+                pk[d] = k;
+                sum8 = __builtin_amdgcn_sad_u8(k, 0u, sum8);
+            }
+        } else {
+            bool skp = false;  // is the current byte the literal of an escape?
+            if (s0 > 0 && s_codes[s0 - 1] == 255) {
+                int r = 0;
+                for (int p = s0 - 1; p >= 0 && s_codes[p] == 255; --p) ++r;
+                skp = r & 1;
+            }
+#pragma unroll
+            for (int d = 0; d < ND; d++) {
+                const uint32_t x = wd[d];
+                uint32_t k = 0;
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const uint32_t c = (x >> (8 * j)) & 0xFFu;
+                    const bool emit = s0 + 4 * d + j < span && !skp;
+                    skp = emit && c == 255;
+                    const uint32_t L = emit ? (c == 255 ? 1u : uint32_t(s_len[c])) : 0u;
+                    k |= L << (8 * j + 3);
+                }
+                pk[d] = k;
+                sum8 = __builtin_amdgcn_sad_u8(k, 0u, sum8);
+            }
+        }
+    }
+    int dec_total;
+    const int seg_rel = block_excl_scan32(int(sum8 >> 3), ws_b, dec_total);
+    if (tid == 0 && dec_total != ttot) __hip_atomic_fetch_or(err, kErrFsst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // a tile whose codes do not decode to its length sum (corrupt input, flagged above) is not written
+    if (!act || dec_total != ttot || (abl & 4)) return;
+    uint32_t o8 = uint32_t(hshift + seg_rel) << 3;  // bit position in the image
+    auto put = [&](uint64_t m, uint32_t L8) {
+        // (w1:w0) = sym << 8(o & 3), w2 = the bytes shifted past them
+        const uint32_t sh = o8 & 24u;
+        const uint32_t w = o8 >> 5;
+        const uint64_t lo64 = m << sh;
+        const uint32_t hi32 = uint32_t((m >> 32) << sh >> 32);
+        __hip_atomic_fetch_or(&s_heap32[w], uint32_t(lo64), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_or(&s_heap32[w + 1], uint32_t(lo64 >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_or(&s_heap32[w + 2], hi32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        o8 += L8;
+    };
+    if (fast) {
+#pragma unroll
+        for (int d = 0; d < ND; d++) {
+            const uint32_t x = c32[(s0 >> 2) + d];
+            uint64_t sy[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) sy[j] = s_sym[(x >> (8 * j)) & 0xFFu];
+#pragma unroll
+            for (int j = 0; j < 4; j++) put(sy[j], (pk[d] >> (8 * j)) & 0xFFu);
+        }
+    } else {
+#pragma unroll
+        for (int d = 0; d < ND; d++) {
+            const uint32_t x = c32[(s0 >> 2) + d];
+            const uint32_t after = s_codes[s0 + 4 * d + 4];  // literal of an escape in byte 3
+            uint64_t sy[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) sy[j] = s_sym[(x >> (8 * j)) & 0xFFu];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t c = (x >> (8 * j)) & 0xFFu;
+                const uint32_t L8 = (pk[d] >> (8 * j)) & 0xFFu;
+                const uint64_t lit = j < 3 ? ((x >> (8 * j + 8)) & 0xFFu) : after;
+                const uint64_t m = c == 255 ? lit : sy[j];
+                put(L8 ? m : 0ull, L8);
+            }
+        }
+    }
+}
+
 template <class OffAcc, class LenAcc, bool EXT>
-__global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t total_tiles,
+__global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) void fsst_decode(FsstTable tab, uint64_t total_tiles,
                                                      const int64_t* __restrict__ tile_prefix_all,
                                                      const int64_t* __restrict__ block_totals_all,
                                                      const int64_t* __restrict__ tile_code_all,
                                                      uint32_t* __restrict__ err,
-                                                     const uint32_t* __restrict__ wg_chunk) {
+                                                     const uint32_t* __restrict__ wg_chunk, uint32_t abl) {
     __shared__ uint64_t s_sym[256];
     __shared__ uint8_t s_len[256];
     __shared__ int ws_a[kTile / 64], ws_b[kTile / 64];
-    __shared__ unsigned ws_bad[kTile / 64];
+    __shared__ unsigned ws_bad[kTile / 64], ws_esc[kTile / 64];
     __shared__ int64_t ws64[kTile / 64];
     __shared__ int64_t s_block_prefix;
+    // + 2 chunks of 0xFF padding past the tile's codes, + slack
     __shared__ __attribute__((aligned(16))) uint8_t s_codes[kCodeLds + 48];
-    // + slack: view reads past a string, and ORs of the (<= 3) code bytes past the tile
+    // + slack: view reads past a string, and ORs of the (<= 3) dwords past the tile
     __shared__ __attribute__((aligned(16))) uint32_t s_heap32[(kHeapLds + 96) / 4];
     uint8_t* const s_heap = reinterpret_cast<uint8_t*>(s_heap32);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -367,27 +524,24 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
     const uint32_t bidx = ch.bidx;
     const uint32_t tile = uint32_t(blockIdx.x - ch.first_tile);
     {
+        // symbols are stored zero-padded past their length, so a code can OR all 8 bytes; a
+        // length > 8 is corrupt input.  Slot 255 (the escape, never a symbol) has length 0 and
+        // no bytes: the fast path's padding code; the general path decodes escapes itself.
         const uint32_t sk = uint32_t(tid) < n_symbols ? uint32_t(tid) : 0;
         const uint64_t sym_v = symbols[sk];
         const uint32_t sl = sym_lens[sk];
-        // slot 255 is the escape (length 1, its byte comes from the code stream).  Symbols are
-        // stored zero-padded past their length, so a code can OR all 8 bytes; a length > 8
-        // is corrupt input.
         const bool has = uint32_t(tid) < n_symbols;
         if (has && sl > 8) __hip_atomic_fetch_or(err, kErrFsst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         s_sym[tid] = has ? (sl >= 8 ? sym_v : sym_v & ((1ull << (8 * sl)) - 1)) : 0;
-        s_len[tid] = has ? uint8_t(min(sl, 8u)) : uint8_t(tid == 255 ? 1 : 0);
+        s_len[tid] = has ? uint8_t(min(sl, 8u)) : uint8_t(0);
     }
     // Prologue: every global load is unconditional (indices clamped, results selected
     // afterwards) so they retire under one wait.
-    // thread tid owns strings i0 .. i0 + kSPT - 1 of the tile
-    const uint64_t first = uint64_t(tile) * kTS;
-    const uint64_t i0 = first + uint64_t(tid) * kSPT;
-    int64_t len_v[kSPT];
-#pragma unroll
-    for (int j = 0; j < kSPT; j++) len_v[j] = lens(i0 + j < n ? i0 + j : n - 1);
-    // kSPT divides 8 and i0 is a multiple of kSPT: the thread's validity bits share one byte
-    const uint8_t vbyte = validity ? validity[(i0 < n ? i0 : n - 1) >> 3] : uint8_t(0xFF);
+    const uint64_t first = uint64_t(tile) * kTile;
+    const bool live = first + uint64_t(tid) < n;
+    const uint32_t kc = live ? uint32_t(tid) : uint32_t(n - 1 - first);  // clamped index in the tile
+    const int64_t len_v = TileLen<LenAcc>::get(lens, first, kc);
+    const uint8_t vbyte = validity ? validity[(first + kc) >> 3] : uint8_t(0xFF);
     const int64_t tp = tile_prefix[tile];
     // the tile's code range [cf, cl) (absolute offsets into `codes`) from the pre-pass records
     // (uniform loads, L2-resident), so the code bytes below are requested in this same round
@@ -401,19 +555,12 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
     const int span = span_ok ? int(span64) : 0;  // tile codes at s_codes[0, span) once staged
     const uint4* const a0 = reinterpret_cast<const uint4*>(ga - uintptr_t(cshift));
     const int nchunk = (span + 15) >> 4;
-    // chunks tid + 256 p (p < kSPT) of the staged image: two aligned 16-byte loads each (an
-    // aligned chunk that holds a tile byte never crosses a page, so it is read whole),
-    // funnel-shifted when written
-    uint4 cx[kSPT], cy[kSPT];
-#pragma unroll
-    for (int p = 0; p < kSPT; p++) {
-        const int q = tid + kTile * p;
-        cx[p] = make_uint4(0, 0, 0, 0);
-        cy[p] = make_uint4(0, 0, 0, 0);
-        if (q < nchunk) {
-            cx[p] = a0[q];
-            if (cshift != 0 && 16 * (q + 1) - cshift < span) cy[p] = a0[q + 1];
-        }
+    // chunk tid of the staged image: two aligned 16-byte loads (an aligned chunk that holds a
+    // tile byte never crosses a page, so it is read whole), funnel-shifted when written
+    uint4 cx = make_uint4(0, 0, 0, 0), cy = make_uint4(0, 0, 0, 0);
+    if (tid < nchunk) {
+        cx = a0[tid];
+        if (cshift != 0 && 16 * (tid + 1) - cshift < span) cy = a0[tid + 1];
     }
     if (wave == 0) {  // prefix of the preceding scan blocks (<= a few hundred totals), one wave
         // four loads per lane in flight per round (clamped index, no per-element branch), so a
@@ -433,183 +580,68 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
         acc = wave_sum(acc);
         if (lane == 0) s_block_prefix = acc;
     }
-    int64_t my_len[kSPT];
-    int64_t my_sum = 0;
-    bool bad = false;
-#pragma unroll
-    for (int j = 0; j < kSPT; j++) {
-        my_len[j] = i0 + j < n ? len_v[j] : 0;
-        bad |= my_len[j] < 0 || my_len[j] > kHeapLds;
-        my_sum += my_len[j];
-    }
+    const int64_t my_len = live ? len_v : 0;
+    const bool bad = my_len < 0 || my_len > kHeapLds;
 
     // (a) length scan: int32 with DPP when every length is in [0, kHeapLds] (then a staged
     // tile is possible), int64 otherwise (direct path).
-    bad |= my_sum > kHeapLds;
     const unsigned long long bm = __ballot(bad);
     if (lane == 0) ws_bad[wave] = bm != 0;
     int t32;
-    const int rel32 = block_excl_scan32(bad ? 0 : int(my_sum), ws_a, t32);
+    const int rel32 = block_excl_scan32(bad ? 0 : int(my_len), ws_a, t32);
     const bool any_bad = (ws_bad[0] | ws_bad[1] | ws_bad[2] | ws_bad[3]) != 0;
     int64_t my_rel = rel32, tile_total = t32;
-    if (any_bad) my_rel = block_exclusive_scan<kTile / 64>(my_sum, ws64, tile_total);  // uniform branch
+    if (any_bad) my_rel = block_exclusive_scan<kTile / 64>(my_len, ws64, tile_total);  // uniform branch
     const int64_t tile_out0 = tp + s_block_prefix;
     const bool stage = !any_bad && span_ok && tile_total <= kHeapLds;
 
+    if (abl & 1) return;
     if (stage) {
         // (b) stage the tile's code bytes into LDS shifted so that the tile's first code is
-        // s_codes[0] (chunk tid was loaded in the prologue; larger tiles load the rest here),
-        // and zero the image
+        // s_codes[0], then two chunks of 0xFF padding; flag escapes; zero the image
         const int hshift = int((reinterpret_cast<uintptr_t>(heap) + tile_out0) & 15);  // image byte hshift = heap[tile_out0]
         const int ttot = int(tile_total);
-        {
-#pragma unroll
-            for (int p = 0; p < kSPT; p++)
-                if (tid + kTile * p < nchunk)
-                    *reinterpret_cast<uint4*>(s_codes + 16 * (tid + kTile * p)) = funnel16(cx[p], cy[p], cshift);
-            for (int q = tid + kTile * kSPT; q < nchunk; q += kTile) {
+        bool esc = false;
+        if (tid < nchunk + 2) {
+            uint4 v = tid < nchunk ? funnel16(cx, cy, cshift) : make_uint4(0, 0, 0, 0);
+            esc |= stage_chunk(v, span - 16 * tid);
+            *reinterpret_cast<uint4*>(s_codes + 16 * tid) = v;
+        }
+        for (int q = tid + kTile; q < nchunk + 2; q += kTile) {  // tiles of > 4 KiB of codes
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (q < nchunk) {
                 const uint4 x = a0[q];
                 uint4 y = make_uint4(0, 0, 0, 0);
                 if (cshift != 0 && 16 * (q + 1) - cshift < span) y = a0[q + 1];
-                *reinterpret_cast<uint4*>(s_codes + 16 * q) = funnel16(x, y, cshift);
+                v = funnel16(x, y, cshift);
             }
-            const int nz = (hshift + ttot + 16 + 15) >> 4;
-            for (int q = tid; q < nz; q += kTile) reinterpret_cast<uint4*>(s_heap32)[q] = make_uint4(0, 0, 0, 0);
+            esc |= stage_chunk(v, span - 16 * q);
+            *reinterpret_cast<uint4*>(s_codes + 16 * q) = v;
         }
+        const int nz = (hshift + ttot + 16 + 15) >> 4;
+        for (int q = tid; q < nz; q += kTile) reinterpret_cast<uint4*>(s_heap32)[q] = make_uint4(0, 0, 0, 0);
+        const unsigned long long eb = __ballot(esc);
+        if (lane == 0) ws_esc[wave] = eb != 0;
         __syncthreads();
-
-        // (c) code-parallel decode over segments of nd dwords (4 code bytes each) per thread,
-        // sized so that ~all 256 threads have work.  A wave whose bytes hold no escape (255)
-        // and does not start right after one takes the fast path (no escape logic, no
-        // predication); otherwise the general path.  Both pack each code's decoded length x 8
-        // into one byte of a per-dword word (sum = v_sad_u8).
-        const int nd = max(1, ((span + kTile - 1) / kTile + 3) >> 2);
-        const int s0 = tid * 4 * nd;
-        bool slow = false;
-        bool skip0 = false;  // is s_codes[s0] the literal byte of an escape?
-        if (s0 > 0 && s0 < span && s_codes[s0 - 1] == 255) {
-            slow = true;
-            int r = 0;
-            for (int p = s0 - 1; p >= 0 && s_codes[p] == 255; --p) ++r;
-            skip0 = r & 1;
+        const bool fast = (ws_esc[0] | ws_esc[1] | ws_esc[2] | ws_esc[3]) == 0;  // tile-uniform
+        if (!(abl & 2)) switch ((span + 4 * kTile - 1) / (4 * kTile)) {  // dwords per thread, tile-uniform
+        case 0:
+        case 1: fsst_segments<1>(s_codes, span, fast, s_sym, s_len, s_heap32, hshift, ttot, ws_b, err, abl); break;
+        case 2: fsst_segments<2>(s_codes, span, fast, s_sym, s_len, s_heap32, hshift, ttot, ws_b, err, abl); break;
+        case 3: fsst_segments<3>(s_codes, span, fast, s_sym, s_len, s_heap32, hshift, ttot, ws_b, err, abl); break;
+        case 4: fsst_segments<4>(s_codes, span, fast, s_sym, s_len, s_heap32, hshift, ttot, ws_b, err, abl); break;
+        case 5: fsst_segments<5>(s_codes, span, fast, s_sym, s_len, s_heap32, hshift, ttot, ws_b, err, abl); break;
+        default: fsst_segments<6>(s_codes, span, fast, s_sym, s_len, s_heap32, hshift, ttot, ws_b, err, abl); break;
         }
-        uint32_t wd[kMaxDw];
-#pragma unroll
-        for (int d = 0; d < kMaxDw; d++) {
-            wd[d] = 0;
-            if (d < nd && s0 + 4 * d < span) {
-                wd[d] = *reinterpret_cast<const uint32_t*>(s_codes + s0 + 4 * d);
-                const uint32_t x = wd[d];
-                slow |= (((x & 0x7F7F7F7Fu) + 0x01010101u) & x & 0x80808080u) != 0;  // a 0xFF byte
-            }
-        }
-        const bool fast = __ballot(slow) == 0;  // wave-uniform
-        // pass 1: pk[d] byte j = decoded length x 8 of code byte 4d + j (0 for literals and
-        // bytes past the tile)
-        uint32_t pk[kMaxDw];
-        uint32_t sum8 = 0;
-        if (fast) {
-#pragma unroll
-            for (int d = 0; d < kMaxDw; d++) {
-                pk[d] = 0;
-                if (d < nd && s0 + 4 * d < span) {
-                    const uint32_t x = wd[d];
-                    uint32_t ls[4];
-#pragma unroll
-                    for (int j = 0; j < 4; j++) ls[j] = s_len[(x >> (8 * j)) & 0xFFu];
-                    uint32_t k = 0;
-#pragma unroll
-                    for (int j = 0; j < 4; j++) k |= ls[j] << (8 * j + 3);
-                    const int vb = span - (s0 + 4 * d);  // valid bytes of this dword
-                    if (vb < 4) k &= (1u << (8 * vb)) - 1u;
-                    pk[d] = k;
-                    sum8 = __builtin_amdgcn_sad_u8(k, 0u, sum8);
-                }
-            }
-        } else {
-            bool skp = skip0;
-#pragma unroll
-            for (int d = 0; d < kMaxDw; d++) {
-                pk[d] = 0;
-                if (d < nd && s0 + 4 * d < span) {
-                    const uint32_t x = wd[d];
-                    uint32_t k = 0;
-#pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        const uint32_t c = (x >> (8 * j)) & 0xFFu;
-                        const bool emit = s0 + 4 * d + j < span && !skp;
-                        skp = emit && c == 255;
-                        const uint32_t L = emit ? uint32_t(s_len[c]) : 0u;
-                        k |= L << (8 * j + 3);
-                    }
-                    pk[d] = k;
-                    sum8 = __builtin_amdgcn_sad_u8(k, 0u, sum8);
-                }
-            }
-        }
-        int dec_total;
-        const int seg_rel = block_excl_scan32(int(sum8 >> 3), ws_b, dec_total);
-        if (tid == 0 && dec_total != ttot)
-            __hip_atomic_fetch_or(err, kErrFsst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // pass 2: every code ORs its (zero-padded) bytes into <= 3 dwords of the zeroed image:
-        // (w1:w0) = sym << 8(o & 3) and w2 = the bytes shifted past them.  Fast path: all 4
-        // symbol reads of a dword issued first, no selects.  Codes past the tile (fast path,
-        // last segment) OR into the image slack after the tile.  A tile whose codes do not
-        // decode to its length sum (corrupt input, flagged above) is not written.
-        if (dec_total == ttot) {
-            uint32_t o8 = uint32_t(hshift + seg_rel) << 3;  // bit position in the image
-            auto put = [&](uint64_t m, uint32_t L8) {
-                const uint32_t sh = o8 & 24u;
-                const uint32_t w = o8 >> 5;
-                const uint64_t lo64 = m << sh;
-                const uint32_t hi32 = uint32_t((m >> 32) << sh >> 32);
-                __hip_atomic_fetch_or(&s_heap32[w], uint32_t(lo64), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                __hip_atomic_fetch_or(&s_heap32[w + 1], uint32_t(lo64 >> 32), __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_WORKGROUP);
-                __hip_atomic_fetch_or(&s_heap32[w + 2], hi32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                o8 += L8;
-            };
-            if (fast) {
-#pragma unroll
-                for (int d = 0; d < kMaxDw; d++) {
-                    if (d < nd && s0 + 4 * d < span) {
-                        const uint32_t x = wd[d];
-                        uint64_t sy[4];
-#pragma unroll
-                        for (int j = 0; j < 4; j++) sy[j] = s_sym[(x >> (8 * j)) & 0xFFu];
-#pragma unroll
-                        for (int j = 0; j < 4; j++) put(sy[j], (pk[d] >> (8 * j)) & 0xFFu);
-                    }
-                }
-            } else {
-#pragma unroll
-                for (int d = 0; d < kMaxDw; d++) {
-                    if (d < nd && s0 + 4 * d < span) {
-                        const uint32_t x = wd[d];
-                        const uint32_t after = s_codes[s0 + 4 * d + 4];  // literal of an escape in byte 3
-                        uint64_t sy[4];
-#pragma unroll
-                        for (int j = 0; j < 4; j++) sy[j] = s_sym[(x >> (8 * j)) & 0xFFu];
-#pragma unroll
-                        for (int j = 0; j < 4; j++) {
-                            const uint32_t c = (x >> (8 * j)) & 0xFFu;
-                            const uint32_t L8 = (pk[d] >> (8 * j)) & 0xFFu;
-                            const uint64_t lit = j < 3 ? ((x >> (8 * j + 8)) & 0xFFu) : after;
-                            uint64_t m = c == 255 ? lit : sy[j];
-                            put(L8 ? m : 0ull, L8);
-                        }
-                    }
-                }
-            }
-        }
+        static_assert(kCodeLds <= 6 * 4 * kTile, "six dwords per thread cover the staged codes");
         __syncthreads();
         // (d) copy-out of [tile_out0, tile_out0 + ttot): the image sits at the same offset mod 16
         // as its destination, so whole aligned chunks move as ds_read_b128 + 16-byte stores;
         // the ragged first/last chunk byte by byte (shared with the neighbouring tiles)
-        {
+        if (!(abl & 8)) {
             uint8_t* const gbase = heap + (tile_out0 - hshift);
-            const int nchunk = (hshift + ttot + 15) >> 4;
-            for (int q = tid; q < nchunk; q += kTile) {
+            const int nchunk_out = (hshift + ttot + 15) >> 4;
+            for (int q = tid; q < nchunk_out; q += kTile) {
                 const int lb = 16 * q;
                 if (lb >= hshift && lb + 16 <= hshift + ttot) {
                     nt_store(reinterpret_cast<uint4*>(gbase + lb), *reinterpret_cast<const uint4*>(s_heap + lb));
@@ -634,52 +666,42 @@ __global__ __launch_bounds__(kTile) void fsst_decode(FsstTable tab, uint64_t tot
                 }
             }
         }
-        int64_t rel = my_rel;
-#pragma unroll
-        for (int j = 0; j < kSPT; j++) {
-            const uint64_t i = i0 + j;
-            if (i < n) {
-                const bool valid = (vbyte >> (i & 7)) & 1;
-                views[i] = valid ? lds_view(s_heap32, hshift + int(rel), uint32_t(my_len[j]), uint32_t(tile_out0 + rel), bidx)
-                                 : make_uint4(0, 0, 0, 0);
-            }
-            rel += my_len[j];
+        if (live && !(abl & 16)) {
+            const bool valid = (vbyte >> (tid & 7)) & 1;
+            views[first + tid] = valid ? lds_view(s_heap32, hshift + int(my_rel), uint32_t(my_len),
+                                                  uint32_t(tile_out0 + my_rel), bidx)
+                                       : make_uint4(0, 0, 0, 0);
         }
     } else {
         // direct path: per-string decode straight into HBM (codes of string i are
         // [offs[i], offs[i+1]); each must decode to exactly lengths[i] bytes)
+        const uint64_t i = first + tid;
+        const int64_t my_c0 = live ? code_offs(i) : 0;
+        const int64_t my_c1 = live ? code_offs(i + 1) : 0;
         int64_t o = tile_out0 + my_rel;
-        for (int j = 0; j < kSPT; j++) {
-            const uint64_t i = i0 + j;
-            const bool live = i < n;
-            const int64_t my_c0 = live ? code_offs(i) : 0;
-            const int64_t my_c1 = live ? code_offs(i + 1) : 0;
-            const uint8_t* gcodes = codes;
-            const int64_t o_start = o, o_end = o + my_len[j];
-            for (int64_t k = my_c0; k < my_c1; k++) {
-                const uint8_t c = gcodes[k];
-                if (c == 255) {
-                    ++k;
-                    if (o < o_end) heap[o] = gcodes[k];
-                    o++;
-                } else {
-                    const uint64_t sym = s_sym[c];
-                    const int L = s_len[c];
-                    for (int b = 0; b < L; b++)
-                        if (o + b < o_end) heap[o + b] = uint8_t(sym >> (8 * b));
-                    o += L;
-                }
+        const int64_t o_start = o, o_end = o + my_len;
+        for (int64_t k = my_c0; k < my_c1; k++) {
+            const uint8_t c = codes[k];
+            if (c == 255) {
+                ++k;
+                if (o < o_end) heap[o] = codes[k];
+                o++;
+            } else {
+                const uint64_t sym = s_sym[c];
+                const int L = s_len[c];
+                for (int b = 0; b < L; b++)
+                    if (o + b < o_end) heap[o + b] = uint8_t(sym >> (8 * b));
+                o += L;
             }
-            if (o != o_end) __hip_atomic_fetch_or(err, kErrFsst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            o = o_end;
-            if (live) {
-                const bool valid = (vbyte >> (i & 7)) & 1;
-                const uint32_t vlen = valid ? uint32_t(my_len[j]) : 0u;
-                const uint8_t* hp = heap + o_start;
-                views[i] = valid ? build_view(vlen, uint32_t(o_start), bidx,
-                                              [&](int b) { return uint32_t(b) < vlen ? hp[b] : uint8_t(0); })
-                                 : make_uint4(0, 0, 0, 0);
-            }
+        }
+        if (o != o_end) __hip_atomic_fetch_or(err, kErrFsst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (live) {
+            const bool valid = (vbyte >> (i & 7)) & 1;
+            const uint32_t vlen = valid ? uint32_t(my_len) : 0u;
+            const uint8_t* hp = heap + o_start;
+            views[i] = valid ? build_view(vlen, uint32_t(o_start), bidx,
+                                          [&](int b) { return uint32_t(b) < vlen ? hp[b] : uint8_t(0); })
+                             : make_uint4(0, 0, 0, 0);
         }
     }
 }
@@ -733,6 +755,8 @@ bool with_acc(int kind, F&& f) {
 
 vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint32_t* err, hipStream_t s,
                              DevTables* dt) {
+    const char* abl_env = std::getenv("VXG_FSST_ABL");  // TEMP ablation
+    const uint32_t abl = abl_env ? uint32_t(std::strtoul(abl_env, nullptr, 10)) : 0u;
     for (const FsstChunk& c : chunks) {
         if (c.n_symbols > 255) return set_error(VXG_ERR_INVALID_ARGUMENT, "FSST symbol table > 255 entries");
         if ((c.n + kTS - 1) / kTS > 0xFFFFFFFFull) return set_error(VXG_ERR_INVALID_ARGUMENT, "FSST array too long");
@@ -801,7 +825,7 @@ vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint
                             hipLaunchKernelGGL((fsst_tile_scan<LA, X>), dim3(unsigned(scans)), dim3(kTile), 0, s, tab,
                                                tp, bt, tc);
                         hipLaunchKernelGGL((fsst_decode<OA, LA, X>), dim3(unsigned(tiles)), dim3(kTile), 0, s, tab,
-                                           tiles, tp, bt, tc, err, wg_chunk);
+                                           tiles, tp, bt, tc, err, wg_chunk, abl);
                     };
                     if (tab.ext) go(std::true_type{});
                     else go(std::false_type{});
