@@ -12,7 +12,7 @@
 //   kernel 2 (scan_blocks): exclusive tile prefix inside 1024-tile blocks + one total per block
 //   kernel 3 (decode):      per tile, in LDS:
 //     (a) block prefix (one wave) + block scan of the lengths -> each string's offset;
-//     (b) the tile's code bytes staged with aligned 16-byte loads, 0xFF-padded, escapes flagged;
+//     (b) the tile's code bytes staged with aligned 16-byte loads;
 //     (c) CODE-parallel decode: thread t takes a segment of ND dwords of the code bytes (not
 //         one string: per-string loops ran as long as the longest of 64 strings and were
 //         VALU-issue bound; ND per tile, the segment code templated on it, branch-free).
@@ -33,7 +33,6 @@
 
 namespace vxg {
 
-__device__ const uint64_t kNoSymbol[1] = {0};
 
 namespace {
 
@@ -101,7 +100,8 @@ __device__ __forceinline__ uint4 build_view(uint32_t len, uint32_t offset, uint3
     return make_uint4(len, w1, w2, w3);
 }
 
-// The same view from an LDS byte image: four aligned dword reads and byte funnel shifts.
+// The same view from an LDS byte image: four aligned dword reads and byte funnel shifts; the
+// inline bytes past the string are masked with hi32(0xFFFFFFFF << 8 k), k = clamp(len - base, 0, 4).
 __device__ __forceinline__ uint4 lds_view(const uint32_t* h32, int a, uint32_t len, uint32_t offset, uint32_t bidx) {
     const int w = a >> 2;
     const uint32_t sh = uint32_t(a & 3);
@@ -111,8 +111,8 @@ __device__ __forceinline__ uint4 lds_view(const uint32_t* h32, int a, uint32_t l
     uint32_t w2 = __builtin_amdgcn_alignbyte(d2, d1, sh);
     uint32_t w3 = __builtin_amdgcn_alignbyte(d3, d2, sh);
     auto keep = [&](int base) -> uint32_t {
-        const int k = int(len) - base;
-        return k >= 4 ? 0xFFFFFFFFu : (k <= 0 ? 0u : (1u << (8 * k)) - 1u);
+        const int k = min(max(int(len) - base, 0), 4);
+        return uint32_t((0xFFFFFFFFull << (8 * k)) >> 32);
     };
     return make_uint4(len, w1 & keep(0), w2 & keep(4), w3 & keep(8));
 }
@@ -318,101 +318,126 @@ __global__ __launch_bounds__(kTile) void fsst_tile_scan_fl32(FsstTable tab, int6
     scan_tile_sums(s_ts, ws, n_tiles, sb, tile_prefix, block_totals, tile_code_all + c.first_tile, code_end);
 }
 
-// Length of string first + k of a tile (k clamped by the caller).  A packed (FastLanes) length
-// column's tile lies in at most two blocks: the block base is uniform and the in-block index
-// 32-bit, so the per-lane work is the unpack_single arithmetic only (intcol.hpp fl_get).
+// Length of string first + k of a tile (k clamped by the caller), in two steps so the load can
+// be issued together with the prologue's other loads and used after all of them: issue() starts
+// the load(s), value() finishes.  A packed (FastLanes) length column's tile lies in at most two
+// blocks: the block base is uniform and the in-block index 32-bit (unpack_single arithmetic of
+// intcol.hpp fl_word_pair, whose two words are combined only in value()).
 template <class LenAcc>
 struct TileLen {
-    __device__ static __forceinline__ int64_t get(const LenAcc& a, uint64_t first, uint32_t k) { return a(first + k); }
+    int64_t x;
+    __device__ __forceinline__ void issue(const LenAcc& a, uint64_t first, uint32_t k) { x = a(first + k); }
+    __device__ __forceinline__ int64_t value(const LenAcc&) const { return x; }
 };
 template <int T>
 struct TileLen<PackedCol<T>> {
-    __device__ static __forceinline__ int64_t get(const PackedCol<T>& a, uint64_t first, uint32_t k) {
-        using E = std::conditional_t<T == 32, uint32_t, uint64_t>;
+    using E = std::conditional_t<T == 32, uint32_t, uint64_t>;
+    E lo, hi;
+    uint32_t sh;
+    __device__ __forceinline__ void issue(const PackedCol<T>& a, uint64_t first, uint32_t k) {
+        // raw buffer loads over the tile's (at most) two blocks: no branch for W = 0 (the
+        // resource then has no records and the loads return 0 without touching memory)
         constexpr uint32_t LANES = 1024 / T;
-        E v = 0;
-        if (a.W != 0) {
-            const uint64_t g0 = first + a.offset;  // uniform
-            const E* __restrict__ base = static_cast<const E*>(a.p) + (g0 >> 10) * (uint64_t(LANES) * a.W);
-            const uint32_t local = uint32_t(g0 & 1023) + k;
-            const uint32_t idx = local & 1023;
-            const uint32_t lane = idx % LANES, s = idx >> 7;
-            const uint32_t fl = ((idx & 127) - lane) >> 4;
-            const uint32_t row = (((fl & 1) << 2) | (fl & 2) | (fl >> 2)) * 8 + s;  // FL_ORDER[fl] * 8 + s
-            const uint32_t start = row * a.W, word = start / T, sh = start % T;
-            const uint32_t word2 = word + 1 < a.W ? word + 1 : word;
-            const uint32_t blk = (local >> 10) * (LANES * a.W);
-            const E lo = base[blk + LANES * word + lane], hi = base[blk + LANES * word2 + lane];
-            v = lo >> sh;
-            if (sh + a.W > uint32_t(T)) v |= hi << (T - sh);
-            if (a.W < uint32_t(T)) v &= (E(1) << a.W) - 1;
+        const uint64_t g0 = first + a.offset;  // uniform
+        const uint8_t* base = static_cast<const uint8_t*>(a.p) + (g0 >> 10) * (128ull * a.W);
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base), short(0), int(256 * a.W), 0x00020000);
+        const uint32_t local = uint32_t(g0 & 1023) + k;
+        const uint32_t idx = local & 1023, lane = idx % LANES, s = idx >> 7;
+        const uint32_t fl = ((idx & 127) - lane) >> 4;
+        const uint32_t row = (((fl & 1) << 2) | (fl & 2) | (fl >> 2)) * 8 + s;  // FL_ORDER[fl]*8 + s
+        const uint32_t start = __umul24(row, a.W), word = start / T;
+        const uint32_t word2 = word + 1 < a.W ? word + 1 : word;
+        const uint32_t bo = (local >> 10) ? 128 * a.W : 0u;
+        sh = start % T;
+        if constexpr (T == 32) {
+            lo = __builtin_amdgcn_raw_buffer_load_b32(rs, bo + 4 * (LANES * word + lane), 0, 0);
+            hi = __builtin_amdgcn_raw_buffer_load_b32(rs, bo + 4 * (LANES * word2 + lane), 0, 0);
+        } else {
+            const auto l2 = __builtin_amdgcn_raw_buffer_load_b64(rs, bo + 8 * (LANES * word + lane), 0, 0);
+            const auto h2 = __builtin_amdgcn_raw_buffer_load_b64(rs, bo + 8 * (LANES * word2 + lane), 0, 0);
+            lo = uint64_t(uint32_t(l2[0])) | (uint64_t(uint32_t(l2[1])) << 32);
+            hi = uint64_t(uint32_t(h2[0])) | (uint64_t(uint32_t(h2[1])) << 32);
         }
+    }
+    __device__ __forceinline__ int64_t value(const PackedCol<T>& a) const {
+        const E mask = a.W >= uint32_t(T) ? E(~E(0)) : E((E(1) << a.W) - 1);
+        E v;
+        if constexpr (T == 32) v = __builtin_amdgcn_alignbit(hi, lo, sh) & mask;
+        else v = (sh ? (lo >> sh) | (hi << (64 - sh)) : lo) & mask;
         const E r = E(E(v << a.shift) + E(a.reference));
         if constexpr (T == 64) return int64_t(r);
         else return a.sgn ? int64_t(int32_t(r)) : int64_t(r);
     }
 };
 
-__device__ __forceinline__ bool has_ff(uint32_t x) { return (((x & 0x7F7F7F7Fu) + 0x01010101u) & x & 0x80808080u) != 0; }
-
-// One staged 16-byte chunk of a tile's code bytes, `nvb` of them the tile's (>= 16: all, <= 0: a
-// padding chunk).  Bytes past the tile become 0xFF -- in the escape-free fast path that code has
-// length 0 and an all-zero symbol, so segments need no tail masks.  Returns whether a tile byte
-// is an escape (255).
-__device__ __forceinline__ bool stage_chunk(uint4& v, int nvb) {
-    if (nvb >= 16) return has_ff(v.x) || has_ff(v.y) || has_ff(v.z) || has_ff(v.w);
-    uint32_t w[4] = {v.x, v.y, v.z, v.w};
-    bool e = false;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const int k = nvb - 4 * j;
-        const uint32_t keep = k >= 4 ? 0xFFFFFFFFu : (k <= 0 ? 0u : (1u << (8 * k)) - 1u);
-        e |= has_ff(w[j] & keep);
-        w[j] = (w[j] & keep) | ~keep;
-    }
-    v = make_uint4(w[0], w[1], w[2], w[3]);
-    return e;
+template <class V4>
+__device__ __forceinline__ uint4 as_uint4(const V4& v) {
+    return make_uint4(uint32_t(v[0]), uint32_t(v[1]), uint32_t(v[2]), uint32_t(v[3]));
 }
 
 // (c) CODE-parallel decode of a staged tile: thread t takes code bytes [4 ND t, 4 ND (t + 1)) of
 // the tile (ND dwords; ND uniform per tile = ceil(span / 1 KiB)).  Pass 1 packs each code's
 // decoded length x 8 into one byte lane per dword (v_sad_u8 sums them), a block scan places every
 // segment, pass 2 ORs each code's zero-padded symbol into <= 3 dwords of the zeroed LDS image.
-// Fast path (no escape byte in the tile): no per-code selects; the 0xFF padding past the tile
-// decodes to nothing.  General path: an escape (255) emits the next byte; a segment that starts
-// inside a run of 255s finds its parity by counting back; bytes past the tile do not count.
-// Threads whose segment starts past the tile do nothing (their ORs would all hit one address).
+// Pass 1 first assumes no escape: code 255 reads the sentinel length 16 (x 8 = bit 7 of its byte
+// lane, real lengths are <= 8), and a tile in which any thread saw it (flag through the scan's
+// barrier) redoes pass 1 in the general form and scans again -- an escape (255) emits the next
+// byte; a segment that starts inside a run of 255s finds its parity by counting back; bytes past
+// the tile do not count.  Threads whose segment starts past the tile do nothing (their ORs
+// would all hit one address); the one thread whose segment straddles the tile end masks it.
 template <int ND>
-__device__ __forceinline__ void fsst_segments(const uint8_t* __restrict__ s_codes, int span, bool fast,
+__device__ __forceinline__ void fsst_segments(const uint8_t* __restrict__ s_codes, int span,
                                               const uint64_t* __restrict__ s_sym, const uint8_t* __restrict__ s_len,
                                               uint32_t* __restrict__ s_heap32, int hshift, int ttot, int* ws_b,
-                                              uint32_t* __restrict__ err, uint32_t abl) {
-    const int tid = threadIdx.x;
+                                              unsigned* ws_esc, uint32_t* __restrict__ err, uint32_t abl) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int s0 = tid * 4 * ND;
     const bool act = s0 < span;
     const uint32_t* __restrict__ c32 = reinterpret_cast<const uint32_t*>(s_codes);
     uint32_t pk[ND];  // (the code dwords are re-read in pass 2: fewer registers live across the scan)
     uint32_t sum8 = 0;
+    bool esc = false;
 #pragma unroll
     for (int d = 0; d < ND; d++) pk[d] = 0;
     if (act) {
         uint32_t wd[ND];
 #pragma unroll
         for (int d = 0; d < ND; d++) wd[d] = c32[(s0 >> 2) + d];
-        if (fast) {
+#pragma unroll
+        for (int d = 0; d < ND; d++) {
+            const uint32_t x = wd[d];
+            uint32_t ls[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) ls[j] = s_len[(x >> (8 * j)) & 0xFFu];
+            uint32_t k = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) k |= ls[j] << (8 * j + 3);
+            pk[d] = k;
+        }
+        if (s0 + 4 * ND > span) {  // bytes past the tile have no length
 #pragma unroll
             for (int d = 0; d < ND; d++) {
-                const uint32_t x = wd[d];
-                uint32_t ls[4];
-#pragma unroll
-                for (int j = 0; j < 4; j++) ls[j] = s_len[(x >> (8 * j)) & 0xFFu];
-                uint32_t k = 0;
-#pragma unroll
-                for (int j = 0; j < 4; j++) k |= ls[j] << (8 * j + 3);
-                pk[d] = k;
-                sum8 = __builtin_amdgcn_sad_u8(k, 0u, sum8);
+                const int vb = span - (s0 + 4 * d);
+                pk[d] &= vb >= 4 ? 0xFFFFFFFFu : (vb <= 0 ? 0u : (1u << (8 * vb)) - 1u);
             }
-        } else {
+        }
+        uint32_t any = 0;
+#pragma unroll
+        for (int d = 0; d < ND; d++) {
+            any |= pk[d];
+            sum8 = __builtin_amdgcn_sad_u8(pk[d], 0u, sum8);
+        }
+        esc = (any & 0x80808080u) != 0;
+    }
+    const unsigned long long eb = __ballot(esc);
+    if (lane == 0) ws_esc[wave] = eb != 0;
+    int dec_total;
+    int seg_rel = block_excl_scan32(int(sum8 >> 3), ws_b, dec_total);
+    const bool fast = (ws_esc[0] | ws_esc[1] | ws_esc[2] | ws_esc[3]) == 0;  // tile-uniform
+    if (!fast) {
+        sum8 = 0;
+        if (act) {
             bool skp = false;  // is the current byte the literal of an escape?
             if (s0 > 0 && s_codes[s0 - 1] == 255) {
                 int r = 0;
@@ -421,7 +446,7 @@ __device__ __forceinline__ void fsst_segments(const uint8_t* __restrict__ s_code
             }
 #pragma unroll
             for (int d = 0; d < ND; d++) {
-                const uint32_t x = wd[d];
+                const uint32_t x = c32[(s0 >> 2) + d];
                 uint32_t k = 0;
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
@@ -435,9 +460,9 @@ __device__ __forceinline__ void fsst_segments(const uint8_t* __restrict__ s_code
                 sum8 = __builtin_amdgcn_sad_u8(k, 0u, sum8);
             }
         }
+        __syncthreads();  // every thread has read the first scan's wave totals
+        seg_rel = block_excl_scan32(int(sum8 >> 3), ws_b, dec_total);
     }
-    int dec_total;
-    const int seg_rel = block_excl_scan32(int(sum8 >> 3), ws_b, dec_total);
     if (tid == 0 && dec_total != ttot) __hip_atomic_fetch_or(err, kErrFsst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // a tile whose codes do not decode to its length sum (corrupt input, flagged above) is not written
     if (!act || dec_total != ttot || (abl & 4)) return;
@@ -496,7 +521,7 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     __shared__ unsigned ws_bad[kTile / 64], ws_esc[kTile / 64];
     __shared__ int64_t ws64[kTile / 64];
     __shared__ int64_t s_block_prefix;
-    // + 2 chunks of 0xFF padding past the tile's codes, + slack
+    // + slack: the straddling segment's dwords past the tile (masked in pass 1)
     __shared__ __attribute__((aligned(16))) uint8_t s_codes[kCodeLds + 48];
     // + slack: view reads past a string, and ORs of the (<= 3) dwords past the tile
     __shared__ __attribute__((aligned(16))) uint32_t s_heap32[(kHeapLds + 96) / 4];
@@ -507,10 +532,6 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     // (one scalar load) instead of the wave-wide count over the table
     const FsstChunk& ch = EXT ? tab.ext[wg_chunk[blockIdx.x]] : fsst_chunk_of<false, EXT>(tab, blockIdx.x);
     const unsigned n_symbols = ch.n_symbols;
-    // an empty table (no symbols: e.g. trained on null strings only) may have null buffers; the
-    // clamped load below then reads a zero entry here instead
-    const uint64_t* __restrict__ symbols = n_symbols ? ch.symbols : kNoSymbol;
-    const uint8_t* __restrict__ sym_lens = n_symbols ? ch.sym_lens : reinterpret_cast<const uint8_t*>(kNoSymbol);
     const uint8_t* __restrict__ codes = ch.codes;
     const OffAcc code_offs(ch.offs);
     const LenAcc lens(ch.lens);
@@ -523,45 +544,41 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     uint4* __restrict__ views = reinterpret_cast<uint4*>(ch.views);
     const uint32_t bidx = ch.bidx;
     const uint32_t tile = uint32_t(blockIdx.x - ch.first_tile);
-    {
-        // symbols are stored zero-padded past their length, so a code can OR all 8 bytes; a
-        // length > 8 is corrupt input.  Slot 255 (the escape, never a symbol) has length 0 and
-        // no bytes: the fast path's padding code; the general path decodes escapes itself.
-        const uint32_t sk = uint32_t(tid) < n_symbols ? uint32_t(tid) : 0;
-        const uint64_t sym_v = symbols[sk];
-        const uint32_t sl = sym_lens[sk];
-        const bool has = uint32_t(tid) < n_symbols;
-        if (has && sl > 8) __hip_atomic_fetch_or(err, kErrFsst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_sym[tid] = has ? (sl >= 8 ? sym_v : sym_v & ((1ull << (8 * sl)) - 1)) : 0;
-        s_len[tid] = has ? uint8_t(min(sl, 8u)) : uint8_t(0);
-    }
-    // Prologue: every global load is unconditional (indices clamped, results selected
-    // afterwards) so they retire under one wait.
+    // Prologue: the scalar records first (their latency overlaps the vector loads below), then
+    // every vector load issued before any result is used -- indices clamped, results selected
+    // afterwards, no atomic or branch between a load and its use -- so they retire under one
+    // wait.  The tile's code range [cf, cl) (absolute offsets into `codes`) comes from the
+    // pre-pass records, so the code bytes are requested in this same round trip.
+    const int64_t tp = tile_prefix[tile];
+    const int64_t cl = tile_code[tile];
+    const int64_t cf = tile > 0 ? tile_code[tile - 1] : code_offs(0);
     const uint64_t first = uint64_t(tile) * kTile;
     const bool live = first + uint64_t(tid) < n;
     const uint32_t kc = live ? uint32_t(tid) : uint32_t(n - 1 - first);  // clamped index in the tile
-    const int64_t len_v = TileLen<LenAcc>::get(lens, first, kc);
+    const bool has = uint32_t(tid) < n_symbols;
+    uint64_t sym_v = 0;
+    uint32_t sl = 0;
+    if (n_symbols) {  // (an empty table -- e.g. trained on null strings only -- may have null buffers)
+        const uint32_t sk = has ? uint32_t(tid) : 0u;
+        sym_v = ch.symbols[sk];
+        sl = ch.sym_lens[sk];
+    }
+    TileLen<LenAcc> tl;
+    tl.issue(lens, first, kc);
     const uint8_t vbyte = validity ? validity[(first + kc) >> 3] : uint8_t(0xFF);
-    const int64_t tp = tile_prefix[tile];
-    // the tile's code range [cf, cl) (absolute offsets into `codes`) from the pre-pass records
-    // (uniform loads, L2-resident), so the code bytes below are requested in this same round
-    // trip instead of after the length scan
-    const int64_t cl = tile_code[tile];
-    const int64_t cf = tile > 0 ? tile_code[tile - 1] : code_offs(0);
-    const uintptr_t ga = reinterpret_cast<uintptr_t>(codes) + uintptr_t(cf);
-    const int cshift = int(ga & 15);
+    const int cshift = int((reinterpret_cast<uintptr_t>(codes) + uintptr_t(cf)) & 15);
     const int64_t span64 = cl - cf;
     const bool span_ok = span64 >= 0 && span64 <= kCodeLds;
     const int span = span_ok ? int(span64) : 0;  // tile codes at s_codes[0, span) once staged
-    const uint4* const a0 = reinterpret_cast<const uint4*>(ga - uintptr_t(cshift));
+    const uint4* const a0 = reinterpret_cast<const uint4*>(codes + (cf - cshift));  // (pointer arithmetic: global loads)
     const int nchunk = (span + 15) >> 4;
-    // chunk tid of the staged image: two aligned 16-byte loads (an aligned chunk that holds a
-    // tile byte never crosses a page, so it is read whole), funnel-shifted when written
-    uint4 cx = make_uint4(0, 0, 0, 0), cy = make_uint4(0, 0, 0, 0);
-    if (tid < nchunk) {
-        cx = a0[tid];
-        if (cshift != 0 && 16 * (tid + 1) - cshift < span) cy = a0[tid + 1];
-    }
+    // chunks tid and tid + 1 of the tile's aligned code range (funnel-shifted when staged), as
+    // bounds-checked buffer loads: no branch (a chunk past the range reads as zeros without a
+    // memory access), so they retire under the prologue's one wait
+    const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint4*>(a0), short(0), span ? int((cshift + span + 15) & ~15) : 0, 0x00020000);
+    const uint4 cx = as_uint4(__builtin_amdgcn_raw_buffer_load_b128(crs, 16 * tid, 0, 0));
+    const uint4 cy = as_uint4(__builtin_amdgcn_raw_buffer_load_b128(crs, 16 * tid + 16, 0, 0));
     if (wave == 0) {  // prefix of the preceding scan blocks (<= a few hundred totals), one wave
         // four loads per lane in flight per round (clamped index, no per-element branch), so a
         // tile deep in a large chunk pays one memory round trip here, not one per 64 blocks
@@ -580,7 +597,12 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         acc = wave_sum(acc);
         if (lane == 0) s_block_prefix = acc;
     }
-    const int64_t my_len = live ? len_v : 0;
+    // symbols are stored zero-padded past their length, so a code can OR all 8 bytes; a length
+    // > 8 is corrupt input (reported after the scan).  Slot 255 (the escape, never a symbol) has no
+    // bytes and the sentinel length 16 (pass 1's escape detector); escapes are decoded explicitly.
+    s_sym[tid] = has ? (sl >= 8 ? sym_v : sym_v & ((1ull << (8 * sl)) - 1)) : 0;
+    s_len[tid] = has ? uint8_t(min(sl, 8u)) : uint8_t(tid == 255 ? 16 : 0);
+    const int64_t my_len = live ? tl.value(lens) : 0;
     const bool bad = my_len < 0 || my_len > kHeapLds;
 
     // (a) length scan: int32 with DPP when every length is in [0, kHeapLds] (then a staged
@@ -592,78 +614,53 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     const bool any_bad = (ws_bad[0] | ws_bad[1] | ws_bad[2] | ws_bad[3]) != 0;
     int64_t my_rel = rel32, tile_total = t32;
     if (any_bad) my_rel = block_exclusive_scan<kTile / 64>(my_len, ws64, tile_total);  // uniform branch
+    if (has && sl > 8) __hip_atomic_fetch_or(err, kErrFsst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int64_t tile_out0 = tp + s_block_prefix;
     const bool stage = !any_bad && span_ok && tile_total <= kHeapLds;
 
     if (abl & 1) return;
     if (stage) {
         // (b) stage the tile's code bytes into LDS shifted so that the tile's first code is
-        // s_codes[0], then two chunks of 0xFF padding; flag escapes; zero the image
+        // s_codes[0] (chunk tid was loaded in the prologue; larger tiles load the rest here),
+        // and zero the image
         const int hshift = int((reinterpret_cast<uintptr_t>(heap) + tile_out0) & 15);  // image byte hshift = heap[tile_out0]
         const int ttot = int(tile_total);
-        bool esc = false;
-        if (tid < nchunk + 2) {
-            uint4 v = tid < nchunk ? funnel16(cx, cy, cshift) : make_uint4(0, 0, 0, 0);
-            esc |= stage_chunk(v, span - 16 * tid);
-            *reinterpret_cast<uint4*>(s_codes + 16 * tid) = v;
-        }
-        for (int q = tid + kTile; q < nchunk + 2; q += kTile) {  // tiles of > 4 KiB of codes
-            uint4 v = make_uint4(0, 0, 0, 0);
-            if (q < nchunk) {
-                const uint4 x = a0[q];
-                uint4 y = make_uint4(0, 0, 0, 0);
-                if (cshift != 0 && 16 * (q + 1) - cshift < span) y = a0[q + 1];
-                v = funnel16(x, y, cshift);
-            }
-            esc |= stage_chunk(v, span - 16 * q);
-            *reinterpret_cast<uint4*>(s_codes + 16 * q) = v;
+        if (tid < nchunk) *reinterpret_cast<uint4*>(s_codes + 16 * tid) = funnel16(cx, cy, cshift);
+        for (int q = tid + kTile; q < nchunk; q += kTile) {  // tiles of > 4 KiB of codes
+            const uint4 x = a0[q];
+            uint4 y = make_uint4(0, 0, 0, 0);
+            if (cshift != 0 && 16 * (q + 1) - cshift < span) y = a0[q + 1];
+            *reinterpret_cast<uint4*>(s_codes + 16 * q) = funnel16(x, y, cshift);
         }
         const int nz = (hshift + ttot + 16 + 15) >> 4;
         for (int q = tid; q < nz; q += kTile) reinterpret_cast<uint4*>(s_heap32)[q] = make_uint4(0, 0, 0, 0);
-        const unsigned long long eb = __ballot(esc);
-        if (lane == 0) ws_esc[wave] = eb != 0;
         __syncthreads();
-        const bool fast = (ws_esc[0] | ws_esc[1] | ws_esc[2] | ws_esc[3]) == 0;  // tile-uniform
         if (!(abl & 2)) switch ((span + 4 * kTile - 1) / (4 * kTile)) {  // dwords per thread, tile-uniform
         case 0:
-        case 1: fsst_segments<1>(s_codes, span, fast, s_sym, s_len, s_heap32, hshift, ttot, ws_b, err, abl); break;
-        case 2: fsst_segments<2>(s_codes, span, fast, s_sym, s_len, s_heap32, hshift, ttot, ws_b, err, abl); break;
-        case 3: fsst_segments<3>(s_codes, span, fast, s_sym, s_len, s_heap32, hshift, ttot, ws_b, err, abl); break;
-        case 4: fsst_segments<4>(s_codes, span, fast, s_sym, s_len, s_heap32, hshift, ttot, ws_b, err, abl); break;
-        case 5: fsst_segments<5>(s_codes, span, fast, s_sym, s_len, s_heap32, hshift, ttot, ws_b, err, abl); break;
-        default: fsst_segments<6>(s_codes, span, fast, s_sym, s_len, s_heap32, hshift, ttot, ws_b, err, abl); break;
+        case 1: fsst_segments<1>(s_codes, span, s_sym, s_len, s_heap32, hshift, ttot, ws_b, ws_esc, err, abl); break;
+        case 2: fsst_segments<2>(s_codes, span, s_sym, s_len, s_heap32, hshift, ttot, ws_b, ws_esc, err, abl); break;
+        case 3: fsst_segments<3>(s_codes, span, s_sym, s_len, s_heap32, hshift, ttot, ws_b, ws_esc, err, abl); break;
+        case 4: fsst_segments<4>(s_codes, span, s_sym, s_len, s_heap32, hshift, ttot, ws_b, ws_esc, err, abl); break;
+        case 5: fsst_segments<5>(s_codes, span, s_sym, s_len, s_heap32, hshift, ttot, ws_b, ws_esc, err, abl); break;
+        default: fsst_segments<6>(s_codes, span, s_sym, s_len, s_heap32, hshift, ttot, ws_b, ws_esc, err, abl); break;
         }
         static_assert(kCodeLds <= 6 * 4 * kTile, "six dwords per thread cover the staged codes");
         __syncthreads();
         // (d) copy-out of [tile_out0, tile_out0 + ttot): the image sits at the same offset mod 16
-        // as its destination, so whole aligned chunks move as ds_read_b128 + 16-byte stores;
-        // the ragged first/last chunk byte by byte (shared with the neighbouring tiles)
+        // as its destination, so whole aligned chunks [qa, qb) move as ds_read_b128 + 16-byte
+        // stores; the <= 15 + 15 bytes of the ragged first/last chunk (shared with the
+        // neighbouring tiles) are one byte store per lane of wave 0 (lanes 0-15 the head, 16-31
+        // the tail) instead of a per-thread loop of byte/short/dword stores.
         if (!(abl & 8)) {
             uint8_t* const gbase = heap + (tile_out0 - hshift);
-            const int nchunk_out = (hshift + ttot + 15) >> 4;
-            for (int q = tid; q < nchunk_out; q += kTile) {
-                const int lb = 16 * q;
-                if (lb >= hshift && lb + 16 <= hshift + ttot) {
-                    nt_store(reinterpret_cast<uint4*>(gbase + lb), *reinterpret_cast<const uint4*>(s_heap + lb));
-                } else {
-                    // ragged first/last chunk: its bytes [b0, b1) as byte / 2-byte / 4-byte stores
-                    // at their natural alignment (<= 7 stores instead of 16)
-                    int b0 = max(hshift - lb, 0);
-                    const int b1 = min(hshift + ttot - lb, 16);
-                    while (b0 < b1) {
-                        const int a = lb + b0;
-                        if ((b0 & 1) || b1 - b0 == 1) {
-                            gbase[a] = s_heap[a];
-                            b0 += 1;
-                        } else if ((b0 & 3) || b1 - b0 < 4) {
-                            *reinterpret_cast<uint16_t*>(gbase + a) = *reinterpret_cast<const uint16_t*>(s_heap + a);
-                            b0 += 2;
-                        } else {
-                            *reinterpret_cast<uint32_t*>(gbase + a) = *reinterpret_cast<const uint32_t*>(s_heap + a);
-                            b0 += 4;
-                        }
-                    }
-                }
+            const int end = hshift + ttot;
+            const int qa = (hshift + 15) >> 4, qb = end >> 4;
+            for (int q = qa + tid; q < qb; q += kTile)
+                nt_store(reinterpret_cast<uint4*>(gbase + 16 * q), *reinterpret_cast<const uint4*>(s_heap + 16 * q));
+            if (tid < 32) {
+                const int a = tid < 16 ? tid : 16 * qb + (tid - 16);
+                const bool in = tid < 16 ? (a >= hshift && a < min(16 * qa, end)) : (a >= max(16 * qb, 16 * qa) && a < end);
+                if (in) gbase[a] = s_heap[a];
             }
         }
         if (live && !(abl & 16)) {

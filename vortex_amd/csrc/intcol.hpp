@@ -19,8 +19,30 @@ __device__ __forceinline__ int64_t ld(const void* p, uint64_t i) {
     else return static_cast<const int64_t*>(p)[i];
 }
 
-// Element i of a T-bit FastLanes column of bit width W (both candidate words are loaded
-// unconditionally so they retire under one wait), then FoR (wrapping in T), sign-extended
+// Value `idx` (< 1024) of the FastLanes block at `blk` (T-bit words, bit width 0 < W <= T):
+// unpack_single's (lane, row) -> bit offset row * W in the lane's words.  Both candidate words are
+// loaded unconditionally (they retire under one wait; no branch the compiler could sink the
+// second load into), the T = 32 pair is one funnel shift (v_alignbit), row * W a 24-bit multiply.
+template <int T>
+__device__ __forceinline__ std::conditional_t<T == 32, uint32_t, uint64_t> fl_word_pair(
+    const std::conditional_t<T == 32, uint32_t, uint64_t>* blk, uint32_t idx, uint32_t W) {
+    using E = std::conditional_t<T == 32, uint32_t, uint64_t>;
+    constexpr uint32_t LANES = 1024 / T;
+    const uint32_t lane = idx % LANES, s = idx >> 7;
+    const uint32_t fl = ((idx & 127) - lane) >> 4;
+    const uint32_t row = (((fl & 1) << 2) | (fl & 2) | (fl >> 2)) * 8 + s;  // FL_ORDER[fl]*8 + s
+    const uint32_t start = __umul24(row, W), word = start / T, sh = start % T;
+    const uint32_t word2 = word + 1 < W ? word + 1 : word;
+    const E lo = blk[LANES * word + lane], hi = blk[LANES * word2 + lane];
+    const E mask = W >= uint32_t(T) ? E(~E(0)) : E((E(1) << W) - 1);
+    if constexpr (T == 32) {
+        return __builtin_amdgcn_alignbit(hi, lo, sh) & mask;
+    } else {
+        return (sh ? (lo >> sh) | (hi << (64 - sh)) : lo) & mask;
+    }
+}
+
+// Element i of a T-bit FastLanes column of bit width W, then FoR (wrapping in T), sign-extended
 // when the logical type is signed.
 template <int T>
 __device__ __forceinline__ int64_t fl_get(const void* packed, uint32_t W, uint32_t shift, uint32_t offset,
@@ -30,17 +52,7 @@ __device__ __forceinline__ int64_t fl_get(const void* packed, uint32_t W, uint32
     E v = 0;
     if (W != 0) {
         const uint64_t g = i + offset;
-        const uint32_t idx = uint32_t(g & 1023);
-        const uint32_t lane = idx % LANES, s = idx >> 7;
-        const uint32_t fl = ((idx & 127) - lane) >> 4;
-        const uint32_t row = (((fl & 1) << 2) | (fl & 2) | (fl >> 2)) * 8 + s;  // FL_ORDER[fl]*8 + s
-        const E* base = static_cast<const E*>(packed) + (g >> 10) * (uint64_t(LANES) * W);
-        const uint32_t start = row * W, word = start / T, sh = start % T;
-        const uint32_t word2 = word + 1 < W ? word + 1 : word;
-        const E lo = base[LANES * word + lane], hi = base[LANES * word2 + lane];
-        v = lo >> sh;
-        if (sh + W > uint32_t(T)) v |= hi << (T - sh);
-        if (W < uint32_t(T)) v &= (E(1) << W) - 1;
+        v = fl_word_pair<T>(static_cast<const E*>(packed) + (g >> 10) * (uint64_t(LANES) * W), uint32_t(g & 1023), W);
     }
     const E r = E(E(v << shift) + E(reference));
     if constexpr (T == 64) return int64_t(r);
