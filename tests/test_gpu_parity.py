@@ -735,6 +735,37 @@ def test_chunked_runend_batched(ctx):
     assert_primitive_parity(A.chunked(chunks), ctx, np.concatenate(expect))
 
 
+def sys_path_bench():
+    import sys
+    from pathlib import Path
+    root = str(Path(__file__).resolve().parent.parent)
+    if root not in sys.path:
+        sys.path.insert(0, root)
+
+
+class plan_mode:
+    """VXG_PLAN_BATCH for the plans created inside (capi.hip reads it at every vxg_plan_create):
+    "0" unbatched, "1" batched, "mixed", None = the default (both recorded, the faster kept)."""
+
+    def __init__(self, mode):
+        self.mode = mode
+
+    def __enter__(self):
+        import os
+        self.old = os.environ.get("VXG_PLAN_BATCH")
+        if self.mode is None:
+            os.environ.pop("VXG_PLAN_BATCH", None)
+        else:
+            os.environ["VXG_PLAN_BATCH"] = self.mode
+
+    def __exit__(self, *exc):
+        import os
+        if self.old is None:
+            os.environ.pop("VXG_PLAN_BATCH", None)
+        else:
+            os.environ["VXG_PLAN_BATCH"] = self.old
+
+
 def test_plan_graph_replay_matches_direct(ctx):
     """vxg_plan: the recorded HIP graph reproduces vxg_canonicalize's bytes on every replay,
     and a replay reads the CURRENT contents of the input buffers (new batch, same buffers)."""
@@ -839,7 +870,8 @@ def test_plan_k1g_every_kind(ctx):
     strs = [[words[i] for i in rng.integers(0, 4, n)] for n in (3000, 1, 5000)]
     sarr = A.chunked([E.encode_dict_strings(s) for s in strs])
     arrs = [c for c, _ in cols] + [sarr]
-    plan = V.Plan([a.to(torch.device("cuda", 0)) for a in arrs], ctx)
+    with plan_mode("1"):
+        plan = V.Plan([a.to(torch.device("cuda", 0)) for a in arrs], ctx)
     for _ in range(2):
         res = plan.launch(sync=True)
         for k, ((a, exp), r) in enumerate(zip(cols, res)):
@@ -863,7 +895,8 @@ def test_plan_mixed_large_and_small_arrays(ctx):
                          for i in range(0, big.size, 1 << 20)])
     cols = _k1g_columns(rng)[:6]
     arrs = [big_arr] + [c for c, _ in cols]
-    plan = V.Plan([a.to(torch.device("cuda", 0)) for a in arrs], ctx)
+    with plan_mode("1"):
+        plan = V.Plan([a.to(torch.device("cuda", 0)) for a in arrs], ctx)
     for _ in range(2):
         res = plan.launch(sync=True)
         assert res[0].numpy().tobytes() == big.tobytes()
@@ -935,7 +968,8 @@ def test_plan_nested_chunked_not_deferred(ctx):
     scodes = rng.integers(0, sdict.len, 9000).astype(np.uint8)
     sarr = A.dict_array(sdict, E.encode_bitpacked(scodes, bit_width=3, allow_patches=False))
     arrs = [root] + [a for a, _ in cases] + [sarr]
-    plan = V.Plan([a.to(torch.device("cuda", 0)) for a in arrs], ctx)
+    with plan_mode("1"):
+        plan = V.Plan([a.to(torch.device("cuda", 0)) for a in arrs], ctx)
     for _ in range(3):
         res = plan.launch(sync=True)
         assert res[0].numpy().tobytes() == canon(root)[0].tobytes()
@@ -1115,6 +1149,57 @@ def test_plan_with_bool_columns(ctx):
         res = plan.launch(sync=True)
         assert np.array_equal(res[0].numpy(), m) and np.array_equal(res[1].numpy(), m)
         assert np.array_equal(res[2].validity_mask(), ~m)
+    plan.close()
+
+
+@pytest.mark.parametrize("mode", ["0", "1", "mixed", None])
+def test_plan_modes_non_c5_mix(ctx, mode):
+    """A plan over a table that is not C5's shape -- a C3-like shard (Chunked[Dict(codes=BitPacked
+    u64 W=10, u64 values)], 6 chunks), a C4-like FSST column, bool columns (RunEndBool, ByteBool,
+    a primitive with a RunEndBool validity) and one large chunked u32 column -- recorded unbatched,
+    batched, mixed (arrays <= VXG_PLAN_BATCH_MAX_BYTES batched) and by default (both recorded, the
+    faster kept): every replay byte-identical to the oracle in every mode."""
+    import torch
+    sys_path_bench()
+    import bench
+    rng = np.random.default_rng(303)
+    dvals = rng.integers(0, 1 << 62, 1024, dtype=np.uint64)
+    c3, c3_plain = [], []
+    for k in range(6):
+        codes = rng.integers(0, 1024, 64 * 1024 + 37 * k, dtype=np.uint64)
+        c3.append(A.dict_array(A.primitive(dvals), E.encode_bitpacked(codes, bit_width=10, allow_patches=False)))
+        c3_plain.append(dvals[codes])
+    c3_arr = A.chunked(c3)
+    heap, offs = bench.c4_heap(rng, 60_000)
+    c4_arr = E.encode_fsst_from_heap(heap, offs)
+    m = rng.integers(0, 2, 150_000).astype(bool)
+    big = rng.integers(0, 1 << 13, 3 * (1 << 20), dtype=np.uint64).astype(np.uint32)  # 12 MB out
+    big_arr = A.chunked([E.encode_bitpacked(big[i:i + (1 << 20)], bit_width=13, allow_patches=False)
+                         for i in range(0, big.size, 1 << 20)])
+    arrs = [c3_arr, c4_arr, E.encode_runend_bool(m), A.byte_bool(m),
+            A.primitive(np.arange(m.size, dtype=np.uint32), validity=E.encode_runend_bool(~m)), big_arr]
+    env = {} if mode is None else {"VXG_PLAN_BATCH_MAX_BYTES": str(4 << 20)}  # mixed: big_arr unbatched
+    import os
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        with plan_mode(mode):
+            plan = V.Plan([a.to(torch_dev()) for a in arrs], ctx)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    (rviews, rheap), _ = canon(c4_arr)  # one data buffer (not chunked)
+    for _ in range(2):
+        res = plan.launch(sync=True)
+        assert res[0].numpy().tobytes() == np.concatenate(c3_plain).tobytes()
+        assert res[1].numpy()[0].tobytes() == rviews.tobytes()
+        assert [b.tobytes() for b in res[1].buffers()] == [rheap.tobytes()]
+        assert np.array_equal(res[2].numpy(), m) and np.array_equal(res[3].numpy(), m)
+        assert np.array_equal(res[4].validity_mask(), ~m)
+        assert res[5].numpy().tobytes() == big.tobytes()
     plan.close()
 
 

@@ -5,7 +5,7 @@ so a rocprofv3 --kernel-trace of this script gives each kernel its own duration)
 HIP events over `reps` back-to-back steps; prints one JSON line per column with its kernel
 time, algorithmic bytes (compressed buffers read + canonical bytes written) and fraction of the
 8 TB/s HBM roofline, then the sum.  Usage:
-  python tools/c5_columns.py [--world N --rank R] [--reps 20]
+  python tools/c5_columns.py [--world N --rank R] [--reps 20] [--mark]
 """
 from __future__ import annotations
 
@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--world", type=int, default=1)
     ap.add_argument("--rank", type=int, default=0)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--mark", action="store_true",
+                    help="launch a torch kernel before every column (segments a rocprofv3 --pmc trace; tools/c5_traffic.py)")
     args = ap.parse_args()
     import torch
     import bench
@@ -38,9 +40,14 @@ def main():
     f = VortexFile(host)
     dc = DeviceColumns(f, ctx, None, mine.start, mine.stop)
     tot_t = tot_p = tot_b = 0.0
+    marker = torch.zeros(1, device="cuda")
     for col, node in zip(dc.columns, dc.nodes):
         keep: list = []
         o, res = A.alloc_canonical(ctx, node, keep)
+        if args.mark:  # after the output sizing (its length readback is not a decode step)
+            torch.cuda.synchronize()
+            marker.add_(1)
+            torch.cuda.synchronize()
 
         def step():
             _lib.check(ctx.lib.vxg_canonicalize(ctx.handle, C.byref(node), C.byref(o), ctx.stream_ptr()))

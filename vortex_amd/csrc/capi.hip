@@ -1957,24 +1957,28 @@ static uint32_t plan_branches_env() {
     return nb;
 }
 
-// Plan batching (PlanBatch + K1g on one branch) is all-or-nothing: it is used when every array's
-// canonical output is <= VXG_PLAN_BATCH_MAX_BYTES (default 64 MiB; 0 disables) and the plan's total
-// is <= VXG_PLAN_BATCH_TOTAL_BYTES (default 400 MB).  C5 per GPU (tools/gpu_thresh.sh): 8-GPU
-// shard (140 MB) 0.120 -> 0.061 ms/step batched; 4-GPU shard (275 MB) 0.131 -> 0.106; 2-GPU
-// shard (550 MB) 0.179 unbatched vs 0.200 batched; mixing batched and unbatched arrays in one
-// plan measured slower than either.
+// Plan batching (PlanBatch + K1g).  Whether it pays depends on the table: C5 per GPU at 8 / 4 GPUs
+// (140 / 275 MB) measured 0.060 / 0.095 ms batched vs 0.120 / 0.131 unbatched, but 0.200 vs
+// 0.180 at 2 GPUs (550 MB), and mixing batched and unbatched arrays was slower than either
+// (tools/gpu_thresh.sh).  So the default is measured, not a byte threshold: vxg_plan_create
+// records the plan both ways (unbatched on 2 graph branches, batched on 1) and keeps the one
+// whose replays are faster (3 interleaved timed replays each after one warm-up).  The knob
+// VXG_PLAN_BATCH (read at every create) is a diagnostic: "0" unbatched, "1" batched, "mixed"
+// (arrays whose output is <= VXG_PLAN_BATCH_MAX_BYTES batched, the others not), unset = measured.
+enum class BatchMode { Auto, Off, On, Mixed };
+static BatchMode plan_batch_mode() {
+    const char* e = std::getenv("VXG_PLAN_BATCH");
+    if (!e || !*e) return BatchMode::Auto;
+    if (e[0] == '0') return BatchMode::Off;
+    if (e[0] == '1') return BatchMode::On;
+    if (e[0] == 'm') return BatchMode::Mixed;
+    return BatchMode::Auto;
+}
 static uint64_t env_bytes(const char* name, uint64_t dflt) {
     const char* e = std::getenv(name);
     return e ? uint64_t(std::strtoull(e, nullptr, 10)) : dflt;
 }
-static uint64_t plan_batch_max_bytes() {
-    static const uint64_t v = env_bytes("VXG_PLAN_BATCH_MAX_BYTES", uint64_t(64) << 20);
-    return v;
-}
-static uint64_t plan_batch_total_bytes() {
-    static const uint64_t v = env_bytes("VXG_PLAN_BATCH_TOTAL_BYTES", uint64_t(400) * 1000 * 1000);
-    return v;
-}
+static uint64_t plan_batch_max_bytes() { return env_bytes("VXG_PLAN_BATCH_MAX_BYTES", uint64_t(64) << 20); }
 
 static uint64_t canonical_out_bytes(const vxg_array& a) {
     const bool str = a.dtype == VXG_DTYPE_UTF8 || a.dtype == VXG_DTYPE_BINARY;
@@ -1990,6 +1994,7 @@ struct vxg_plan {
     // FSST pre-pass -> decode -> K1g) replays as direct launches of its kernel nodes: one stream,
     // no graph-to-graph dependency (a graph replay boundary cost ~14 us on the C5 shard).
     std::vector<hipKernelNodeParams> direct;
+    bool batched = false;  // recorded with a PlanBatch (diagnostics)
 };
 
 // Direct replay of short kernel chains (VXG_PLAN_DIRECT=0 disables; at most
@@ -2055,44 +2060,20 @@ static std::vector<hipKernelNodeParams> kernel_chain(hipGraph_t g) {
     return out;
 }
 
-extern "C" {
-
-vxg_status vxg_plan_create(vxg_ctx* ctx, const vxg_array* arrays, vxg_canonical* outs, uint32_t n, vxg_plan** plan) {
-    VXG_TRY(use_device(ctx));
-    if (!plan || (n && (!arrays || !outs))) return set_error(VXG_ERR_INVALID_ARGUMENT, "null plan/arrays/outs");
+// Record one candidate plan: arrays with batched[i] defer their deferrable launches into one
+// PlanBatch flushed at the end; `branches` parallel graph branches (arrays spread longest-first).
+static vxg_status record_plan(vxg_ctx* ctx, const vxg_array* arrays, vxg_canonical* outs, uint32_t n,
+                              const std::vector<bool>& batched, uint32_t branches, vxg_plan** plan) {
     *plan = nullptr;
-    for (uint32_t i = 0; i < n; i++) {  // nothing may allocate or synchronise while recording
-        const vxg_array& a = arrays[i];
-        const vxg_canonical& o = outs[i];
-        const bool str = a.dtype == VXG_DTYPE_UTF8 || a.dtype == VXG_DTYPE_BINARY;
-        if (str ? (!o.views || !o.data) : !o.values)
-            return set_error(VXG_ERR_INVALID_ARGUMENT, "a plan needs caller-allocated outputs");
-        if (a.nullable && !o.validity)
-            return set_error(VXG_ERR_INVALID_ARGUMENT, "a plan needs caller-allocated validity for nullable arrays");
-    }
-    // Record on an origin stream forked into kPlanBranches streams (2: measured 0.343-0.358
-    // ms/step on C5 vs 0.363-0.364 with 4 and 0.389 with 1, tools/gpu_branches.sh): the arrays are
-    // independent, so their launches become parallel graph branches (the graph runs them on
-    // several hardware queues, overlapping the ramp and drain of the many small kernels of a
-    // chunked scan), joined back into the origin stream.
-    // The small arrays' deferrable launches (PlanBatch: K1 decodes, RunEnd expansions,
-    // dictionary views of chunked columns) go to one more branch, recorded after all arrays were
-    // visited.
-    uint64_t total = 0;
-    bool all_small = n > 0;
-    for (uint32_t i = 0; i < n; i++) {
-        const uint64_t b = canonical_out_bytes(arrays[i]);
-        total += b;
-        all_small = all_small && b <= plan_batch_max_bytes();
-    }
-    const bool batching = all_small && total <= plan_batch_total_bytes();
-    // Branches: 2 by default; ONE when the plan is batched (a sharded scan): each cross-branch
-    // edge of a graph costs the replay several microseconds of queue synchronisation, more than
-    // the small kernels gain from overlapping (C5 8-GPU shard: 82 -> 68 us per replay).
-    const uint32_t kPlanBranches = plan_branches_env() ? plan_branches_env() : (batching ? 1u : 2u);
-    // (one branch requested: the batch follows the arrays on that branch -- a single-stream graph)
-    const bool own = batching && kPlanBranches > 1;
-    const uint32_t nb = (n < kPlanBranches ? (n ? n : 1) : kPlanBranches) + (own ? 1 : 0);
+    const bool batching = std::find(batched.begin(), batched.end(), true) != batched.end();
+    // Record on an origin stream forked into `branches` streams: the arrays are independent, so
+    // their launches become parallel graph branches (the graph runs them on several hardware
+    // queues, overlapping the ramp and drain of the many small kernels of a chunked scan), joined
+    // back into the origin stream.  The batched arrays' deferrable launches (K1 decodes, RunEnd
+    // expansions, dictionary views of chunked columns) go to one more branch -- or, with one
+    // branch, follow the arrays on it (a single-stream graph) -- recorded after every array.
+    const bool own = batching && branches > 1;
+    const uint32_t nb = (n < branches ? (n ? n : 1) : branches) + (own ? 1 : 0);
     const uint32_t na = own ? nb - 1 : nb;  // branches the arrays are spread over
     PlanBatch batch;
     hipStream_t cs;
@@ -2106,6 +2087,7 @@ vxg_status vxg_plan_create(vxg_ctx* ctx, const vxg_array* arrays, vxg_canonical*
         st = hip_check(hipEventCreateWithFlags(&ev[b], hipEventDisableTiming), "plan event");
     auto* pl = new vxg_plan();
     pl->ctx = ctx;
+    pl->batched = batching;
     if (st == VXG_OK) st = hip_check(hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed), "hipStreamBeginCapture");
     if (st == VXG_OK) {
         st = hip_check(hipEventRecord(ev[nb], cs), "fork");
@@ -2125,7 +2107,7 @@ vxg_status vxg_plan_create(vxg_ctx* ctx, const vxg_array* arrays, vxg_canonical*
             const uint32_t i = order[k];
             const uint32_t b = uint32_t(std::min_element(load.begin(), load.end()) - load.begin());
             load[b] += cost[i];
-            Planner p(ctx, br[b], &pl->store, batching ? &batch : nullptr);
+            Planner p(ctx, br[b], &pl->store, batched[i] ? &batch : nullptr);
             st = p.canonical(arrays[i], outs[i]);
         }
         if (batching && st == VXG_OK) st = flush_plan_batch(batch, ctx->c.err_word, br[nb - 1], &pl->store);
@@ -2149,6 +2131,97 @@ vxg_status vxg_plan_create(vxg_ctx* ctx, const vxg_array* arrays, vxg_canonical*
     (void)hipStreamDestroy(cs);
     if (st == VXG_OK) *plan = pl;
     else vxg_plan_destroy(pl);
+    return st;
+}
+
+// Median device time of `reps` interleaved replays of each candidate (after one warm-up each).
+static vxg_status time_plans(const std::vector<vxg_plan*>& cands, int reps, std::vector<float>* ms) {
+    hipStream_t s;
+    VXG_TRY(hip_check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "plan timing stream"));
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    vxg_status st = hip_check(hipEventCreate(&e0), "plan timing event");
+    if (st == VXG_OK) st = hip_check(hipEventCreate(&e1), "plan timing event");
+    std::vector<std::vector<float>> t(cands.size());
+    for (vxg_plan* p : cands)
+        if (st == VXG_OK) st = vxg_plan_launch(p, s);
+    for (int r = 0; r < reps && st == VXG_OK; r++) {
+        for (size_t c = 0; c < cands.size() && st == VXG_OK; c++) {
+            st = hip_check(hipEventRecord(e0, s), "plan timing");
+            if (st == VXG_OK) st = vxg_plan_launch(cands[c], s);
+            if (st == VXG_OK) st = hip_check(hipEventRecord(e1, s), "plan timing");
+            if (st == VXG_OK) st = hip_check(hipEventSynchronize(e1), "plan timing");
+            float x = 0;
+            if (st == VXG_OK) st = hip_check(hipEventElapsedTime(&x, e0, e1), "plan timing");
+            t[c].push_back(x);
+        }
+    }
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    (void)hipStreamSynchronize(s);
+    (void)hipStreamDestroy(s);
+    ms->clear();
+    for (auto& v : t) {
+        std::sort(v.begin(), v.end());
+        ms->push_back(v.empty() ? 0.f : v[v.size() / 2]);
+    }
+    return st;
+}
+
+extern "C" {
+
+vxg_status vxg_plan_create(vxg_ctx* ctx, const vxg_array* arrays, vxg_canonical* outs, uint32_t n, vxg_plan** plan) {
+    VXG_TRY(use_device(ctx));
+    if (!plan || (n && (!arrays || !outs))) return set_error(VXG_ERR_INVALID_ARGUMENT, "null plan/arrays/outs");
+    *plan = nullptr;
+    for (uint32_t i = 0; i < n; i++) {  // nothing may allocate or synchronise while recording
+        const vxg_array& a = arrays[i];
+        const vxg_canonical& o = outs[i];
+        const bool str = a.dtype == VXG_DTYPE_UTF8 || a.dtype == VXG_DTYPE_BINARY;
+        if (str ? (!o.views || !o.data) : !o.values)
+            return set_error(VXG_ERR_INVALID_ARGUMENT, "a plan needs caller-allocated outputs");
+        if (a.nullable && !o.validity)
+            return set_error(VXG_ERR_INVALID_ARGUMENT, "a plan needs caller-allocated validity for nullable arrays");
+    }
+    // candidates: (batched mask, branches); 2 branches unbatched (C5 at 1 GPU 322.6 us/replay vs
+    // 362 with 1 and 348 with 3), 1 batched (each cross-branch edge costs a replay several
+    // microseconds of queue synchronisation: C5 shard 82 -> 68 us)
+    const uint32_t env_br = plan_branches_env();
+    const std::vector<bool> none(n, false), all(n, true);
+    std::vector<bool> mixed(n);
+    for (uint32_t i = 0; i < n; i++) mixed[i] = canonical_out_bytes(arrays[i]) <= plan_batch_max_bytes();
+    std::vector<std::pair<std::vector<bool>, uint32_t>> cand;
+    switch (plan_batch_mode()) {
+    case BatchMode::Off: cand.emplace_back(none, env_br ? env_br : 2u); break;
+    case BatchMode::On: cand.emplace_back(all, env_br ? env_br : 1u); break;
+    case BatchMode::Mixed: cand.emplace_back(mixed, env_br ? env_br : 2u); break;
+    case BatchMode::Auto:
+        cand.emplace_back(none, env_br ? env_br : 2u);
+        if (n) cand.emplace_back(all, env_br ? env_br : 1u);
+        break;
+    }
+    std::vector<vxg_plan*> plans;
+    vxg_status st = VXG_OK;
+    for (const auto& [mask, branches] : cand) {
+        vxg_plan* p = nullptr;
+        st = record_plan(ctx, arrays, outs, n, mask, branches, &p);
+        if (st != VXG_OK) break;
+        plans.push_back(p);
+    }
+    size_t best = 0;
+    if (st == VXG_OK && plans.size() > 1) {
+        std::vector<float> ms;
+        st = time_plans(plans, 3, &ms);
+        for (size_t c = 1; c < ms.size(); c++)
+            if (ms[c] < ms[best]) best = c;
+        if (std::getenv("VXG_PLAN_DEBUG"))
+            for (size_t c = 0; c < ms.size(); c++)
+                std::fprintf(stderr, "plan candidate %zu (%s, %zu kernel-chain nodes): %.4f ms%s\n", c,
+                             plans[c]->batched ? "batched" : "unbatched", plans[c]->direct.size(), ms[c],
+                             c == best ? "  <- kept" : "");
+    }
+    for (size_t c = 0; c < plans.size(); c++)
+        if (st != VXG_OK || c != best) vxg_plan_destroy(plans[c]);
+    if (st == VXG_OK && !plans.empty()) *plan = plans[best];
     return st;
 }
 
