@@ -390,7 +390,7 @@ template <int ND>
 __device__ __forceinline__ void fsst_segments(const uint8_t* __restrict__ s_codes, int span,
                                               const uint64_t* __restrict__ s_sym, const uint8_t* __restrict__ s_len,
                                               uint32_t* __restrict__ s_heap32, int hshift, int ttot, int* ws_b,
-                                              unsigned* ws_esc, uint32_t* __restrict__ err, uint32_t abl) {
+                                              unsigned* ws_esc, uint32_t* __restrict__ err) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int s0 = tid * 4 * ND;
     const bool act = s0 < span;
@@ -465,7 +465,7 @@ __device__ __forceinline__ void fsst_segments(const uint8_t* __restrict__ s_code
     }
     if (tid == 0 && dec_total != ttot) __hip_atomic_fetch_or(err, kErrFsst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // a tile whose codes do not decode to its length sum (corrupt input, flagged above) is not written
-    if (!act || dec_total != ttot || (abl & 4)) return;
+    if (!act || dec_total != ttot) return;
     uint32_t o8 = uint32_t(hshift + seg_rel) << 3;  // bit position in the image
     auto put = [&](uint64_t m, uint32_t L8) {
         // (w1:w0) = sym << 8(o & 3), w2 = the bytes shifted past them
@@ -514,7 +514,7 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) v
                                                      const int64_t* __restrict__ block_totals_all,
                                                      const int64_t* __restrict__ tile_code_all,
                                                      uint32_t* __restrict__ err,
-                                                     const uint32_t* __restrict__ wg_chunk, uint32_t abl) {
+                                                     const uint32_t* __restrict__ wg_chunk) {
     __shared__ uint64_t s_sym[256];
     __shared__ uint8_t s_len[256];
     __shared__ int ws_a[kTile / 64], ws_b[kTile / 64];
@@ -618,7 +618,6 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     const int64_t tile_out0 = tp + s_block_prefix;
     const bool stage = !any_bad && span_ok && tile_total <= kHeapLds;
 
-    if (abl & 1) return;
     if (stage) {
         // (b) stage the tile's code bytes into LDS shifted so that the tile's first code is
         // s_codes[0] (chunk tid was loaded in the prologue; larger tiles load the rest here),
@@ -635,14 +634,14 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         const int nz = (hshift + ttot + 16 + 15) >> 4;
         for (int q = tid; q < nz; q += kTile) reinterpret_cast<uint4*>(s_heap32)[q] = make_uint4(0, 0, 0, 0);
         __syncthreads();
-        if (!(abl & 2)) switch ((span + 4 * kTile - 1) / (4 * kTile)) {  // dwords per thread, tile-uniform
+        switch ((span + 4 * kTile - 1) / (4 * kTile)) {  // dwords per thread, tile-uniform
         case 0:
-        case 1: fsst_segments<1>(s_codes, span, s_sym, s_len, s_heap32, hshift, ttot, ws_b, ws_esc, err, abl); break;
-        case 2: fsst_segments<2>(s_codes, span, s_sym, s_len, s_heap32, hshift, ttot, ws_b, ws_esc, err, abl); break;
-        case 3: fsst_segments<3>(s_codes, span, s_sym, s_len, s_heap32, hshift, ttot, ws_b, ws_esc, err, abl); break;
-        case 4: fsst_segments<4>(s_codes, span, s_sym, s_len, s_heap32, hshift, ttot, ws_b, ws_esc, err, abl); break;
-        case 5: fsst_segments<5>(s_codes, span, s_sym, s_len, s_heap32, hshift, ttot, ws_b, ws_esc, err, abl); break;
-        default: fsst_segments<6>(s_codes, span, s_sym, s_len, s_heap32, hshift, ttot, ws_b, ws_esc, err, abl); break;
+        case 1: fsst_segments<1>(s_codes, span, s_sym, s_len, s_heap32, hshift, ttot, ws_b, ws_esc, err); break;
+        case 2: fsst_segments<2>(s_codes, span, s_sym, s_len, s_heap32, hshift, ttot, ws_b, ws_esc, err); break;
+        case 3: fsst_segments<3>(s_codes, span, s_sym, s_len, s_heap32, hshift, ttot, ws_b, ws_esc, err); break;
+        case 4: fsst_segments<4>(s_codes, span, s_sym, s_len, s_heap32, hshift, ttot, ws_b, ws_esc, err); break;
+        case 5: fsst_segments<5>(s_codes, span, s_sym, s_len, s_heap32, hshift, ttot, ws_b, ws_esc, err); break;
+        default: fsst_segments<6>(s_codes, span, s_sym, s_len, s_heap32, hshift, ttot, ws_b, ws_esc, err); break;
         }
         static_assert(kCodeLds <= 6 * 4 * kTile, "six dwords per thread cover the staged codes");
         __syncthreads();
@@ -651,7 +650,7 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         // stores; the <= 15 + 15 bytes of the ragged first/last chunk (shared with the
         // neighbouring tiles) are one byte store per lane of wave 0 (lanes 0-15 the head, 16-31
         // the tail) instead of a per-thread loop of byte/short/dword stores.
-        if (!(abl & 8)) {
+        {
             uint8_t* const gbase = heap + (tile_out0 - hshift);
             const int end = hshift + ttot;
             const int qa = (hshift + 15) >> 4, qb = end >> 4;
@@ -663,7 +662,7 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) v
                 if (in) gbase[a] = s_heap[a];
             }
         }
-        if (live && !(abl & 16)) {
+        if (live) {
             const bool valid = (vbyte >> (tid & 7)) & 1;
             views[first + tid] = valid ? lds_view(s_heap32, hshift + int(my_rel), uint32_t(my_len),
                                                   uint32_t(tile_out0 + my_rel), bidx)
@@ -752,8 +751,6 @@ bool with_acc(int kind, F&& f) {
 
 vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint32_t* err, hipStream_t s,
                              DevTables* dt) {
-    const char* abl_env = std::getenv("VXG_FSST_ABL");  // TEMP ablation
-    const uint32_t abl = abl_env ? uint32_t(std::strtoul(abl_env, nullptr, 10)) : 0u;
     for (const FsstChunk& c : chunks) {
         if (c.n_symbols > 255) return set_error(VXG_ERR_INVALID_ARGUMENT, "FSST symbol table > 255 entries");
         if ((c.n + kTS - 1) / kTS > 0xFFFFFFFFull) return set_error(VXG_ERR_INVALID_ARGUMENT, "FSST array too long");
@@ -822,7 +819,7 @@ vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint
                             hipLaunchKernelGGL((fsst_tile_scan<LA, X>), dim3(unsigned(scans)), dim3(kTile), 0, s, tab,
                                                tp, bt, tc);
                         hipLaunchKernelGGL((fsst_decode<OA, LA, X>), dim3(unsigned(tiles)), dim3(kTile), 0, s, tab,
-                                           tiles, tp, bt, tc, err, wg_chunk, abl);
+                                           tiles, tp, bt, tc, err, wg_chunk);
                     };
                     if (tab.ext) go(std::true_type{});
                     else go(std::false_type{});

@@ -132,7 +132,28 @@ __device__ __forceinline__ void runend_runs_body(const RunEndChunk& c, uint64_t 
 #pragma unroll
         for (int k = 0; k < PER; k++) s_head[tid * PER + k] = uint16_t(max(vv[k], before));
         __syncthreads();
-        for (int i = tid; i < wn; i += kBlock) nt_store(out + wb + i, s_val[s_head[i] - 1]);
+        if constexpr (sizeof(V) == 4 || sizeof(V) == 8) {
+            // two consecutive outputs per lane, one 8/16-byte store (half the per-output address
+            // work of a VALU-bound loop; 1 KiB per store instruction for u64)
+            using P = std::conditional_t<sizeof(V) == 8, uint4, uint64_t>;
+            // pairs start at a 2V-aligned output (the window's first output alone if it is not)
+            const int a = int((reinterpret_cast<uintptr_t>(out + wb) / sizeof(V)) & 1);
+            if (a && tid == 0 && wn > 0) nt_store(out + wb, s_val[s_head[0] - 1]);
+            for (int i = a + 2 * tid; i < wn; i += 2 * kBlock) {
+                const V v0 = s_val[s_head[i] - 1];
+                if (i + 1 < wn) {
+                    const V v1 = s_val[s_head[i + 1] - 1];
+                    P pv;
+                    __builtin_memcpy(&pv, &v0, sizeof(V));
+                    __builtin_memcpy(reinterpret_cast<uint8_t*>(&pv) + sizeof(V), &v1, sizeof(V));
+                    nt_store(reinterpret_cast<P*>(out + wb + i), pv);
+                } else {
+                    nt_store(out + wb + i, v0);
+                }
+            }
+        } else {
+            for (int i = tid; i < wn; i += kBlock) nt_store(out + wb + i, s_val[s_head[i] - 1]);
+        }
         if (tid == 0) s_carry = s_head[wn - 1];
         __syncthreads();
         carry = s_carry;
