@@ -14,7 +14,7 @@ from pathlib import Path
 
 
 def short(name: str) -> str:
-    return name.split("(")[0][:90]
+    return name.replace("(anonymous namespace)::", "").split("(")[0][:90]
 
 
 def main():
