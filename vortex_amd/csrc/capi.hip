@@ -1941,10 +1941,21 @@ static uint64_t tree_bytes(const vxg_array& a) {
     return b;
 }
 
+// Encoding that decides an array's decode kernel: the first non-Chunked node of its tree.
+static uint16_t leading_encoding(const vxg_array& a) {
+    return a.encoding == VXG_ENC_CHUNKED && a.n_children ? leading_encoding(a.children[0]) : a.encoding;
+}
+
+// Branch-balancing weight: estimated device time ~ bytes moved / the kernel's measured fraction
+// of the HBM roofline (round 3, each lineitem column alone, profiles/r03_c5_columns_w1.jsonl):
+// FSST 0.45, string dictionaries (16-byte views) 0.55, short-run RunEnd 0.34, other decodes ~0.7.
 static uint64_t plan_cost(const vxg_array& a) {
     const bool str = a.dtype == VXG_DTYPE_UTF8 || a.dtype == VXG_DTYPE_BINARY;
     const uint64_t out = a.dtype == VXG_DTYPE_BOOL ? a.len / 8 : a.len * (str ? 16 : ptype_width(a.ptype));
-    return tree_bytes(a) + out;
+    const uint64_t bytes = tree_bytes(a) + out;
+    const uint16_t e = leading_encoding(a);
+    const uint64_t pct = e == VXG_ENC_FSST ? 45 : e == VXG_ENC_RUN_END ? 34 : str ? 55 : 70;
+    return bytes * 100 / pct;
 }
 
 // Parallel graph branches of a plan (VXG_PLAN_BRANCHES overrides, 1..16; 0 = unset).
@@ -2215,9 +2226,9 @@ vxg_status vxg_plan_create(vxg_ctx* ctx, const vxg_array* arrays, vxg_canonical*
             if (ms[c] < ms[best]) best = c;
         if (std::getenv("VXG_PLAN_DEBUG"))
             for (size_t c = 0; c < ms.size(); c++)
-                std::fprintf(stderr, "plan candidate %zu (%s, %zu kernel-chain nodes): %.4f ms%s\n", c,
-                             plans[c]->batched ? "batched" : "unbatched", plans[c]->direct.size(), ms[c],
-                             c == best ? "  <- kept" : "");
+                std::fprintf(stderr, "plan candidate %zu (%s, %u branches, %zu kernel-chain nodes): %.4f ms%s\n", c,
+                             plans[c]->batched ? "batched" : "unbatched", cand[c].second, plans[c]->direct.size(),
+                             ms[c], c == best ? "  <- kept" : "");
     }
     for (size_t c = 0; c < plans.size(); c++)
         if (st != VXG_OK || c != best) vxg_plan_destroy(plans[c]);
