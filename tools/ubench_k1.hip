@@ -257,6 +257,58 @@ __global__ __launch_bounds__(256) void k_burst(const uint4* __restrict__ in, uin
     }
 }
 
+// Pipelined burst copy: persistent workgroups, two LDS buffers; the next group's input is requested
+// with LDS-DMA (global_load_lds_dwordx4: no VGPRs) BEFORE the current group's stores, and waited for
+// with a counted vmcnt (the stores issued after it may stay in flight) and a raw s_barrier.
+template <int NT, int BPG>
+__global__ __launch_bounds__(256) void k_burst_pipe(const uint4* __restrict__ in, uint4* __restrict__ out,
+                                                    uint64_t n_blocks) {
+    constexpr int Q = BPG * 56;      // uint4 per group (BPG blocks x 896 B)
+    constexpr int J = (Q + 255) / 256;  // DMA rounds per group (a wave-uniform guard on the last)
+    static_assert(Q % 64 == 0, "group must be a whole number of 1 KiB wave DMAs");
+    constexpr int ST = BPG * 256 / 64 / 4;  // 1 KiB stores per wave per group
+    __shared__ __attribute__((aligned(16))) uint4 s_in[2][Q];
+    const uint64_t n_groups = n_blocks / BPG;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint64_t g = blockIdx.x;
+    auto dma = [&](uint64_t grp, int b) {
+        // inline-asm LDS-DMA (cdna_hip_programming.md: hipcc does not count asm memory ops, so it
+        // inserts no vmcnt(0) before the next ds_read of the OTHER buffer; the waits below are ours)
+        const uint4* src = in + grp * Q;
+#pragma unroll
+        for (int j = 0; j < J; j++) {
+            const int q = j * 256 + wave * 64;
+            if (q < Q) {
+                const uint32_t lds_dst = __builtin_amdgcn_readfirstlane(uint32_t(reinterpret_cast<uintptr_t>(&s_in[b][q])));
+                const uint4* gsrc = src + q + lane;
+                unsigned keep;
+                asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                             : "=&s"(keep) : "v"(gsrc), "s"(lds_dst) : "memory");
+            }
+        }
+    };
+    if (g < n_groups) dma(g, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (no stores yet: the counted wait below would not wait)
+    int b = 0;
+    for (; g < n_groups; g += gridDim.x) {
+        // this group's DMA was issued before the previous group's ST stores: wait for it only
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ST) : "memory");
+        __builtin_amdgcn_s_barrier();
+        const uint64_t gn = g + gridDim.x;
+        if (gn < n_groups) dma(gn, b ^ 1);
+        const uint4 acc = s_in[b][wave * (Q / 4) + lane];
+        uint4* dst = out + (g * BPG + wave * (BPG / 4)) * 256;
+#pragma unroll
+        for (int k = 0; k < ST; k++) {
+            uint4 v = make_uint4(acc.x + k, acc.y, acc.z, acc.w);
+            store_bytes<16, NT>(reinterpret_cast<uint8_t*>(dst + k * 64 + lane), &v);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // every wave is done reading buffer b before it is refilled
+        b ^= 1;
+    }
+}
+
 // K1 with burst reads + wave-contiguous stores: the workgroup reads its 32 blocks' packed bytes
 // into LDS in one burst; then every wave decodes whole blocks, all 64 lanes on one block: in
 // store k, lane group g (8 lanes) produces the row whose 128 output bytes sit at k*1 KiB + g*128
@@ -426,7 +478,9 @@ int main(int argc, char** argv) {
                              {"tr_plain", 9}, {"tr_nt", 10}, {"burst_plain", 20}, {"burst_nt", 21},
                              {"write_wave_plain", 22}, {"lds_plain", 23}, {"lds_nt", 24},
                              {"lds2_plain", 25}, {"lds2_nt", 26}, {"lds_k1_plain", 27}, {"lds_k1_nt", 28},
-                             {"lds2_nt_bpw16", 29}, {"lds2_nt_bpw64", 30}, {"lds2_nt_bpw8", 31}};
+                             {"lds2_nt_bpw16", 29}, {"lds2_nt_bpw64", 30}, {"lds2_nt_bpw8", 31},
+                             {"bpipe32_nt_x2", 32}, {"bpipe16_nt_x4", 33}, {"bpipe16_nt_x3", 34}, {"bpipe32_plain_x2", 35},
+                             {"bpipe16_plain_x4", 36}};
     std::vector<Var> vars;
     for (auto& v : vars_all)
         if (std::getenv("UB_ALL") || v.id == 1 || v.id == 7 || v.id == 20 || v.id == 21 || v.id == 22 || v.id >= 25)
@@ -463,13 +517,18 @@ int main(int argc, char** argv) {
         case 29: hipLaunchKernelGGL((k_lds2<1, 16>), dim3(unsigned(n_blocks / 16)), dim3(256), 0, 0, src, out, n_blocks); break;
         case 30: hipLaunchKernelGGL((k_lds2<1, 64>), dim3(unsigned(n_blocks / 64)), dim3(256), 0, 0, src, out, n_blocks); break;
         case 31: hipLaunchKernelGGL((k_lds2<1, 8>), dim3(unsigned(n_blocks / 8)), dim3(256), 0, 0, src, out, n_blocks); break;
+        case 32: hipLaunchKernelGGL((k_burst_pipe<1, 32>), dim3(cus * 2), dim3(256), 0, 0, (const uint4*)src, (uint4*)out, n_blocks); break;
+        case 33: hipLaunchKernelGGL((k_burst_pipe<1, 16>), dim3(cus * 4), dim3(256), 0, 0, (const uint4*)src, (uint4*)out, n_blocks); break;
+        case 34: hipLaunchKernelGGL((k_burst_pipe<1, 16>), dim3(cus * 3), dim3(256), 0, 0, (const uint4*)src, (uint4*)out, n_blocks); break;
+        case 35: hipLaunchKernelGGL((k_burst_pipe<0, 32>), dim3(cus * 2), dim3(256), 0, 0, (const uint4*)src, (uint4*)out, n_blocks); break;
+        case 36: hipLaunchKernelGGL((k_burst_pipe<0, 16>), dim3(cus * 4), dim3(256), 0, 0, (const uint4*)src, (uint4*)out, n_blocks); break;
         case 8: hipLaunchKernelGGL(k_write, dim3(cus * 8), dim3(256), 0, 0, (uint4*)out, out_bytes / 16); break;
         }
     };
     std::vector<uint32_t> h_ref(n_vals), h_out(n_vals);
     CK(hipMemcpy(h_ref.data(), ref, out_bytes, hipMemcpyDeviceToHost));
     for (auto& v : vars) {
-        if (v.id == 7 || v.id == 8 || v.id == 12 || (v.id >= 17 && v.id != 9 && v.id != 10 && v.id < 23)) continue;
+        if (v.id == 7 || v.id == 8 || v.id == 12 || (v.id >= 17 && v.id != 9 && v.id != 10 && v.id < 23) || v.id >= 32) continue;
         CK(hipMemset(out, 0, out_bytes));
         launch(v.id, in[0]);
         CK(hipDeviceSynchronize());
