@@ -64,26 +64,17 @@ __global__ __launch_bounds__(kRowsThreads) void dict_rows_kernel(ChunkTable tab,
     }
     __syncthreads();
     V* __restrict__ out = static_cast<V*>(c.out);
-    const E mask = W >= unsigned(T) ? E(~E(0)) : E((E(1) << W) - E(1));
+    const RtRows<T> rows(W);
     bool oob = false;
     for (unsigned b = 0; b < nb; b++) {
         const E* __restrict__ pw = s_packed + b * (LANES * W);
         const int64_t base = int64_t((blk0 + b) * 1024) - int64_t(c.offset);
+        const bool whole = base >= 0 && uint64_t(base) + 1024 <= c.len;  // uniform
 #pragma unroll
         for (unsigned k = 0; k < 4; k++) {
-            const unsigned i = k * kRowsThreads + tid;  // value index inside the block
-            const int64_t o = base + int64_t(i);
-            if (o < 0 || uint64_t(o) >= c.len) continue;
-            // unpack_single: lane, row of value i (FL_ORDER is an involution)
-            const unsigned lane = i % LANES, s = i / 128, fl = (i - s * 128 - lane) / 16;
-            const unsigned row = unsigned(fl_order(int(fl))) * 8 + s;
-            const unsigned start = row * W, w0 = start / T, sh = start % T;
-            uint64_t code = 0;
-            if (W) {
-                uint64_t v = uint64_t(pw[LANES * w0 + lane]) >> sh;
-                if (sh + W > unsigned(T)) v |= uint64_t(pw[LANES * (w0 + 1) + lane]) << (T - sh);
-                code = uint64_t(E(v) & mask);
-            }
+            const int64_t o = base + int64_t(k * kRowsThreads + tid);
+            if (!whole && (o < 0 || uint64_t(o) >= c.len)) continue;
+            const uint64_t code = W ? uint64_t(rows.get(pw, k)) : 0;
             const bool bad = code >= c.dict_len;
             oob |= bad;
             nt_store(out + o, dict[bad ? 0 : code]);

@@ -189,6 +189,43 @@ __device__ __forceinline__ typename EpiOut<T, EPI, VW>::type apply_epi(typename 
     return r;
 }
 
+// Thread-per-output extraction from LDS-staged blocks with a RUNTIME bit width (K1g, K14): thread
+// t produces values i = 256 k + t (k < 4) of every block.  For LANES <= 256 the lane (i % LANES)
+// and the FL_ORDER group of i do not depend on k, and the row advances by 2 per k, so the bit
+// offset is start0 + 2 k W: one 24-bit multiply per thread instead of one per value.  Both words
+// of a value are read and combined branch-free (v_alignbit for T <= 32).
+template <int T>
+struct RtRows {
+    using E = typename Fl<T>::E;
+    static constexpr uint32_t LANES = 1024 / T;
+    uint32_t lane, start0, W;
+    E mask;
+    __device__ __forceinline__ explicit RtRows(uint32_t w) : W(w) {
+        const uint32_t t = threadIdx.x;  // value t of the block (k = 0)
+        lane = t % LANES;
+        const uint32_t fl = ((t & 127) - lane) >> 4;
+        const uint32_t row = (((fl & 1) << 2) | (fl & 2) | (fl >> 2)) * 8 + (t >> 7);  // FL_ORDER[fl]*8 + s
+        start0 = __umul24(row, w);
+        mask = w >= uint32_t(T) ? E(~E(0)) : E((E(1) << w) - E(1));
+    }
+    // value 256 k + threadIdx.x of the block whose words start at pw (LDS)
+    __device__ __forceinline__ E get(const E* __restrict__ pw, uint32_t k) const {
+        if constexpr (T == 64) {
+            const uint32_t start = start0 + 2 * k * W, w0 = start >> 6, sh = start & 63;
+            const uint32_t w1 = w0 + 1 < W ? w0 + 1 : w0;
+            const uint64_t lo = pw[LANES * w0 + lane], hi = pw[LANES * w1 + lane];
+            return (sh ? (lo >> sh) | (hi << (64 - sh)) : lo) & mask;
+        } else {
+            constexpr uint32_t LT = T == 32 ? 5 : (T == 16 ? 4 : 3);
+            const uint32_t start = start0 + 2 * k * W, w0 = start >> LT, sh = start & (T - 1);
+            const uint32_t w1 = w0 + 1 < W ? w0 + 1 : w0;
+            const uint32_t lo = pw[LANES * w0 + lane], hi = pw[LANES * w1 + lane];
+            if constexpr (T == 32) return E(__builtin_amdgcn_alignbit(hi, lo, sh) & mask);
+            else return E(((lo | (hi << T)) >> sh) & mask);
+        }
+    }
+};
+
 // Output store policy of the K1 launches (1 = non-temporal streaming stores).
 constexpr int kOutNT = 1;
 

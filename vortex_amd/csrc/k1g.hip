@@ -102,25 +102,26 @@ __device__ __forceinline__ void gen_body(const GenChunk& gc, uint64_t g, uint8_t
     }
     __syncthreads();
     O* __restrict__ out = static_cast<O*>(c.out);
-    const E mask = W >= uint32_t(T) ? E(~E(0)) : E((E(1) << W) - E(1));
+    const RtRows<T> rows(W);
     bool oob = false;
     for (uint32_t b = 0; b < nb; b++) {
         const E* __restrict__ pw = s_packed + b * (LANES * W);
         const int64_t base = int64_t((blk0 + b) * 1024) - int64_t(c.offset);
+        if (base >= 0 && uint64_t(base) + 1024 <= c.len) {  // whole block inside the array (uniform)
+            O* __restrict__ ob = out + base + threadIdx.x;
 #pragma unroll
-        for (uint32_t k = 0; k < 4; k++) {
-            const uint32_t i = k * kGenThreads + tid;  // value index inside the block
-            const int64_t o = base + int64_t(i);
-            if (o < 0 || uint64_t(o) >= c.len) continue;
-            const uint32_t lane = i % LANES, s = i >> 7, fl = (i - s * 128 - lane) >> 4;
-            const uint32_t start = (fl_order_rt(fl) * 8 + s) * W, w0 = start / T, sh = start % T;
-            E v = 0;
-            if (W) {
-                uint64_t x = uint64_t(pw[LANES * w0 + lane]) >> sh;
-                if (sh + W > uint32_t(T)) x |= uint64_t(pw[LANES * (w0 + 1) + lane]) << (T - sh);
-                v = E(x) & mask;
+            for (uint32_t k = 0; k < 4; k++) {
+                const E v = W ? rows.get(pw, k) : E(0);
+                gen_store(ob + k * kGenThreads, apply_epi<T, EPI, VW>(v, ep, oob));
             }
-            gen_store(out + o, apply_epi<T, EPI, VW>(v, ep, oob));
+        } else {
+#pragma unroll
+            for (uint32_t k = 0; k < 4; k++) {
+                const int64_t o = base + int64_t(k * kGenThreads + tid);
+                if (o < 0 || uint64_t(o) >= c.len) continue;
+                const E v = W ? rows.get(pw, k) : E(0);
+                gen_store(out + o, apply_epi<T, EPI, VW>(v, ep, oob));
+            }
         }
     }
     if constexpr (EPI == Epi::Dict)
@@ -160,18 +161,33 @@ __device__ __forceinline__ void gen_dispatch_one(const GenChunk& gc, uint64_t g,
     }
 }
 
-template <int... Ks>
+// The job's body: a switch (one jump-table dispatch; a fold over 43 compares cost the late kinds
+// -- VarBin dictionaries, RunEnd -- ~80 scalar instructions per wave).
 __device__ __forceinline__ void gen_dispatch(int kind, const GenChunk& gc, uint64_t g, uint8_t* lds, uint32_t doff, bool dl,
-                                             uint32_t* err, std::integer_sequence<int, Ks...>) {
-    ((kind == Ks ? gen_dispatch_one<Ks>(gc, g, lds, doff, dl, err) : void()), ...);
+                                             uint32_t* err) {
+#define VXG_K1G_CASE(K) \
+    case K: gen_dispatch_one<K>(gc, g, lds, doff, dl, err); break;
+    switch (kind) {
+        VXG_K1G_CASE(0) VXG_K1G_CASE(1) VXG_K1G_CASE(2) VXG_K1G_CASE(3) VXG_K1G_CASE(4) VXG_K1G_CASE(5)
+        VXG_K1G_CASE(6) VXG_K1G_CASE(7) VXG_K1G_CASE(8) VXG_K1G_CASE(9) VXG_K1G_CASE(10) VXG_K1G_CASE(11)
+        VXG_K1G_CASE(12) VXG_K1G_CASE(13) VXG_K1G_CASE(14) VXG_K1G_CASE(15) VXG_K1G_CASE(16) VXG_K1G_CASE(17)
+        VXG_K1G_CASE(18) VXG_K1G_CASE(19) VXG_K1G_CASE(20) VXG_K1G_CASE(21) VXG_K1G_CASE(22) VXG_K1G_CASE(23)
+        VXG_K1G_CASE(24) VXG_K1G_CASE(25) VXG_K1G_CASE(26) VXG_K1G_CASE(27) VXG_K1G_CASE(28) VXG_K1G_CASE(29)
+        VXG_K1G_CASE(30) VXG_K1G_CASE(31) VXG_K1G_CASE(32) VXG_K1G_CASE(33) VXG_K1G_CASE(34) VXG_K1G_CASE(35)
+        VXG_K1G_CASE(36) VXG_K1G_CASE(37) VXG_K1G_CASE(38) VXG_K1G_CASE(39) VXG_K1G_CASE(40) VXG_K1G_CASE(41)
+        VXG_K1G_CASE(42)
+    default: break;
+    }
+#undef VXG_K1G_CASE
 }
+static_assert(kGenKinds == 43, "gen_dispatch's switch lists every kind");
 
 __global__ __launch_bounds__(kGenThreads) void k1_generic_kernel(const GenChunk* __restrict__ tab, uint32_t n,
                                                                  uint32_t dict_off, bool dict_lds, uint32_t* err) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const uint64_t g = blockIdx.x;
     const GenChunk& gc = tab[ext_chunk_index(tab, n, g, [](const GenChunk& d) { return d.d.first_group; })];
-    gen_dispatch(int(gc.kind), gc, g, lds, dict_off, dict_lds, err, std::make_integer_sequence<int, kGenKinds>{});
+    gen_dispatch(int(gc.kind), gc, g, lds, dict_off, dict_lds, err);
 }
 
 }  // namespace
