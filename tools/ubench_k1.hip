@@ -239,13 +239,21 @@ __global__ __launch_bounds__(256) void k_copy(const uint4* __restrict__ in, uint
 // burst copy reference: a workgroup reads its 32 blocks' packed bytes (28 KiB) into LDS in one
 // burst, then writes its 128 KiB of output, each wave 32 KiB with 1 KiB contiguous instructions
 // (plain or NT stores) -- do phase-separated reads and writes beat interleaved ones?
-template <int NT>
+template <int NT, int NTL = 0>
 __global__ __launch_bounds__(256) void k_burst(const uint4* __restrict__ in, uint4* __restrict__ out, uint64_t n_blocks) {
     __shared__ uint4 s_in[32 * 56];  // 32 blocks x 896 B
     const uint64_t b0 = uint64_t(blockIdx.x) * 32;
     if (b0 >= n_blocks) return;
     const uint4* src = in + b0 * 56;
-    for (int q = threadIdx.x; q < 32 * 56; q += 256) s_in[q] = src[q];
+    for (int q = threadIdx.x; q < 32 * 56; q += 256) {
+        if constexpr (NTL) {  // non-temporal loads (read once)
+            using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
+            const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src) + q);
+            s_in[q] = make_uint4(v[0], v[1], v[2], v[3]);
+        } else {
+            s_in[q] = src[q];
+        }
+    }
     __syncthreads();
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     uint4 acc = s_in[wave * 448 + lane];
@@ -480,7 +488,7 @@ int main(int argc, char** argv) {
                              {"lds2_plain", 25}, {"lds2_nt", 26}, {"lds_k1_plain", 27}, {"lds_k1_nt", 28},
                              {"lds2_nt_bpw16", 29}, {"lds2_nt_bpw64", 30}, {"lds2_nt_bpw8", 31},
                              {"bpipe32_nt_x2", 32}, {"bpipe16_nt_x4", 33}, {"bpipe16_nt_x3", 34}, {"bpipe32_plain_x2", 35},
-                             {"bpipe16_plain_x4", 36}};
+                             {"bpipe16_plain_x4", 36}, {"burst_nt_ntload", 37}};
     std::vector<Var> vars;
     for (auto& v : vars_all)
         if (std::getenv("UB_ALL") || v.id == 1 || v.id == 7 || v.id == 20 || v.id == 21 || v.id == 22 || v.id >= 25)
@@ -522,6 +530,7 @@ int main(int argc, char** argv) {
         case 34: hipLaunchKernelGGL((k_burst_pipe<1, 16>), dim3(cus * 3), dim3(256), 0, 0, (const uint4*)src, (uint4*)out, n_blocks); break;
         case 35: hipLaunchKernelGGL((k_burst_pipe<0, 32>), dim3(cus * 2), dim3(256), 0, 0, (const uint4*)src, (uint4*)out, n_blocks); break;
         case 36: hipLaunchKernelGGL((k_burst_pipe<0, 16>), dim3(cus * 4), dim3(256), 0, 0, (const uint4*)src, (uint4*)out, n_blocks); break;
+        case 37: hipLaunchKernelGGL((k_burst<1, 1>), dim3(unsigned(n_blocks / 32)), dim3(256), 0, 0, (const uint4*)src, (uint4*)out, n_blocks); break;
         case 8: hipLaunchKernelGGL(k_write, dim3(cus * 8), dim3(256), 0, 0, (uint4*)out, out_bytes / 16); break;
         }
     };

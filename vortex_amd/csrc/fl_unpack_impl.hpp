@@ -550,8 +550,14 @@ __device__ __forceinline__ void unpack_chunk_w(const ChunkDev& c, uint64_t g, ui
     const uint64_t blk0 = (g - c.first_group) * BPW;
     const int nb = c.n_blocks - blk0 < uint64_t(BPW) ? int(c.n_blocks - blk0) : BPW;
     if constexpr (W > 0) {  // burst: the workgroup's packed words, coalesced 16-byte loads
-        const uint4* src = reinterpret_cast<const uint4*>(c.packed + blk0 * (128 * W));
-        for (int q = threadIdx.x; q < nb * 8 * W; q += 256) reinterpret_cast<uint4*>(s_pk)[q] = src[q];
+        // non-temporal: every packed byte is read once (a copy with this shape: 55.1 -> 53.0 us,
+        // profiles/r03_ubench_k1.txt)
+        using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
+        const u32x4* src = reinterpret_cast<const u32x4*>(c.packed + blk0 * (128 * W));
+        for (int q = threadIdx.x; q < nb * 8 * W; q += 256) {
+            const u32x4 v = __builtin_nontemporal_load(src + q);
+            reinterpret_cast<uint4*>(s_pk)[q] = make_uint4(v[0], v[1], v[2], v[3]);
+        }
     }
     __syncthreads();
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, gq = lane >> 3, t = lane & 7;
