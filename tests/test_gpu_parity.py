@@ -231,6 +231,69 @@ def test_alp_reference_kats_on_gpu(ctx):
     assert assert_primitive_parity(arr, ctx).tobytes() == vals32.tobytes()
 
 
+def _alp_patched(rng, n, pos, f32=False, offset=0, indices_offset=0, packed_indices=True):
+    """ALP -> FoR -> BitPacked (sliced by `offset`) with outer patches at the ascending positions
+    `pos` (values the ALP exponents cannot produce); returns (array, expected values)."""
+    ft = np.float32 if f32 else np.float64
+    vals = (np.round(rng.uniform(1, 1000 if f32 else 100000, n) * 100) / 100).astype(ft)
+    e, f, enc, idx, _ = E.alp_encode(vals)
+    u, ref, sh = E.for_compress(enc)
+    bp = E.encode_bitpacked(u, bit_width=max(1, int(u.max()).bit_length()), allow_patches=False, offset=offset)
+    child = A.frame_of_reference(bp, ref, sh, "i32" if f32 else "i64")
+    allp = np.union1d(pos, idx).astype(np.int64)  # the encoder's own exceptions are patches too
+    pv = vals[allp].copy()
+    mine = np.isin(allp, pos)
+    pv[mine] = (rng.standard_normal(int(mine.sum())) * 1e9 + 0.123456789).astype(ft)
+    pos = allp
+    ind = pos.astype(np.uint64) + np.uint64(indices_offset)
+    ia = (E.encode_bitpacked(ind, bit_width=max(1, int(ind.max()).bit_length()), allow_patches=False)
+          if packed_indices else A.primitive(ind))
+    arr = A.alp(child, e, f, A.sparse(ia, A.primitive(pv, validity="ALL_VALID"), n, indices_offset=indices_offset))
+    expect = vals.copy()
+    expect[pos] = pv
+    return arr, expect
+
+
+# ALP's outer patches are written by the K1w launch itself (fl_unpack_impl.hpp unpack_chunk_w):
+# a 256-patch window guessed from an even spread, or a 256-ary search when the window does not
+# bracket the workgroup's output range.  Both against the separate scatter (VXG_FUSED_PATCHES=0).
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_k1w_fused_patches(ctx, fused, monkeypatch):
+    monkeypatch.setenv("VXG_K1_WAVE", "force")
+    monkeypatch.setenv("VXG_FUSED_PATCHES", fused)
+    rng = np.random.default_rng(77)
+    n = 300_000
+    cases = [
+        dict(pos=np.sort(rng.choice(n, n // 1000, replace=False))),                      # spread: windows
+        dict(pos=np.concatenate([[0], np.arange(100_000, 105_000), [n - 1]])),          # clustered: search
+        dict(pos=np.sort(rng.choice(n, 20_000, replace=False))),                         # dense: both
+        dict(pos=np.array([n - 1])),                                                     # one, at the end
+        dict(pos=np.sort(rng.choice(n, 300, replace=False)), offset=517, indices_offset=1000,
+             packed_indices=False),                                                      # sliced
+        dict(pos=np.sort(rng.choice(n, 3000, replace=False)), f32=True),
+        dict(pos=np.concatenate([np.arange(0, 40_000, 7), np.arange(250_000, n)]), f32=True, offset=3),
+    ]
+    for kw in cases:
+        pos = kw.pop("pos")
+        arr, expect = _alp_patched(rng, n, pos, **kw)
+        assert_primitive_parity(arr, ctx, expect)
+
+
+def test_k1w_fused_patches_errors(ctx, monkeypatch):
+    """Out-of-range and descending patch indices are reported, as by the separate scatter."""
+    monkeypatch.setenv("VXG_K1_WAVE", "force")
+    rng = np.random.default_rng(78)
+    n = 50_000
+    arr, _ = _alp_patched(rng, n, np.array([5, 70, n - 1]))
+    arr.children[1].children[0] = A.primitive(np.array([5, 70, n], np.uint64))
+    with pytest.raises(V.VortexGpuError, match="out of bounds"):
+        gpu(arr, ctx)
+    arr, _ = _alp_patched(rng, n, np.array([5, 70, 900]))
+    arr.children[1].children[0] = A.primitive(np.array([5, 900, 70], np.uint64))
+    with pytest.raises(V.VortexGpuError, match="not sorted"):
+        gpu(arr, ctx)
+
+
 def test_alp_f32_cascade(ctx):
     rng = np.random.default_rng(4)
     vals = (np.round(rng.uniform(-500, 500, 50_000) * 10) / 10).astype(np.float32)

@@ -75,6 +75,22 @@ static bool dict_rows_enabled() {
     return on;
 }
 
+// VXG_FUSED_PATCHES=0 (read at every decode): ALP's outer patches take the separate scatter
+// launch instead of the K1w launch (A/B measurements, parity tests of both paths).
+static bool fused_patches_enabled() {
+    const char* e = std::getenv("VXG_FUSED_PATCHES");
+    return !(e && e[0] == '0');
+}
+
+// launch_one's choice (fl_unpack_impl.hpp) for a kernel-argument table: K1w unless the launch is
+// small enough for the row split (T = 32/64) or VXG_K1_WAVE says otherwise.
+bool k1_takes_wave(int T, int W, Epi epi, uint64_t groups32) {
+    const char* e = std::getenv("VXG_K1_WAVE");
+    const int mode = !e ? 1 : (e[0] == '0' ? 0 : (e[0] == 'f' ? 2 : 1));
+    const bool split = (T == 32 || T == 64) && W > 0 && groups32 < kSplitBelowGroups;
+    return groups32 > 0 && (mode == 2 || (mode == 1 && !split && epi != Epi::Dict));
+}
+
 // K1 dispatch over the instantiation units.
 vxg_status launch_fl_unpack(int T, int W, Epi epi, int vw, const ChunkTable& t, uint64_t g, hipStream_t s) {
     if (W < 0 || W > T) return set_error(VXG_ERR_INVALID_ARGUMENT, "bit width out of range");
@@ -162,7 +178,8 @@ static int k1_out_width(const K1Job& j) {
 // edges than in data.
 vxg_status launch_k1_jobs(std::vector<K1Job>& jobs, uint32_t* err, hipStream_t s, DevTables* dt = nullptr,
                           bool generic_small = false,
-                          const std::vector<std::pair<int, RunEndChunk>>* gen_runs = nullptr) {
+                          const std::vector<std::pair<int, RunEndChunk>>* gen_runs = nullptr,
+                          const PatchCol* patch = nullptr) {
     std::stable_sort(jobs.begin(), jobs.end(), [](const K1Job& a, const K1Job& b) {
         return std::make_tuple(a.T, a.W, int(a.epi), a.vw, a.vb) < std::make_tuple(b.T, b.W, int(b.epi), b.vw, b.vb);
     });
@@ -186,6 +203,7 @@ vxg_status launch_k1_jobs(std::vector<K1Job>& jobs, uint32_t* err, hipStream_t s
         }
         ChunkTable tab{};
         tab.err = err;
+        if (patch && jobs.size() == 1) tab.patch = *patch;  // a single array's K1w (k1_takes_wave)
         ChunkDev* cs = tab.c;
         if (live > size_t(kArgChunks)) {  // only when dt is set
             if (live > 0xFFFFFFFFull) return set_error(VXG_ERR_INVALID_ARGUMENT, "too many chunks");
@@ -464,6 +482,7 @@ class Planner {
     };
     std::vector<K1Job>* k1_batch_ = nullptr;
     std::vector<PatchJob>* patch_batch_ = nullptr;
+    const PatchCol* fused_patch_ = nullptr;  // decode_alp -> decode_bitpacked: patches K1w writes
     std::vector<FsstChunk>* fsst_batch_ = nullptr;  // FSST chunks of a chunked string array
     bool k1_fusable(const vxg_array& c) const;
 
@@ -500,6 +519,8 @@ class Planner {
     vxg_status runend_column(const vxg_array& a, bool in_place, IntCol& c);
 
     vxg_status decode_bitpacked(const vxg_array& bp, Epi epi, int vw, UnpackArgs a, void* dst);
+    bool patch_fusable(const vxg_array& sparse, int value_width) const;
+    vxg_status sparse_patch_col(const vxg_array& sparse, PatchCol& pc);
     vxg_status apply_sparse_patches(const vxg_array& sparse, int T, Epi epi, int vw, const UnpackArgs& a,
                                     void* dst, uint64_t out_len);
     vxg_status decode_alp(const vxg_array& a, void* dst);
@@ -601,11 +622,27 @@ vxg_status Planner::apply_sparse_patches(const vxg_array& sp, int T, Epi epi, in
     const vxg_array* val = child(sp, 1);
     if (!idx || !val) return set_error(VXG_ERR_INVALID_ARGUMENT, "Sparse patches need indices and values");
     if (idx->len != val->len) return set_error(VXG_ERR_INVALID_ARGUMENT, "Sparse indices/values length mismatch");
-    const void* pv;
-    IntCol ic;  // a packed index column is unpacked by the scatter itself (no temporary)
-    VXG_TRY(int_column(*idx, ic));
-    VXG_TRY(view_primitive(*val, &pv));
-    return launch_patch(vw, ic, epi, T, dst, out_len, sp.meta.sparse.indices_offset, pv, idx->len, a, s_);
+    PatchCol pc;  // a packed index column is unpacked by the scatter itself (no temporary)
+    VXG_TRY(int_column(*idx, pc.idx));
+    VXG_TRY(view_primitive(*val, &pc.vals));
+    return launch_patch(vw, pc.idx, epi, T, dst, out_len, sp.meta.sparse.indices_offset, pc.vals, idx->len, a, s_);
+}
+
+bool Planner::patch_fusable(const vxg_array& sp, int value_width) const {
+    const vxg_array* idx = child(sp, 0);
+    const vxg_array* val = child(sp, 1);
+    return sp.encoding == VXG_ENC_SPARSE && idx && val && idx->len == val->len && idx->len > 0 &&
+           width(*val) == value_width && width(*idx) == 8 && ptype_is_int(idx->ptype);
+}
+
+vxg_status Planner::sparse_patch_col(const vxg_array& sp, PatchCol& pc) {
+    // patch_fusable(sp) holds
+    const vxg_array* idx = child(sp, 0);
+    VXG_TRY(int_column(*idx, pc.idx));
+    VXG_TRY(view_primitive(*child(sp, 1), &pc.vals));
+    pc.n = idx->len;
+    pc.idx_off = sp.meta.sparse.indices_offset;
+    return VXG_OK;
 }
 
 vxg_status Planner::decode_bitpacked(const vxg_array& bp, Epi epi, int vw, UnpackArgs a, void* dst) {
@@ -629,7 +666,7 @@ vxg_status Planner::decode_bitpacked(const vxg_array& bp, Epi epi, int vw, Unpac
         return VXG_OK;
     }
     std::vector<K1Job> one{j};
-    VXG_TRY(launch_k1_jobs(one, ctx_->c.err_word, s_, plan_));
+    VXG_TRY(launch_k1_jobs(one, ctx_->c.err_word, s_, plan_, false, nullptr, fused_patch_));
     if (p) VXG_TRY(apply_sparse_patches(*p, T, epi, vw, a, dst, bp.len));
     return VXG_OK;
 }
@@ -656,14 +693,28 @@ vxg_status Planner::decode_alp(const vxg_array& a, void* dst) {
     } else if (enc->encoding == VXG_ENC_FL_BITPACKED) {
         bp = enc;
     }
+    bool fused = false;  // the outer patches written by the K1w launch itself
     if (bp && width(*bp) == (f32 ? 4 : 8)) {
-        VXG_TRY(decode_bitpacked(*bp, epi, 0, ua, dst));  // fused unpack+FoR+ALP (+inner patches)
+        PatchCol pc{};
+        const vxg_array* p = a.meta.alp.has_patches ? child(a, 1) : nullptr;
+        if (p && !k1_batch_ && !patch_batch_ && !bp->meta.bitpacked.has_patches && bp->len == a.len &&
+            patch_fusable(*p, f32 ? 4 : 8) && fused_patches_enabled()) {
+            const uint64_t nblk = (bp->len + bp->meta.bitpacked.offset + 1023) / 1024;
+            if (k1_takes_wave(f32 ? 32 : 64, int(bp->meta.bitpacked.bit_width), epi, (nblk + 31) / 32)) {
+                VXG_TRY(sparse_patch_col(*p, pc));
+                fused = !pc.idx.packed || pc.idx.W > 0;  // K1w reads 8-byte index words directly
+            }
+        }
+        fused_patch_ = fused ? &pc : nullptr;
+        const vxg_status st = decode_bitpacked(*bp, epi, 0, ua, dst);  // fused unpack+FoR+ALP (+patches)
+        fused_patch_ = nullptr;
+        VXG_TRY(st);
     } else {
         const void* penc;
         VXG_TRY(view_primitive(*enc, &penc));
         VXG_TRY(launch_alp(a.ptype, penc, a.len, ua.alp_a, ua.alp_b, dst, s_));
     }
-    if (a.meta.alp.has_patches) {
+    if (a.meta.alp.has_patches && !fused) {
         const vxg_array* p = child(a, 1);
         if (!p) return set_error(VXG_ERR_INVALID_ARGUMENT, "ALPArray: patches child missing");
         UnpackArgs plain{};
@@ -1878,6 +1929,7 @@ vxg_status vxg_stream_sync(vxg_ctx* ctx, void* stream) {
         VXG_TRY(hip_check(hipMemset(ctx->c.err_word, 0, 4), "error word reset"));
         if (err & kErrTakeOOB) return set_error(VXG_ERR_OUT_OF_BOUNDS, "take: index out of bounds");
         if (err & kErrPatchOOB) return set_error(VXG_ERR_OUT_OF_BOUNDS, "patch index out of bounds");
+        if (err & kErrPatchOrder) return set_error(VXG_ERR_INVALID_ARGUMENT, "patch indices are not sorted");
         if (err & kErrRunEnd) return set_error(VXG_ERR_INVALID_ARGUMENT, "RunEnd ends do not cover the array");
         if (err & kErrFsst)
             return set_error(VXG_ERR_INVALID_ARGUMENT, "FSST codes do not decode to uncompressed_lengths");

@@ -32,6 +32,7 @@
 #include <utility>
 
 #include "vxg_internal.hpp"
+#include "intcol.hpp"
 
 namespace vxg {
 
@@ -89,6 +90,7 @@ __device__ __forceinline__ Vec16<T> load16(const uint8_t* p) {
     __builtin_memcpy(v.w, &q, 16);
     return v;
 }
+
 
 // Extract row R of W-bit values from the register-resident word rows (SWAR over lanes).
 template <int T, int W, int R>
@@ -528,8 +530,33 @@ constexpr int kw_packed_lds() {
     return (W > 0 ? kw_bpw(W, LDSD) * 128 * W : 0) + 128;
 }
 
+// First patch (ascending keys idx[i] - idx_off) whose key is >= x: a 256-ary search by the whole
+// workgroup, one memory round trip per round (3 rounds for 2^24 patches).  `s_cnt`: 4 LDS words.
+__device__ __forceinline__ uint64_t patch_lower_bound(const PatchCol& pc, uint64_t x, uint32_t* s_cnt) {
+    uint64_t lo = 0, hi = pc.n;  // the answer is in [lo, hi]
+    while (lo < hi) {            // workgroup-uniform
+        const uint64_t step = (hi - lo + 255) / 256;
+        const uint64_t i = lo + uint64_t(threadIdx.x) * step;
+        const bool below = i < hi && uint64_t(intcol_get(pc.idx, i)) - pc.idx_off < x;
+        const uint32_t cw = uint32_t(__popcll(__ballot(below)));
+        if ((threadIdx.x & 63) == 0) s_cnt[threadIdx.x >> 6] = cw;
+        __syncthreads();
+        const uint64_t cnt = uint64_t(s_cnt[0]) + s_cnt[1] + s_cnt[2] + s_cnt[3];
+        __syncthreads();
+        // samples 0 .. cnt-1 are below x: the answer is in (lo + (cnt-1) step, lo + cnt step]
+        if (cnt == 0) {
+            hi = lo;
+        } else {
+            const uint64_t nhi = lo + cnt * step;
+            lo = lo + (cnt - 1) * step + 1;
+            hi = nhi < hi ? nhi : hi;
+        }
+    }
+    return lo;
+}
+
 template <int T, int W, Epi EPI, int VW, bool LDSD>
-__device__ __forceinline__ void unpack_chunk_w(const ChunkDev& c, uint64_t g, uint32_t* err) {
+__device__ __forceinline__ void unpack_chunk_w(const ChunkDev& c, uint64_t g, uint32_t* err, const PatchCol& pc) {
     using O = typename EpiOut<T, EPI, VW>::type;
     constexpr int BPW = kw_bpw(W, LDSD);
     extern __shared__ __attribute__((aligned(16))) uint8_t k1w_lds[];
@@ -549,6 +576,42 @@ __device__ __forceinline__ void unpack_chunk_w(const ChunkDev& c, uint64_t g, ui
     }
     const uint64_t blk0 = (g - c.first_group) * BPW;
     const int nb = c.n_blocks - blk0 < uint64_t(BPW) ? int(c.n_blocks - blk0) : BPW;
+    // Fused patches: the raw words of a 256-patch window around where the workgroup's output
+    // range [olo, ohi) falls if the patches are spread evenly, loaded before the burst and used
+    // only after the decode (no wait in between: 8-byte index words, plain or FastLanes-packed,
+    // loaded unconditionally).  When the window brackets the range, each thread holds at most one
+    // of the workgroup's patches and stores it after the decode; otherwise the range is found by
+    // patch_lower_bound.  Scratch: the LDS slack row, whose bytes kw_extract always masks off.
+    uint32_t* const s_pscr = reinterpret_cast<uint32_t*>(k1w_lds + kw_packed_lds<W, LDSD>() - 128);
+    const bool patched = pc.n != 0;
+    uint64_t olo = 0, ohi = 0, pbase = 0, pw0 = 0, pw1 = 0;
+    uint32_t psh = 0;
+    O pval{};
+    if (patched) {
+        const uint64_t s0 = blk0 * 1024, s1 = (blk0 + uint64_t(nb)) * 1024;
+        olo = s0 > c.offset ? s0 - c.offset : 0;
+        ohi = s1 - c.offset < c.len ? s1 - c.offset : c.len;
+        const uint64_t guess = uint64_t(double(olo) * double(pc.n) / double(c.len));
+        pbase = guess > 128 ? guess - 128 : 0;
+        if (pbase + 256 > pc.n) pbase = pc.n > 256 ? pc.n - 256 : 0;
+        const uint64_t i0 = pbase + threadIdx.x, i = i0 < pc.n ? i0 : pc.n - 1;
+        const uint64_t* ip = static_cast<const uint64_t*>(pc.idx.p);
+        uint64_t a0 = i, a1 = i;
+        if (pc.idx.packed) {  // fl_word_pair<64>'s two word indices
+            const uint64_t g2 = i + pc.idx.offset;
+            const uint32_t e = uint32_t(g2 & 1023), lane = e % 16, s = e >> 7;
+            const uint32_t fl = ((e & 127) - lane) >> 4;
+            const uint32_t row = (((fl & 1) << 2) | (fl & 2) | (fl >> 2)) * 8 + s;
+            const uint32_t start = __umul24(row, pc.idx.W), word = start / 64;
+            psh = start % 64;
+            const uint64_t blk = (g2 >> 10) * (16ull * pc.idx.W);
+            a0 = blk + 16ull * word + lane;
+            a1 = blk + 16ull * (word + 1 < pc.idx.W ? word + 1 : word) + lane;
+        }
+        pw0 = ip[a0];
+        pw1 = ip[a1];
+        pval = static_cast<const O*>(pc.vals)[i];
+    }
     if constexpr (W > 0) {  // burst: the workgroup's packed words, coalesced 16-byte loads
         // non-temporal: every packed byte is read once (a copy with this shape: 55.1 -> 53.0 us,
         // profiles/r03_ubench_k1.txt)
@@ -575,6 +638,44 @@ __device__ __forceinline__ void unpack_chunk_w(const ChunkDev& c, uint64_t g, ui
     }
     if constexpr (EPI == Epi::Dict)
         if (oob) __hip_atomic_fetch_or(err, kErrTakeOOB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (patched) {
+        // the window's words are used from here on (keeps the compiler from hoisting their use,
+        // and its wait, above the decode)
+        asm volatile("" : "+v"(pw0), "+v"(pw1));
+        uint64_t pkey = pw0;
+        if (pc.idx.packed) {  // fl_get<64>
+            const uint64_t mask = pc.idx.W >= 64 ? ~0ull : ((1ull << pc.idx.W) - 1);
+            const uint64_t v = pc.idx.W ? ((psh ? (pw0 >> psh) | (pw1 << (64 - psh)) : pw0) & mask) : 0;
+            pkey = (v << pc.idx.shift) + pc.idx.reference;
+        }
+        const bool valid = pbase + threadIdx.x < pc.n;
+        pkey = valid ? pkey - pc.idx_off : ~0ull;
+        const bool pin = pkey >= olo && pkey < ohi;
+        // the window brackets [olo, ohi): nothing before it is >= olo, nothing after it < ohi
+        if (threadIdx.x == 0) s_pscr[0] = pbase == 0 || pkey < olo;
+        if (threadIdx.x == 255) s_pscr[1] = pbase + 256 >= pc.n || pkey >= ohi;
+        // keys ascending inside the window (a cheap check of the invariant the search relies on)
+        const uint64_t nk = __shfl_down(pkey, 1, 64);
+        if ((threadIdx.x & 63) != 63 && pbase + threadIdx.x + 1 < pc.n && nk < pkey)
+            __hip_atomic_fetch_or(err, kErrPatchOrder, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (g == c.first_group && threadIdx.x == 0) {  // sorted keys: all in [0, len) iff both ends are
+            const uint64_t k0 = uint64_t(intcol_get(pc.idx, 0)) - pc.idx_off;
+            const uint64_t k1 = uint64_t(intcol_get(pc.idx, pc.n - 1)) - pc.idx_off;
+            if (k0 >= c.len || k1 >= c.len)
+                __hip_atomic_fetch_or(err, kErrPatchOOB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        // every block store of the workgroup is complete before any patch store
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+        if (s_pscr[0] && s_pscr[1]) {
+            if (pin) out[pkey] = pval;
+        } else {
+            const uint64_t ps = patch_lower_bound(pc, olo, s_pscr + 4);
+            const uint64_t pe = patch_lower_bound(pc, ohi, s_pscr + 4);
+            for (uint64_t i = ps + threadIdx.x; i < pe; i += 256)
+                out[uint64_t(intcol_get(pc.idx, i)) - pc.idx_off] = static_cast<const O*>(pc.vals)[i];
+        }
+    }
 }
 
 template <int T, int W, Epi EPI, int VW, bool LDSD, bool EXT>
@@ -583,14 +684,14 @@ __global__ __launch_bounds__(256) void fl_unpack_w_kernel(ChunkTable tab) {
     if constexpr (EXT) {
         const ChunkDev& c =
             tab.ext[ext_chunk_index(tab.ext, tab.n, g, [](const ChunkDev& d) { return d.first_group; })];
-        unpack_chunk_w<T, W, EPI, VW, LDSD>(c, g, tab.err);
+        unpack_chunk_w<T, W, EPI, VW, LDSD>(c, g, tab.err, PatchCol{});
     } else {
         uint32_t lo = 0, hi = tab.n;
         while (hi - lo > 1) {
             const uint32_t mid = (lo + hi) >> 1;
             if (tab.c[mid].first_group <= g) lo = mid; else hi = mid;
         }
-        unpack_chunk_w<T, W, EPI, VW, LDSD>(tab.c[lo], g, tab.err);
+        unpack_chunk_w<T, W, EPI, VW, LDSD>(tab.c[lo], g, tab.err, tab.patch);
     }
 }
 
@@ -614,8 +715,6 @@ __global__ __launch_bounds__(256) void fl_unpack_kernel(ChunkTable tab) {
     }
 }
 
-// A launch with fewer 32-block workgroups than this uses the row split (S = 4).
-constexpr uint64_t kSplitBelowGroups = 512;
 
 template <int T, int W, Epi EPI, int VW, bool LDSD, bool EXT>
 vxg_status launch_w(ChunkTable tab, hipStream_t s) {

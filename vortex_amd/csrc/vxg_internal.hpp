@@ -55,7 +55,8 @@ extern const double kF10d[24];
 extern const double kIF10d[24];
 
 // Device error word bits (set by kernels, read by vxg_check via vxg_stream_sync).
-enum : uint32_t { kErrTakeOOB = 1u, kErrPatchOOB = 2u, kErrRunEnd = 4u, kErrFsst = 8u, kErrRoaring = 16u, kErrVarBin = 32u };
+enum : uint32_t { kErrTakeOOB = 1u, kErrPatchOOB = 2u, kErrRunEnd = 4u, kErrFsst = 8u, kErrRoaring = 16u, kErrVarBin = 32u,
+                  kErrPatchOrder = 64u };
 
 struct Ctx {
     int device = 0;
@@ -157,13 +158,7 @@ struct ChunkDev {
 // plan's launch may use a device table of any length instead (ext: device, host: its mirror,
 // which the host-side launch code reads and completes before the upload).
 constexpr int kArgChunks = 32;
-struct ChunkTable {
-    ChunkDev c[kArgChunks];
-    uint32_t n;
-    uint32_t* err;
-    const ChunkDev* ext;
-    ChunkDev* host;
-};
+struct ChunkTable;  // below IntCol
 
 // T in {8,16,32,64} bits; value_width only used for Epi::Dict.  `groups` = total 32-block
 // workgroups of the table (first_group filled in).
@@ -183,6 +178,32 @@ struct IntCol {
     uint32_t offset;     // packed: BitPacked slice offset (< 1024)
     uint64_t reference;  // packed: FoR reference (0 for a bare BitPacked column)
 };
+// Sparse patches written by the K1w launch of a single array (n = 0: none), after the
+// workgroup's own block stores: each value is written as-is (sizeof(output element) bytes) --
+// ALP's outer f32/f64 exceptions (alp/compress.rs:80-96).  Indices: 8-byte integers, plain or
+// [FoR](BitPacked u64) with W > 0.
+// The indices are ascending (the Patches invariant; sparse/mod.rs:132-144 resolves them in order).
+struct PatchCol {
+    IntCol idx;
+    const void* vals;
+    uint64_t n;
+    uint64_t idx_off;    // SparseArray indices_offset
+};
+
+struct ChunkTable {
+    ChunkDev c[kArgChunks];
+    uint32_t n;
+    uint32_t* err;
+    const ChunkDev* ext;
+    ChunkDev* host;
+    PatchCol patch;      // kernel-argument tables with n == 1 only (launch_fl_unpack, K1w)
+};
+
+// A launch with fewer 32-block workgroups than this uses the row split (S = 4).
+constexpr uint64_t kSplitBelowGroups = 512;
+// Whether launch_fl_unpack takes K1w for a kernel-argument table of `groups32` 32-block workgroups.
+bool k1_takes_wave(int T, int W, Epi epi, uint64_t groups32);
+
 // Patch scatter with the same epilogue applied to the patch value.
 vxg_status launch_patch(int val_width, const IntCol& indices, Epi epi, int T, void* out, uint64_t out_len,
                         uint64_t indices_offset, const void* values, uint64_t n, const UnpackArgs& ep,
