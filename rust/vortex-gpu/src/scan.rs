@@ -225,7 +225,8 @@ pub fn scan_file(
         }
         tables.push(table);
     }
-    // (4) one plan for every column
+    // (4) one plan for every column; launched once, so recorded without VXG_PLAN_MEASURE (create
+    // executes nothing and picks batched/unbatched by the plan's output size)
     let mut raw_plan = ptr::null_mut();
     check(unsafe {
         ffi::vxg_plan_create(session.raw(), nodes.as_ptr(), outs.as_mut_ptr(), nodes.len() as u32, &mut raw_plan)

@@ -22,7 +22,7 @@ PTYPES = ["u8", "u16", "u32", "u64", "i8", "i16", "i32", "i64", "f16", "f32", "f
 PTYPE = {n: i for i, n in enumerate(PTYPES)}
 DTYPE = dict(NULL=0, BOOL=1, PRIMITIVE=2, UTF8=3, BINARY=4)
 VALIDITY = dict(NON_NULLABLE=0, ALL_VALID=1, ALL_INVALID=2, ARRAY=3)
-ABI_VERSION = 5  # VXG_ABI_VERSION
+ABI_VERSION = 6  # VXG_ABI_VERSION
 STATUS = {0: "OK", 1: "OutOfBounds", 2: "ComputeError", 3: "InvalidArgument", 4: "InvalidSerde",
           5: "NotImplemented", 6: "MismatchedTypes", 7: "AssertionFailed", 8: "HipError",
           9: "OutOfMemory"}
@@ -138,6 +138,15 @@ class VxgCanonical(C.Structure):
                 ("data_buffers", C.POINTER(VxgDataBuffer))]
 
 
+PLAN_MEASURE = 1  # VXG_PLAN_MEASURE
+
+
+class VxgPlanInfo(C.Structure):
+    _fields_ = [("batched", C.c_uint32), ("branches", C.c_uint32), ("direct_nodes", C.c_uint32),
+                ("n_candidates", C.c_uint32), ("candidate_batched", C.c_uint32 * 2),
+                ("candidate_ms", C.c_float * 2), ("create_ms", C.c_float), ("reserved", C.c_uint32)]
+
+
 class VxgIntStats(C.Structure):
     _fields_ = [("n", C.c_uint64), ("min_bits", C.c_uint64), ("max_bits", C.c_uint64), ("trailing_zeros", C.c_uint32),
                 ("reserved", C.c_uint32), ("bit_width_freq", C.c_uint64 * 65)]
@@ -171,6 +180,8 @@ GPU_SIGNATURES = {
     "vxg_canonical_size": (ST, [VP, C.POINTER(VxgArray), C.POINTER(U64), C.POINTER(U64)]),
     "vxg_canonicalize": (ST, [VP, C.POINTER(VxgArray), C.POINTER(VxgCanonical), VP]),
     "vxg_plan_create": (ST, [VP, C.POINTER(VxgArray), C.POINTER(VxgCanonical), U32, C.POINTER(VP)]),
+    "vxg_plan_create_ex": (ST, [VP, C.POINTER(VxgArray), C.POINTER(VxgCanonical), U32, U32, C.POINTER(VP)]),
+    "vxg_plan_get_info": (ST, [VP, C.c_void_p]),
     "vxg_plan_launch": (ST, [VP, VP]),
     "vxg_plan_destroy": (ST, [VP]),
     "vxg_canonical_layout": (ST, [VP, C.POINTER(VxgArray), C.POINTER(U64), C.POINTER(U64),

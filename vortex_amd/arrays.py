@@ -720,7 +720,9 @@ class Plan:
     `arrays` are Array trees (device buffers) or already-flattened VxgArray nodes (e.g. the
     trees a vxg_file reader built over a file's bytes in HBM)."""
 
-    def __init__(self, arrays: Sequence, ctx: Context):
+    def __init__(self, arrays: Sequence, ctx: Context, measure: bool = False):
+        """measure=True: VXG_PLAN_MEASURE -- record both candidates and keep the faster (runs the
+        decode several times at create; inputs must be resident and valid)."""
         self.ctx = ctx
         self.keep: list = []
         n = len(arrays)
@@ -733,12 +735,23 @@ class Plan:
             self.outs[i] = o
             self.results.append(res)
         h = C.c_void_p()
-        _lib.check(ctx.lib.vxg_plan_create(ctx.handle, self.nodes, self.outs, n, C.byref(h)))
+        flags = _lib.PLAN_MEASURE if measure else 0
+        _lib.check(ctx.lib.vxg_plan_create_ex(ctx.handle, self.nodes, self.outs, n, flags, C.byref(h)))
         self.handle = h
         # a nullable array whose validity turned out all-valid leaves out.validity NULL
         for i, res in enumerate(self.results):
             if res.validity is not None and not self.outs[i].validity:
                 res.validity = None
+
+    def info(self) -> dict:
+        """vxg_plan_get_info: the kept graph's shape, the candidates' measured replay times and
+        the create call's wall time."""
+        i = _lib.VxgPlanInfo()
+        _lib.check(self.ctx.lib.vxg_plan_get_info(self.handle, C.byref(i)))
+        cands = [{"batched": bool(i.candidate_batched[c]), "ms": round(float(i.candidate_ms[c]), 4)}
+                 for c in range(i.n_candidates)]
+        return {"batched": bool(i.batched), "branches": int(i.branches), "direct_nodes": int(i.direct_nodes),
+                "candidates": cands, "create_ms": round(float(i.create_ms), 3)}
 
     def launch(self, sync: bool = False):
         _lib.check(self.ctx.lib.vxg_plan_launch(self.handle, self.ctx.stream_ptr()))

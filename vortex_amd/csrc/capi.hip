@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -81,6 +82,8 @@ static bool fused_patches_enabled() {
     const char* e = std::getenv("VXG_FUSED_PATCHES");
     return !(e && e[0] == '0');
 }
+
+thread_local bool g_k1w_wrote_patches = false;
 
 // launch_one's choice (fl_unpack_impl.hpp) for a kernel-argument table: K1w unless the launch is
 // small enough for the row split (T = 32/64) or VXG_K1_WAVE says otherwise.
@@ -706,9 +709,11 @@ vxg_status Planner::decode_alp(const vxg_array& a, void* dst) {
             }
         }
         fused_patch_ = fused ? &pc : nullptr;
+        g_k1w_wrote_patches = false;
         const vxg_status st = decode_bitpacked(*bp, epi, 0, ua, dst);  // fused unpack+FoR+ALP (+patches)
         fused_patch_ = nullptr;
         VXG_TRY(st);
+        fused = fused && g_k1w_wrote_patches;  // any other K1 path left them to the scatter below
     } else {
         const void* penc;
         VXG_TRY(view_primitive(*enc, &penc));
@@ -1843,6 +1848,18 @@ vxg_status Planner::canonical(const vxg_array& a, vxg_canonical& out) {
 // ===================================================================================
 // C ABI
 // ===================================================================================
+// The device error word's bits -> the VortexError variant each one stands for.
+static vxg_status status_of_err_word(uint32_t err) {
+    if (err & kErrTakeOOB) return set_error(VXG_ERR_OUT_OF_BOUNDS, "take: index out of bounds");
+    if (err & kErrPatchOOB) return set_error(VXG_ERR_OUT_OF_BOUNDS, "patch index out of bounds");
+    if (err & kErrPatchOrder) return set_error(VXG_ERR_INVALID_ARGUMENT, "patch indices are not sorted");
+    if (err & kErrRunEnd) return set_error(VXG_ERR_INVALID_ARGUMENT, "RunEnd ends do not cover the array");
+    if (err & kErrFsst) return set_error(VXG_ERR_INVALID_ARGUMENT, "FSST codes do not decode to uncompressed_lengths");
+    if (err & kErrRoaring) return set_error(VXG_ERR_INVALID_SERDE, "RoaringBool buffer is not a croaring Native bitmap");
+    if (err & kErrVarBin) return set_error(VXG_ERR_INVALID_ARGUMENT, "VarBin offsets out of range of the bytes");
+    return set_error(VXG_ERR_ASSERTION_FAILED, "unknown device error bit");
+}
+
 extern "C" {
 
 int vxg_abi_version(void) { return VXG_ABI_VERSION; }
@@ -1927,15 +1944,7 @@ vxg_status vxg_stream_sync(vxg_ctx* ctx, void* stream) {
     VXG_TRY(hip_check(hipMemcpy(&err, ctx->c.err_word, 4, hipMemcpyDeviceToHost), "error word readback"));
     if (err) {
         VXG_TRY(hip_check(hipMemset(ctx->c.err_word, 0, 4), "error word reset"));
-        if (err & kErrTakeOOB) return set_error(VXG_ERR_OUT_OF_BOUNDS, "take: index out of bounds");
-        if (err & kErrPatchOOB) return set_error(VXG_ERR_OUT_OF_BOUNDS, "patch index out of bounds");
-        if (err & kErrPatchOrder) return set_error(VXG_ERR_INVALID_ARGUMENT, "patch indices are not sorted");
-        if (err & kErrRunEnd) return set_error(VXG_ERR_INVALID_ARGUMENT, "RunEnd ends do not cover the array");
-        if (err & kErrFsst)
-            return set_error(VXG_ERR_INVALID_ARGUMENT, "FSST codes do not decode to uncompressed_lengths");
-        if (err & kErrRoaring)
-            return set_error(VXG_ERR_INVALID_SERDE, "RoaringBool buffer is not a croaring Native bitmap");
-        if (err & kErrVarBin) return set_error(VXG_ERR_INVALID_ARGUMENT, "VarBin offsets out of range of the bytes");
+        return status_of_err_word(err);
     }
     return VXG_OK;
 }
@@ -2042,6 +2051,10 @@ static uint64_t env_bytes(const char* name, uint64_t dflt) {
     return e ? uint64_t(std::strtoull(e, nullptr, 10)) : dflt;
 }
 static uint64_t plan_batch_max_bytes() { return env_bytes("VXG_PLAN_BATCH_MAX_BYTES", uint64_t(64) << 20); }
+// vxg_plan_create without VXG_PLAN_MEASURE records one candidate: batched when the plan's
+// canonical output is at most this (C5 shards at 4 / 8 GPUs, 275 / 140 MB: batched 0.095 / 0.060
+// vs unbatched 0.131 / 0.120 ms; at 2 GPUs, 550 MB, unbatched 0.180 vs 0.200).
+constexpr uint64_t kPlanBatchDefaultBytes = 400ull << 20;
 
 static uint64_t canonical_out_bytes(const vxg_array& a) {
     const bool str = a.dtype == VXG_DTYPE_UTF8 || a.dtype == VXG_DTYPE_BINARY;
@@ -2058,6 +2071,8 @@ struct vxg_plan {
     // no graph-to-graph dependency (a graph replay boundary cost ~14 us on the C5 shard).
     std::vector<hipKernelNodeParams> direct;
     bool batched = false;  // recorded with a PlanBatch (diagnostics)
+    uint32_t branches = 0;
+    vxg_plan_info info{};  // filled by vxg_plan_create_ex
 };
 
 // Direct replay of short kernel chains (VXG_PLAN_DIRECT=0 disables; at most
@@ -2151,6 +2166,7 @@ static vxg_status record_plan(vxg_ctx* ctx, const vxg_array* arrays, vxg_canonic
     auto* pl = new vxg_plan();
     pl->ctx = ctx;
     pl->batched = batching;
+    pl->branches = na;
     if (st == VXG_OK) st = hip_check(hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed), "hipStreamBeginCapture");
     if (st == VXG_OK) {
         st = hip_check(hipEventRecord(ev[nb], cs), "fork");
@@ -2233,9 +2249,17 @@ static vxg_status time_plans(const std::vector<vxg_plan*>& cands, int reps, std:
 extern "C" {
 
 vxg_status vxg_plan_create(vxg_ctx* ctx, const vxg_array* arrays, vxg_canonical* outs, uint32_t n, vxg_plan** plan) {
+    return vxg_plan_create_ex(ctx, arrays, outs, n, 0, plan);
+}
+
+vxg_status vxg_plan_create_ex(vxg_ctx* ctx, const vxg_array* arrays, vxg_canonical* outs, uint32_t n,
+                              uint32_t flags, vxg_plan** plan) {
+    const auto t0 = std::chrono::steady_clock::now();
     VXG_TRY(use_device(ctx));
     if (!plan || (n && (!arrays || !outs))) return set_error(VXG_ERR_INVALID_ARGUMENT, "null plan/arrays/outs");
+    if (flags & ~uint32_t(VXG_PLAN_MEASURE)) return set_error(VXG_ERR_INVALID_ARGUMENT, "unknown plan flags");
     *plan = nullptr;
+    uint64_t total_out = 0;
     for (uint32_t i = 0; i < n; i++) {  // nothing may allocate or synchronise while recording
         const vxg_array& a = arrays[i];
         const vxg_canonical& o = outs[i];
@@ -2244,6 +2268,7 @@ vxg_status vxg_plan_create(vxg_ctx* ctx, const vxg_array* arrays, vxg_canonical*
             return set_error(VXG_ERR_INVALID_ARGUMENT, "a plan needs caller-allocated outputs");
         if (a.nullable && !o.validity)
             return set_error(VXG_ERR_INVALID_ARGUMENT, "a plan needs caller-allocated validity for nullable arrays");
+        total_out += canonical_out_bytes(a);
     }
     // candidates: (batched mask, branches); 2 branches unbatched (C5 at 1 GPU 322.6 us/replay vs
     // 362 with 1 and 348 with 3), 1 batched (each cross-branch edge costs a replay several
@@ -2253,13 +2278,20 @@ vxg_status vxg_plan_create(vxg_ctx* ctx, const vxg_array* arrays, vxg_canonical*
     std::vector<bool> mixed(n);
     for (uint32_t i = 0; i < n; i++) mixed[i] = canonical_out_bytes(arrays[i]) <= plan_batch_max_bytes();
     std::vector<std::pair<std::vector<bool>, uint32_t>> cand;
+    const bool measure = (flags & VXG_PLAN_MEASURE) != 0;
     switch (plan_batch_mode()) {
     case BatchMode::Off: cand.emplace_back(none, env_br ? env_br : 2u); break;
     case BatchMode::On: cand.emplace_back(all, env_br ? env_br : 1u); break;
     case BatchMode::Mixed: cand.emplace_back(mixed, env_br ? env_br : 2u); break;
     case BatchMode::Auto:
-        cand.emplace_back(none, env_br ? env_br : 2u);
-        if (n) cand.emplace_back(all, env_br ? env_br : 1u);
+        if (measure) {
+            cand.emplace_back(none, env_br ? env_br : 2u);
+            if (n) cand.emplace_back(all, env_br ? env_br : 1u);
+        } else if (n && total_out <= kPlanBatchDefaultBytes) {
+            cand.emplace_back(all, env_br ? env_br : 1u);
+        } else {
+            cand.emplace_back(none, env_br ? env_br : 2u);
+        }
         break;
     }
     std::vector<vxg_plan*> plans;
@@ -2271,21 +2303,49 @@ vxg_status vxg_plan_create(vxg_ctx* ctx, const vxg_array* arrays, vxg_canonical*
         plans.push_back(p);
     }
     size_t best = 0;
-    if (st == VXG_OK && plans.size() > 1) {
-        std::vector<float> ms;
-        st = time_plans(plans, 3, &ms);
+    std::vector<float> ms(plans.size(), 0.f);
+    if (st == VXG_OK && measure && !plans.empty()) {
+        // the candidates read the inputs now: every upload the caller enqueued (any stream) first
+        st = hip_check(hipDeviceSynchronize(), "plan create: device synchronize");
+        if (st == VXG_OK) st = time_plans(plans, 3, &ms);
         for (size_t c = 1; c < ms.size(); c++)
             if (ms[c] < ms[best]) best = c;
+        if (st == VXG_OK) {  // errors the measured runs found belong to create, not the next sync
+            uint32_t err = 0;
+            st = hip_check(hipMemcpy(&err, ctx->c.err_word, 4, hipMemcpyDeviceToHost), "error word readback");
+            if (st == VXG_OK && err) {
+                st = hip_check(hipMemset(ctx->c.err_word, 0, 4), "error word reset");
+                if (st == VXG_OK) st = status_of_err_word(err);
+            }
+        }
         if (std::getenv("VXG_PLAN_DEBUG"))
             for (size_t c = 0; c < ms.size(); c++)
                 std::fprintf(stderr, "plan candidate %zu (%s, %u branches, %zu kernel-chain nodes): %.4f ms%s\n", c,
                              plans[c]->batched ? "batched" : "unbatched", cand[c].second, plans[c]->direct.size(),
                              ms[c], c == best ? "  <- kept" : "");
     }
+    if (st == VXG_OK && !plans.empty()) {
+        vxg_plan_info& in = plans[best]->info;
+        in.batched = plans[best]->batched;
+        in.branches = plans[best]->branches;
+        in.direct_nodes = uint32_t(plans[best]->direct.size());
+        in.n_candidates = uint32_t(std::min<size_t>(plans.size(), 2));
+        for (size_t c = 0; c < plans.size() && c < 2; c++) {
+            in.candidate_batched[c] = plans[c]->batched;
+            in.candidate_ms[c] = ms[c];
+        }
+        in.create_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
     for (size_t c = 0; c < plans.size(); c++)
         if (st != VXG_OK || c != best) vxg_plan_destroy(plans[c]);
     if (st == VXG_OK && !plans.empty()) *plan = plans[best];
     return st;
+}
+
+vxg_status vxg_plan_get_info(const vxg_plan* plan, vxg_plan_info* info) {
+    if (!plan || !info) return set_error(VXG_ERR_INVALID_ARGUMENT, "null plan/info");
+    *info = plan->info;
+    return VXG_OK;
 }
 
 vxg_status vxg_plan_launch(vxg_plan* plan, void* stream) {

@@ -672,8 +672,15 @@ __device__ __forceinline__ void unpack_chunk_w(const ChunkDev& c, uint64_t g, ui
         } else {
             const uint64_t ps = patch_lower_bound(pc, olo, s_pscr + 4);
             const uint64_t pe = patch_lower_bound(pc, ohi, s_pscr + 4);
-            for (uint64_t i = ps + threadIdx.x; i < pe; i += 256)
-                out[uint64_t(intcol_get(pc.idx, i)) - pc.idx_off] = static_cast<const O*>(pc.vals)[i];
+            // sorted keys in [ps, pe) all lie in [olo, ohi); one outside is unsorted input (a
+            // malformed file) and is reported, never stored
+            bool bad = false;
+            for (uint64_t i = ps + threadIdx.x; i < pe; i += 256) {
+                const uint64_t key = uint64_t(intcol_get(pc.idx, i)) - pc.idx_off;
+                if (key >= olo && key < ohi) out[key] = static_cast<const O*>(pc.vals)[i];
+                else bad = true;
+            }
+            if (bad) __hip_atomic_fetch_or(err, kErrPatchOrder, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }
@@ -731,6 +738,9 @@ vxg_status launch_w(ChunkTable tab, hipStream_t s) {
     if (groups > 0xFFFFFFFFull) return set_error(VXG_ERR_INVALID_ARGUMENT, "array too long for one launch");
     const size_t shm = size_t(kw_packed_lds<W, LDSD>()) + (LDSD ? size_t(dict_bytes) : 0);
     hipLaunchKernelGGL((fl_unpack_w_kernel<T, W, EPI, VW, LDSD, EXT>), dim3(unsigned(groups)), dim3(256), shm, s, tab);
+    if constexpr (!EXT) {
+        if (tab.patch.n) g_k1w_wrote_patches = true;  // only this kernel reads tab.patch
+    }
     return hip_check(hipGetLastError(), "fl_unpack_w_kernel launch");
 }
 

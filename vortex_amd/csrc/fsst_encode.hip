@@ -149,15 +149,17 @@ __device__ __forceinline__ bool is_valid(const StrSrc& src, uint64_t i) {
     return !src.validity || ((src.validity[i >> 3] >> (i & 7)) & 1);
 }
 
-// pass A: per-string code lengths (u32) and one total per 1024-string tile
+// pass A: per-string code lengths (u32) and one total per 1024-string tile (u64: a tile of
+// all-escape strings can hold more than 4 GiB of codes, which must be rejected, not wrapped)
 __global__ __launch_bounds__(kFB) void fsst_enc_len(StrSrc src, const EncTab* __restrict__ gtab,
-                                                    uint32_t* __restrict__ clen, uint32_t* __restrict__ tile_tot) {
+                                                    uint32_t* __restrict__ clen,
+                                                    unsigned long long* __restrict__ tile_tot) {
     __shared__ EncTab t;
-    __shared__ uint32_t s_w[kFB / 64];
+    __shared__ unsigned long long s_w[kFB / 64];
     stage_tab(t, gtab);
     const uint64_t first = uint64_t(blockIdx.x) * kFTile + uint64_t(threadIdx.x) * kFPer;
     const uint8_t* end = src.bytes + src.bytes_len;
-    uint32_t sum = 0;
+    unsigned long long sum = 0;
     for (int k = 0; k < kFPer; k++) {
         const uint64_t i = first + k;
         if (i >= src.n) break;
@@ -179,7 +181,7 @@ __global__ __launch_bounds__(kFB) void fsst_enc_len(StrSrc src, const EncTab* __
 }
 
 // exclusive scan of the tile totals into tile_off (u64), total at tile_off[m]; one workgroup
-__global__ __launch_bounds__(kFB) void fsst_enc_scan(const uint32_t* __restrict__ tot, uint64_t m,
+__global__ __launch_bounds__(kFB) void fsst_enc_scan(const unsigned long long* __restrict__ tot, uint64_t m,
                                                      unsigned long long* __restrict__ tile_off) {
     __shared__ unsigned long long s_ws[kFB / 64];
     __shared__ unsigned long long s_carry;
@@ -216,20 +218,20 @@ __global__ __launch_bounds__(kFB) void fsst_enc_write(StrSrc src, const EncTab* 
                                                       uint8_t* __restrict__ codes, int32_t* __restrict__ code_offs,
                                                       int32_t* __restrict__ ulens) {
     __shared__ EncTab t;
-    __shared__ uint32_t s_w[kFB / 64];
+    __shared__ unsigned long long s_w[kFB / 64];
     stage_tab(t, gtab);
     const uint64_t first = uint64_t(blockIdx.x) * kFTile + uint64_t(threadIdx.x) * kFPer;
     uint32_t c[kFPer];
-    uint32_t mine = 0;
+    unsigned long long mine = 0;
     for (int k = 0; k < kFPer; k++) {
         c[k] = first + k < src.n ? clen[first + k] : 0u;
         mine += c[k];
     }
     // workgroup exclusive prefix of the per-thread sums
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    uint32_t x = mine;
+    unsigned long long x = mine;
     for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d, 64);
+        const unsigned long long y = __shfl_up(x, d, 64);
         if (lane >= d) x += y;
     }
     if (lane == 63) s_w[wave] = x;
@@ -307,7 +309,7 @@ vxg_status launch_fsst_compress(const uint64_t* symbols, const uint8_t* sym_lens
     // scratch: table | per-string lengths | tile totals | tile offsets
     const uint64_t o_len = (sizeof(EncTab) + 255) & ~255ull;
     const uint64_t o_tot = o_len + ((n * 4 + 255) & ~255ull);
-    const uint64_t o_off = o_tot + ((tiles * 4 + 255) & ~255ull);
+    const uint64_t o_off = o_tot + ((tiles * 8 + 255) & ~255ull);
     const uint64_t o_bad = o_off + (tiles + 1) * 8;
     const uint64_t scratch_bytes = o_bad + 8;
     void* scratch = nullptr;
@@ -325,7 +327,7 @@ vxg_status launch_fsst_compress(const uint64_t* symbols, const uint8_t* sym_lens
     StrSrc src{offsets, offs_width, offs_signed, bytes, bytes_len, validity, n, bad};
     const EncTab* dt = reinterpret_cast<const EncTab*>(sc);
     uint32_t* clen = reinterpret_cast<uint32_t*>(sc + o_len);
-    uint32_t* tot = reinterpret_cast<uint32_t*>(sc + o_tot);
+    auto* tot = reinterpret_cast<unsigned long long*>(sc + o_tot);
     auto* toff = reinterpret_cast<unsigned long long*>(sc + o_off);
     if (tiles) hipLaunchKernelGGL(fsst_enc_len, dim3(unsigned(tiles)), dim3(kFB), 0, s, src, dt, clen, tot);
     hipLaunchKernelGGL(fsst_enc_scan, dim3(1), dim3(kFB), 0, s, tot, tiles, toff);

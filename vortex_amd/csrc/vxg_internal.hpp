@@ -199,6 +199,11 @@ struct ChunkTable {
     PatchCol patch;      // kernel-argument tables with n == 1 only (launch_fl_unpack, K1w)
 };
 
+// Set (host side) by a kernel-argument K1w launch that was handed tab.patch, the only K1 path
+// that writes patches; a caller that offered patches clears it first and runs the separate
+// scatter when it stays false (no other path may silently drop them).
+extern thread_local bool g_k1w_wrote_patches;
+
 // A launch with fewer 32-block workgroups than this uses the row split (S = 4).
 constexpr uint64_t kSplitBelowGroups = 512;
 // Whether launch_fl_unpack takes K1w for a kernel-argument table of `groups32` 32-block workgroups.
