@@ -311,7 +311,8 @@ class FileWorkload:
         torch.cuda.synchronize()
         self.setup_s = time.perf_counter() - t0
         self.dcs += [DeviceColumns(self.f, ctx, None, c0, c1) for _ in range(copies - 1)]
-        self.plans = [A.Plan(dc.nodes, ctx) for dc in self.dcs]
+        # replayed many times: each plan measures its candidates (VXG_PLAN_MEASURE)
+        self.plans = [A.Plan(dc.nodes, ctx, measure=True) for dc in self.dcs]
         self.n_copies = copies
         self.read_bytes = sum(_tree_buffer_bytes(n) for n in self.dcs[0].nodes)
         self.region_bytes = self.dcs[0].nbytes()
@@ -335,6 +336,9 @@ class FileWorkload:
     def run_copy(self, k: int):
         self.i = k
         self.step()
+
+    def nodes0(self):
+        return list(self.dcs[0].nodes)
 
     def close(self):
         for p in self.plans:
@@ -448,7 +452,7 @@ class Workload:
         self.copies = [[arr.to(dev) for arr in arrs] for _ in range(copies)]
         self.n_copies = copies
         if graph:
-            self.plans = [A.Plan(trees, ctx) for trees in self.copies]
+            self.plans = [A.Plan(trees, ctx, measure=True) for trees in self.copies]
         else:
             self.keep = []
             self.cols = []
@@ -479,6 +483,10 @@ class Workload:
             chk(self.ctx.lib.vxg_canonicalize(self.ctx.handle, C.byref(nodes[k % len(nodes)]), C.byref(out),
                                               self.ctx.stream_ptr()))
 
+    def nodes0(self):
+        self.keep0 = []
+        return [A_flatten(t, self.keep0) for t in self.copies[0]]
+
     def close(self):
         for p in getattr(self, "plans", []):
             p.close()
@@ -487,6 +495,62 @@ class Workload:
 def chk(st):
     from vortex_amd import _lib
     _lib.check(st)
+
+
+def A_flatten(tree, keep):
+    import vortex_amd.arrays as A
+    return A.flatten(tree, keep)
+
+
+def plan_report(wl, steps: int) -> dict:
+    """What the replayed plan hides: the kept graph's mode and its measured
+    candidates (vxg_plan_get_info of copy 0's plan), and what a ONE-SHOT scan of copy 0 pays
+    instead: vxg_plan_create without measurement + its first replay (device time by HIP events,
+    create by host wall clock), and direct vxg_canonicalize calls of every array per step (no
+    graph; host wall time per step over `steps` back-to-back steps, outputs preallocated)."""
+    import torch
+    import vortex_amd.arrays as A
+    ctx = wl.ctx
+    info = wl.plans[0].info()
+    nodes = wl.nodes0()
+    p = A.Plan(nodes, ctx)
+    create_ms = p.info()["create_ms"]
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    e0.record()
+    p.launch()
+    e1.record()
+    torch.cuda.synchronize()
+    first_wall = (time.perf_counter() - t0) * 1e3
+    ctx.sync()
+    first_dev = e0.elapsed_time(e1)
+    one_shot_mode = p.info()
+    p.close()
+    keep: list = []
+    outs = [A.alloc_canonical(ctx, n, keep)[0] for n in nodes]
+
+    def direct():
+        for n, o in zip(nodes, outs):
+            chk(ctx.lib.vxg_canonicalize(ctx.handle, C.byref(n), C.byref(o), ctx.stream_ptr()))
+    for _ in range(3):
+        direct()
+    ctx.sync()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        direct()
+    torch.cuda.synchronize()
+    direct_ms = (time.perf_counter() - t0) * 1e3 / steps
+    ctx.sync()
+    del keep, outs
+    return {"plan_mode": {"batched": info["batched"], "branches": info["branches"],
+                          "direct_launch_nodes": info["direct_nodes"]},
+            "plan_candidates": info["candidates"], "plan_create_ms_measured": info["create_ms"],
+            "one_shot": {"plan_create_ms": create_ms, "batched": one_shot_mode["batched"],
+                         "first_replay_device_ms": round(first_dev, 4), "first_replay_wall_ms": round(first_wall, 4),
+                         "create_plus_first_replay_ms": round(create_ms + first_wall, 4),
+                         "no_graph_ms_per_step": round(direct_ms, 4)}}
 
 
 def run_workload(wl, steps: int, warmup: int, dist):
@@ -623,6 +687,16 @@ def pmc_traffic(name: str):
 
 
 # ------------------------------------------------------------------------------ CPU baseline
+def cpu_model() -> str:
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def _cpu_cores() -> int:
     """Host cores this process may use (the GPU box's share is 16 per GPU; the affinity mask
     may show the whole machine)."""
@@ -675,7 +749,7 @@ def cpu_baselines(budget_s: float, reps: int = 20) -> dict:
     from tools import lineitem as L
     cores = _cpu_cores()
     per_budget = budget_s / 7
-    out = {"nproc": os.cpu_count(), "cores_all": cores, "reps": reps, "kind": "port"}
+    out = {"nproc": os.cpu_count(), "cores_all": cores, "reps": reps, "kind": "port", "cpu_model": cpu_model()}
     Lb = O.lib()
     # C1 full array, 1 core
     rng = np.random.default_rng(42)
@@ -855,8 +929,10 @@ def main():
         del arr
         if rank == 0:
             log(f"[bench] {info['name']}: built in {time.perf_counter() - t0:.1f}s; timing...")
-        steps = args.steps if key == "c1" else max(3, args.steps // 2)
-        elapsed, kmean, kmed = run_workload(wl, steps, args.warmup if key == "c1" else 2, dist)
+        # every config: >= 20 timed steps after >= 3 warm-ups (median of >= 20 reps)
+        steps = args.steps if key == "c1" else max(20, args.steps)
+        warm = args.warmup if key == "c1" else max(3, args.warmup)
+        elapsed, kmean, kmed = run_workload(wl, steps, warm, dist)
         check = None
         if not args.no_verify:
             t1 = time.perf_counter()
@@ -875,8 +951,9 @@ def main():
             t = torch.tensor([float(info["write_bytes"])], dtype=torch.float64, device="cuda")
             dist.all_reduce(t)
             total_write = float(t.item())
+        plan = plan_report(wl, steps) if getattr(wl, "plans", None) else None
         results[key] = dict(info=info, elapsed=elapsed, ms_per_step=per_step * 1e3, kernel_ms_mean=kmean,
-                            kernel_ms_median=kmed, algo_bytes=algo,
+                            kernel_ms_median=kmed, algo_bytes=algo, steps=steps, warmup=warm, plan=plan,
                             value=total_write * steps / elapsed / 1e9, e2e=e2e, check=check, rotation=rotation)
         wl.close()
         del wl
@@ -916,6 +993,7 @@ def main():
                          "kernel_ms_median": round(h["kernel_ms_median"], 5),
                          "algorithmic_bytes_per_launch": h["algo_bytes"]},
             "verified": bool(h["check"] and h["check"]["verified"]),
+            "host": {"cpu_model": cpu_model(), "nproc": os.cpu_count(), "cores_used_max": _cpu_cores()},
             "encodings": {},
         }
         for k, r in results.items():
@@ -928,8 +1006,10 @@ def main():
                 "decoded_GBps_per_gpu_kernel": round(i["write_bytes"] / (r["kernel_ms_mean"] / 1e3) / 1e9, 1),
                 "hbm_frac_algorithmic": round(r["algo_bytes"] / (r["kernel_ms_mean"] / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
                 "kernel_ms_mean": round(r["kernel_ms_mean"], 5), "kernel_ms_median": round(r["kernel_ms_median"], 5),
-                "ms_per_step": round(r["ms_per_step"], 5),
+                "ms_per_step": round(r["ms_per_step"], 5), "steps": r["steps"], "warmup": r["warmup"],
                 "read_bytes": i["read_bytes"], "write_bytes": i["write_bytes"]}
+            if r.get("plan"):
+                ent.update(r["plan"])
             for extra in ("chunks_per_gpu", "chunk_range", "global_chunks", "h2d_region_bytes", "reader_setup_ms"):
                 if extra in i:
                     ent[extra] = i[extra]
@@ -946,7 +1026,7 @@ def main():
                 "value": c1["1core_GBps"], "unit": "GB/s", "cores": 1, "kind": "port",
                 "sample": f"C1 full array (64 Mi u32, W=7) decoded by oracle/vx_oracle.c vxo_unpack (-O3 "
                           f"-march=native), fresh output per call, median of {c1['reps']} reps "
-                          f"(pre-faulted output: {c1['1core_prefaulted_GBps']} GB/s); nproc={cpu['nproc']}; "
+                          f"(pre-faulted output: {c1['1core_prefaulted_GBps']} GB/s); {cpu['cpu_model']}, nproc={cpu['nproc']}; "
                           f"C2-C5 (1 core, and all {cpu['cores_all']} cores for C3/C5) under encodings.*.cpu_baseline"}
         print(json.dumps(line), flush=True)
     if dist is not None:

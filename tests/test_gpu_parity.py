@@ -294,6 +294,66 @@ def test_k1w_fused_patches_errors(ctx, monkeypatch):
         gpu(arr, ctx)
 
 
+def _alp_bad_cluster(rng, n=300_000):
+    """> 256 patches clustered (so workgroups take the 256-ary search, not a window) with first and
+    last index in range and one middle index past the end: a malformed file's patches."""
+    pos = np.concatenate([[0], np.arange(100_000, 105_000), [n - 1]])
+    arr, _ = _alp_patched(rng, n, pos, packed_indices=False)
+    idx = np.asarray(arr.children[1].children[0].buffers[0]).view(np.uint64).copy()
+    assert idx.size > 256 and idx[0] == 0 and idx[-1] == n - 1
+    idx[idx.size // 2] = n + 5
+    arr.children[1].children[0] = A.primitive(idx)
+    return arr
+
+
+def test_k1w_fused_patches_unsorted_cluster_never_writes_out_of_range(ctx, monkeypatch):
+    """the search fallback stores only keys inside the workgroup's range; an index
+    past the end inside an unsorted cluster is reported, not written (the device would fault or
+    corrupt the neighbour allocation otherwise)."""
+    monkeypatch.setenv("VXG_K1_WAVE", "force")
+    rng = np.random.default_rng(79)
+    with pytest.raises(V.VortexGpuError, match="not sorted|out of bounds"):
+        gpu(_alp_bad_cluster(rng), ctx)
+    ctx.sync()  # the error word was cleared by the failing sync
+
+
+def test_plan_measure_flag_and_info(ctx):
+    """vxg_plan_create executes nothing and records one candidate; VXG_PLAN_MEASURE records both,
+    times them and reports a device error found by its runs from create itself."""
+    import torch
+    rng = np.random.default_rng(80)
+    arrs = [E.encode_for_bitpacked(rng.integers(-99, 99, 50_000).astype(np.int64)),
+            E.encode_dict_strings([b"row-%d" % (i % 37) for i in range(20_000)])]
+    dev = [a.to(torch.device("cuda", 0)) for a in arrs]
+    p0 = V.Plan(dev, ctx)
+    i0 = p0.info()
+    assert len(i0["candidates"]) == 1 and i0["candidates"][0]["ms"] == 0.0 and i0["batched"]
+    p1 = V.Plan(dev, ctx, measure=True)
+    i1 = p1.info()
+    assert len(i1["candidates"]) == 2 and all(c["ms"] > 0 for c in i1["candidates"])
+    assert {c["batched"] for c in i1["candidates"]} == {False, True} and i1["create_ms"] > 0
+    for p in (p0, p1):
+        res = p.launch(sync=True)
+        for a, r in zip(arrs, res):
+            ref = canon(a)[0]
+            if isinstance(ref, tuple):
+                assert r.numpy()[0].tobytes() == ref[0].tobytes()
+            else:
+                assert r.numpy().tobytes() == ref.tobytes()
+        p.close()
+    bad = _alp_patched(rng, 50_000, np.array([5, 70, 900]))[0]
+    bad.children[1].children[0] = A.primitive(np.array([5, 70, 50_000], np.uint64))
+    bdev = [bad.to(torch.device("cuda", 0))]
+    with pytest.raises(V.VortexGpuError, match="out of bounds"):
+        V.Plan(bdev, ctx, measure=True)
+    ctx.sync()  # nothing left behind for the caller's next sync
+    p2 = V.Plan(bdev, ctx)  # no measurement: nothing ran, the error comes from the replay
+    ctx.sync()
+    with pytest.raises(V.VortexGpuError, match="out of bounds"):
+        p2.launch(sync=True)
+    p2.close()
+
+
 def test_alp_f32_cascade(ctx):
     rng = np.random.default_rng(4)
     vals = (np.round(rng.uniform(-500, 500, 50_000) * 10) / 10).astype(np.float32)
