@@ -149,6 +149,21 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
     return x;
 }
 
+// Exact wave-wide total of one int64 per lane, uniform (SGPR) result, without LDS: three DPP
+// inclusive scans of 32-bit parts (16 + 16 bits of the low word: each sum < 2^22; the high word
+// modulo 2^32, which is all the 64-bit total needs), read from lane 63.  Replaces a 64-bit
+// __shfl_xor tree (6 rounds of two ds_bpermute + ~7 VALU).
+__device__ __forceinline__ int64_t wave_total64(int64_t v) {
+    const uint64_t u = uint64_t(v);
+    const int a = wave_incl_scan(int(uint32_t(u) & 0xFFFFu));
+    const int b = wave_incl_scan(int(uint32_t(u) >> 16));
+    const int c = wave_incl_scan(int(uint32_t(u >> 32)));
+    const uint32_t A = uint32_t(__builtin_amdgcn_readlane(a, 63));
+    const uint32_t B = uint32_t(__builtin_amdgcn_readlane(b, 63));
+    const uint32_t C = uint32_t(__builtin_amdgcn_readlane(c, 63));
+    return int64_t(uint64_t(A) + (uint64_t(B) << 16) + (uint64_t(C) << 32));
+}
+
 // Exclusive block scan of one int32 per thread (kTile/64 waves); `ws` must not be reused
 // before the next barrier.
 __device__ __forceinline__ int block_excl_scan32(int v, int* ws, int& total) {
@@ -248,7 +263,7 @@ __global__ __launch_bounds__(kTile) void fsst_tile_scan(FsstTable tab, int64_t* 
         }
 #pragma unroll
         for (int r = 0; r < 8; r++) {
-            const int64_t sum = wave_sum(v[r]);
+            const int64_t sum = wave_total64(v[r]);
             if (lane == 0) s_ts[4 * (r0 + r) + wave] = sum;
         }
     }
@@ -260,10 +275,13 @@ __global__ __launch_bounds__(kTile) void fsst_tile_scan(FsstTable tab, int64_t* 
 // whole FastLanes blocks K1-style (8 threads per block, W x 16-byte loads, SWAR rows).  Row R
 // of a block holds strings (R % 8) * 128 + ..., i.e. tile (R % 8) * 128 / kTS of the block, so
 // each thread accumulates kTPB tile partial sums, reduced across its 8 threads.
-template <int W, int... Rs>
+// A: int64 (any lengths) or uint32 (every length of the column < 2^23 and non-negative, so
+// 256 of them sum below 2^31: the common case, half the adds and no 64-bit selects).
+template <int W, class A, int... Rs>
 __device__ __forceinline__ void fl32_tile_rows(const Vec16<32>* p, int t, uint64_t blk0, uint64_t n, uint32_t shift,
-                                               uint32_t reference, bool sgn, int64_t* acc,
+                                               uint32_t reference, bool sgn, A* acc,
                                                std::integer_sequence<int, Rs...>) {
+    const uint32_t left = blk0 + 1024 <= n ? 1024u : uint32_t(n - blk0);  // valid elements of the block
     auto row = [&](auto rc) {
         constexpr int R = decltype(rc)::value;
         const Vec16<32> v = extract_row<32, W, R>(p);
@@ -271,8 +289,10 @@ __device__ __forceinline__ void fl32_tile_rows(const Vec16<32>* p, int t, uint64
 #pragma unroll
         for (int j = 0; j < 4; j++) {
             const uint32_t u = uint32_t(v.elem(j) << shift) + reference;
-            const int64_t x = sgn ? int64_t(int32_t(u)) : int64_t(u);
-            acc[(R % 8) * 128 / kTS] += blk0 + uint64_t(idx0 + j) < n ? x : 0;
+            A x;
+            if constexpr (sizeof(A) == 8) x = sgn ? A(int32_t(u)) : A(u);
+            else x = u;
+            acc[(R % 8) * 128 / kTS] += uint32_t(idx0 + j) < left ? x : A(0);
         }
     };
     (row(std::integral_constant<int, Rs>{}), ...);
@@ -294,26 +314,34 @@ __global__ __launch_bounds__(kTile) void fsst_tile_scan_fl32(FsstTable tab, int6
     int64_t* const block_totals = block_totals_all + c.first_scan;
     const uint64_t blk = sb * 32 + (tid >> 3);
     const int64_t code_end = tile_code_end(c, sb);
-    int64_t acc[kTPB];
+    // every value of the column below 2^23 (uniform): 32-bit sums are exact
+    const uint64_t vmax = ((W >= 32 ? 0xFFFFFFFFull : ((1ull << W) - 1)) << shift) + reference;
+    const bool small = vmax < (1ull << 23) && !(sgn && int32_t(reference) < 0);
+    auto run = [&](auto* tag) {
+        using A = std::remove_pointer_t<decltype(tag)>;
+        A acc[kTPB];
 #pragma unroll
-    for (int k = 0; k < kTPB; k++) acc[k] = 0;
-    if (blk * 1024 < n) {
-        Vec16<32> p[W > 0 ? W : 1];
-        if constexpr (W > 0) {
+        for (int k = 0; k < kTPB; k++) acc[k] = 0;
+        if (blk * 1024 < n) {
+            Vec16<32> p[W > 0 ? W : 1];
+            if constexpr (W > 0) {
 #pragma unroll
-            for (int w = 0; w < W; w++) p[w] = load16<32>(packed + blk * (128 * W) + 128 * w + 16 * t);
+                for (int w = 0; w < W; w++) p[w] = load16<32>(packed + blk * (128 * W) + 128 * w + 16 * t);
+            }
+            fl32_tile_rows<W>(p, t, blk * 1024, n, shift, reference, sgn, acc, std::make_integer_sequence<int, 32>{});
         }
-        fl32_tile_rows<W>(p, t, blk * 1024, n, shift, reference, sgn, acc, std::make_integer_sequence<int, 32>{});
-    }
 #pragma unroll
-    for (int k = 0; k < kTPB; k++) {
+        for (int k = 0; k < kTPB; k++) {
 #pragma unroll
-        for (int d = 1; d < 8; d <<= 1) acc[k] += __shfl_xor(acc[k], d, 64);
-    }
-    if (t == 0) {
+            for (int d = 1; d < 8; d <<= 1) acc[k] += __shfl_xor(acc[k], d, 64);
+        }
+        if (t == 0) {
 #pragma unroll
-        for (int k = 0; k < kTPB; k++) s_ts[(tid >> 3) * kTPB + k] = acc[k];
-    }
+            for (int k = 0; k < kTPB; k++) s_ts[(tid >> 3) * kTPB + k] = int64_t(acc[k]);
+        }
+    };
+    if (small) run(static_cast<uint32_t*>(nullptr));
+    else run(static_cast<int64_t*>(nullptr));
     __syncthreads();
     scan_tile_sums(s_ts, ws, n_tiles, sb, tile_prefix, block_totals, tile_code_all + c.first_tile, code_end);
 }
@@ -579,10 +607,11 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         const_cast<uint4*>(a0), short(0), span ? int((cshift + span + 15) & ~15) : 0, 0x00020000);
     const uint4 cx = as_uint4(__builtin_amdgcn_raw_buffer_load_b128(crs, 16 * tid, 0, 0));
     const uint4 cy = as_uint4(__builtin_amdgcn_raw_buffer_load_b128(crs, 16 * tid + 16, 0, 0));
-    if (wave == 0) {  // prefix of the preceding scan blocks (<= a few hundred totals), one wave
+    const uint32_t nb = tile / kScanTiles;
+    if (wave == 0 && nb == 0 && lane == 0) s_block_prefix = 0;
+    if (wave == 0 && nb > 0) {  // prefix of the preceding scan blocks (<= a few hundred totals), one wave
         // four loads per lane in flight per round (clamped index, no per-element branch), so a
         // tile deep in a large chunk pays one memory round trip here, not one per 64 blocks
-        const uint32_t nb = tile / kScanTiles;
         int64_t acc = 0;
         for (uint32_t b0 = 0; b0 < nb; b0 += 256) {
             int64_t v[4];
@@ -594,7 +623,7 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) v
 #pragma unroll
             for (int k = 0; k < 4; k++) acc += b0 + 64 * k + lane < nb ? v[k] : 0;
         }
-        acc = wave_sum(acc);
+        acc = wave_total64(acc);
         if (lane == 0) s_block_prefix = acc;
     }
     // symbols are stored zero-padded past their length, so a code can OR all 8 bytes; a length
