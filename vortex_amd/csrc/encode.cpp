@@ -253,10 +253,13 @@ uint64_t alp_encode_t(const F* values, uint64_t n, uint8_t* e, uint8_t* f, typen
     alp_encode_all<F>(values, n, be, bf, enc, pidx, pval);
     *e = uint8_t(be);
     *f = uint8_t(bf);
-    std::memcpy(encoded, enc.data(), n * sizeof(typename Alp<F>::I));
+    // (an empty vector's data() may be null: memcpy from it is undefined even for 0 bytes)
+    if (n) std::memcpy(encoded, enc.data(), n * sizeof(typename Alp<F>::I));
     const uint64_t m = std::min<uint64_t>(cap, pidx.size());
-    std::memcpy(patch_idx, pidx.data(), m * 8);
-    std::memcpy(patch_vals, pval.data(), m * sizeof(F));
+    if (m) {
+        std::memcpy(patch_idx, pidx.data(), m * 8);
+        std::memcpy(patch_vals, pval.data(), m * sizeof(F));
+    }
     return pidx.size();
 }
 
