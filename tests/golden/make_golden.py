@@ -53,6 +53,11 @@ def kats() -> list[dict]:
         expect_e=16, expect_f=13, expect_encoded=[1234, 2718, 1234, 4000],
         expect_patches=[[2, f64bits(math.pi)]]))
     out.append(dict(
+        name="alp_f64_nullable_patched", ref="encodings/alp/src/alp/compress.rs:167-192",
+        kind="alp", ptype="f64", values_bits=[f64bits(v) for v in (1.234, 2.718, math.pi, 4.0, 0.0)],
+        validity=[True, True, True, True, False], expect_e=16, expect_f=13, expect_has_patches=True,
+        expect_valid_decoded_bits=[f64bits(v) for v in (1.234, 2.718, math.pi, 4.0)]))
+    out.append(dict(
         name="alp_f32_close_fractional", ref="encodings/alp/src/alp/compress.rs:194-205",
         kind="alp", ptype="f32",
         values_bits=[f32bits(195.26274), f32bits(195.27837), f32bits(-48.815685)],
@@ -72,6 +77,37 @@ def kats() -> list[dict]:
         name="bitpacked_best_bit_width", ref="encodings/fastlanes/src/bitpacking/compress.rs:382-392",
         kind="bit_width_freq", freq=[0, 10, 20, 15, 1, 0, 0, 0], ptype="u8",
         expect_best=3, expect_min_patchless=4))
+    # ---- BitPacked take / slice (compute on compressed) ----------------------
+    out.append(dict(
+        name="bitpacked_take_indices", ref="encodings/fastlanes/src/bitpacking/compute/take.rs:227-241",
+        kind="bitpacked_take", ptype="u8", gen="i % 63", n=4096, bit_width=6,
+        indices=[0, 125, 2047, 2049, 2151, 2790], expect_taken=[0, 62, 31, 33, 9, 18]))
+    out.append(dict(
+        name="bitpacked_take_sliced_indices", ref="encodings/fastlanes/src/bitpacking/compute/take.rs:243-255",
+        kind="bitpacked_take", ptype="u8", gen="i % 63", n=4096, bit_width=6, slice=[128, 2050],
+        indices=[1919, 1921], expect_taken=[31, 33]))
+    out.append(dict(
+        name="bitpacked_take_after_slice", ref="encodings/fastlanes/src/bitpacking/compute/slice.rs:182-206",
+        kind="bitpacked_take", ptype="u32", gen="63 + i", n=3072, bit_width=6, slice=[922, 2061],
+        indices=[101, 1125, 1138], expect_len=3,
+        # the reference asserts only the length; the values are the sliced array's (63 + 922 + i)
+        expect_taken=[1086, 2110, 2123]))
+    out.append(dict(
+        name="bitpacked_slices", ref="encodings/fastlanes/src/bitpacking/compute/slice.rs:54-180",
+        kind="bitpacked_slice",
+        cases=[dict(test="slice_block", ptype="u32", gen="i % 64", n=2048, bit_width=6, slices=[[1024, 2048]],
+                    expect_offset=0, expect_len=1024, expect_at=[[0, 1024 % 64], [1023, 2047 % 64]]),
+               dict(test="slice_within_block", ptype="u32", gen="i % 64", n=2048, bit_width=6, slices=[[512, 1434]],
+                    expect_offset=512, expect_len=922, expect_at=[[0, 512 % 64], [921, 1433 % 64]]),
+               dict(test="slice_within_block_u8s", ptype="u8", gen="i % 63", n=10_000, bit_width=7,
+                    slices=[[768, 9999]], expect_len=9231, expect_at=[[0, 768 % 63], [9230, 9998 % 63]]),
+               dict(test="slice_block_boundary_u8s", ptype="u8", gen="i % 63", n=10_000, bit_width=7,
+                    slices=[[7168, 9216]], expect_len=2048, expect_at=[[0, 7168 % 63], [2047, 9215 % 63]]),
+               dict(test="double_slice_within_block", ptype="u32", gen="i % 64", n=2048, bit_width=6,
+                    slices=[[512, 1434], [127, 911]], expect_offset=639, expect_len=784,
+                    expect_at=[[0, (512 + 127) % 64], [783, (512 + 910) % 64]]),
+               dict(test="slice_empty_patches", ptype="u32", gen="i", n=65, bit_width=6, slices=[[0, 64]],
+                    expect_patches_before=1, expect_has_patches=False, expect_len=64)]))
     # ---- FoR -------------------------------------------------------------------------------
     out.append(dict(
         name="for_u32_offset_million", ref="encodings/fastlanes/src/for/compress.rs:126-133",
@@ -126,6 +162,19 @@ def kats() -> list[dict]:
         name="dict_encode_varbin", ref="encodings/dict/src/compress.rs:239-254",
         kind="dict_varbin", strings=["hello", "world", "hello", "again", "world"],
         expect_codes=[0, 1, 0, 2, 1], expect_values=["hello", "world", "again"]))
+    out.append(dict(
+        name="dict_encode_primitive_nulls", ref="encodings/dict/src/compress.rs:211-237",
+        kind="dict_nullable", ptype="i32", values=[1, 1, 0, 3, 3, 0, 3, 0],
+        validity=[True, True, False, True, True, False, True, False],
+        expect_codes=[1, 1, 0, 2, 2, 0, 2, 0], expect_values=[None, 1, 3]))
+    out.append(dict(
+        name="dict_encode_varbin_nulls", ref="encodings/dict/src/compress.rs:256-282",
+        kind="dict_varbin_nullable", strings=["hello", None, "world", "hello", None, "again", "world", None],
+        expect_codes=[1, 0, 2, 1, 0, 3, 2, 0], expect_values=[None, "hello", "world", "again"]))
+    out.append(dict(
+        name="dict_repeated_values", ref="encodings/dict/src/compress.rs:284-302",
+        kind="dict_varbin", strings=["a", "a", "b", "b", "a", "b", "a", "b"],
+        expect_codes=[0, 0, 1, 1, 0, 1, 0, 1], expect_values=["a", "b"]))
     out.append(dict(
         name="take_primitive", ref="vortex-array/src/array/primitive/compute/take.rs:39-44",
         kind="take", ptype="i32", values=[1, 2, 3, 4, 5], codes=[0, 0, 4, 2],

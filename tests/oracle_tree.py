@@ -339,3 +339,59 @@ def filter_canon(a: Array, predicate: Array):
     O.lib().vxo_make_views(O.p(new_heap), O.p(offs), len(strs), O.p(vbits) if vbits is not None else None, 0,
                            O.p(out))
     return (out, new_heap), fvalid
+
+
+# ---- slice (SliceFn) of the arrays the reference's slice KATs build: metadata-only, as the
+# reference does it (no decode), so the sliced trees exercise the engine's offset handling.
+def slice_primitive(a: Array, start: int, stop: int) -> Array:
+    """primitive/compute/slice.rs:8-16 (buffer sub-range; validity sliced likewise)."""
+    from vortex_amd import arrays as A
+    vals = np.ascontiguousarray(a.buffers[0]).view(NP_OF_PTYPE[a.ptype])[start:stop]
+    mask = _validity(a)
+    return A.primitive(vals, a.ptype, validity=None if mask is None else mask[start:stop])
+
+
+def slice_sparse(sp: Array, start: int, stop: int) -> Array:
+    """sparse/compute/slice.rs:7-21: the indices in [start, stop) found by search_sorted(Left) of
+    indices_offset + start / + stop (sparse/mod.rs:123-129); new indices_offset = old + start."""
+    from vortex_amd import arrays as A
+    off = sp.meta["indices_offset"]
+    idx = canon(sp.children[0])[0].astype(np.uint64)
+    i0 = int(np.searchsorted(idx, np.uint64(off + start), side="left"))
+    i1 = int(np.searchsorted(idx, np.uint64(off + stop), side="left"))
+    ind = slice_any(sp.children[0], i0, i1)
+    vals = slice_any(sp.children[1], i0, i1)
+    fill = None if sp.meta["fill_is_null"] else np.frombuffer(
+        sp.meta["fill"][: ptype_width(sp.ptype)], NP_OF_PTYPE[sp.ptype])[0]
+    return A.sparse(ind, vals, stop - start, indices_offset=off + start, fill=fill, ptype=sp.ptype)
+
+
+def slice_bitpacked(a: Array, start: int, stop: int) -> Array:
+    """bitpacking/compute/slice.rs:10-43: whole blocks of packed words around [start, stop) of the
+    physical positions (offset included), the new offset = physical start % 1024, patches sliced
+    and dropped when the slice holds none."""
+    from vortex_amd import arrays as A
+    if a.validity == VALIDITY["ARRAY"]:
+        raise NotImplementedError("slice of a BitPacked validity child")
+    W, off0 = a.meta["bit_width"], a.meta["offset"]
+    s, e = start + off0, stop + off0
+    offset = s % 1024
+    block_start, block_stop = s - offset, ((e + 1023) // 1024) * 1024
+    packed = np.ascontiguousarray(a.buffers[0]).view(np.uint8)[(block_start // 8) * W: (block_stop // 8) * W]
+    patches = None
+    if a.meta["has_patches"]:
+        sp = slice_sparse(a.children[0], start, stop)
+        if sp.children[0].len:
+            patches = sp
+    return A.bitpacked(packed, a.ptype, W, stop - start, offset, patches,
+                       validity=None if a.validity == VALIDITY["NON_NULLABLE"] else "ALL_VALID")
+
+
+def slice_any(a: Array, start: int, stop: int) -> Array:
+    if a.encoding == ENC["FL_BITPACKED"]:
+        return slice_bitpacked(a, start, stop)
+    if a.encoding == ENC["PRIMITIVE"]:
+        return slice_primitive(a, start, stop)
+    if a.encoding == ENC["SPARSE"]:
+        return slice_sparse(a, start, stop)
+    raise NotImplementedError(f"slice of encoding {a.encoding}")

@@ -473,3 +473,77 @@ def test_filter_oracle_rejects_bad_predicates():
         filter_canon(arr, A.bool_array(np.ones(3, bool)))
     with pytest.raises(ValueError):
         filter_canon(arr, A.bool_array(np.ones(4, bool), validity=np.ones(4, bool)))
+
+
+# ---------------------------------------------------------------- round-4 KATs
+def _kat_bitpacked(k):
+    vals = _gen(k)
+    return vals, E.encode_bitpacked(vals, bit_width=k["bit_width"])
+
+
+@pytest.mark.parametrize("name", ["bitpacked_take_indices", "bitpacked_take_sliced_indices",
+                                  "bitpacked_take_after_slice"])
+def test_kat_bitpacked_take(name):
+    from oracle_tree import slice_any
+    k = KATS[name]
+    _, arr = _kat_bitpacked(k)
+    if "slice" in k:
+        arr = slice_any(arr, *k["slice"])
+    got = canon(arr)[0][np.array(k["indices"])]
+    assert got.tolist() == k["expect_taken"]
+
+
+@pytest.mark.parametrize("case", [c["test"] for c in KATS["bitpacked_slices"]["cases"]])
+def test_kat_bitpacked_slices(case):
+    from oracle_tree import slice_any
+    k = next(c for c in KATS["bitpacked_slices"]["cases"] if c["test"] == case)
+    vals, arr = _kat_bitpacked(k)
+    if "expect_patches_before" in k:
+        assert arr.meta["has_patches"] and arr.children[0].children[0].len == k["expect_patches_before"]
+    for s in k["slices"]:
+        arr = slice_any(arr, *s)
+    assert arr.len == k["expect_len"]
+    if "expect_offset" in k:
+        assert arr.meta["offset"] == k["expect_offset"]
+    if "expect_has_patches" in k:
+        assert arr.meta["has_patches"] == k["expect_has_patches"]
+    got = canon(arr)[0]
+    for i, v in k.get("expect_at", []):
+        assert int(got[i]) == v
+
+
+def test_kat_alp_f64_nullable_patched():
+    k = KATS["alp_f64_nullable_patched"]
+    vals = _f(k["values_bits"], "f64")
+    valid = np.array(k["validity"])
+    e, f, enc, idx, pv = E.alp_encode(vals)
+    assert (e, f) == (k["expect_e"], k["expect_f"]) and (idx.size > 0) == k["expect_has_patches"]
+    arr = A.alp(A.primitive(enc, validity=valid), e, f, A.sparse(A.primitive(idx), A.primitive(pv, validity="ALL_VALID"),
+                                                                   vals.size))
+    got, gvalid = canon(arr)
+    assert gvalid.tolist() == k["validity"]
+    assert [struct.pack("<d", x).hex() for x in got[valid]] == k["expect_valid_decoded_bits"]
+
+
+def test_kat_dict_nullable():
+    k = KATS["dict_encode_primitive_nulls"]
+    codes, dv, vvalid = E.dict_encode_nullable(np.array(k["values"], np.int32), k["validity"])
+    assert codes.tolist() == k["expect_codes"]
+    assert [None if not ok else int(x) for x, ok in zip(dv, vvalid)] == k["expect_values"]
+    arr = E.encode_dict_nullable(np.array(k["values"], np.int32), k["validity"])
+    got, gvalid = canon(arr)
+    assert gvalid.tolist() == k["validity"]
+    assert [int(x) for x, ok in zip(got, k["validity"]) if ok] == [v for v, ok in zip(k["values"], k["validity"]) if ok]
+    k = KATS["dict_encode_varbin_nulls"]
+    strs = [None if s is None else s.encode() for s in k["strings"]]
+    arr = E.encode_dict_strings_nullable(strs)
+    assert canon(arr.children[1])[0].tolist() == k["expect_codes"]
+    (views, heap), gvalid = canon(arr)
+    assert gvalid.tolist() == [s is not None for s in strs]
+    assert [view_bytes(views, heap, i) if s is not None else None for i, s in enumerate(strs)] == strs
+    vals = arr.children[0]
+    (vv, vh), vvalid = canon(vals)
+    assert [view_bytes(vv, vh, i).decode() if vvalid[i] else None for i in range(vals.len)] == k["expect_values"]
+    k = KATS["dict_repeated_values"]
+    arr = E.encode_dict_strings([s.encode() for s in k["strings"]])
+    assert canon(arr.children[1])[0].tolist() == k["expect_codes"]

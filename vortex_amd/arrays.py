@@ -507,6 +507,30 @@ class Canonical:
     data: Any = None         # torch.uint8 tensor holding every data buffer of the view array
     validity: Any = None     # torch.uint8 LSB bitmap or None (no nulls)
     data_buffers: Any = None  # [(offset, len)] of each data buffer inside `data`
+    binary: bool = False      # VarBinView of DType::Binary (else Utf8)
+
+    def to_arrow(self):
+        """Canonical::into_arrow (canonical.rs:71-85; varbinview/mod.rs:518 varbinview_as_arrow):
+        the canonical buffers copied to host memory and handed to pyarrow without conversion --
+        Primitive [validity, values], Bool [validity, LSB bits], VarBinView [validity, views, data
+        buffer 0..n-1] (Utf8View / BinaryView).  pyarrow is optional: only this method imports it."""
+        import pyarrow as pa
+        validity = None if self.validity is None else pa.py_buffer(self.validity.cpu().numpy()[: (self.len + 7) // 8].copy())
+        nulls = -1 if validity is not None else 0
+        if self.kind == "primitive":
+            t = {"u8": pa.uint8(), "u16": pa.uint16(), "u32": pa.uint32(), "u64": pa.uint64(), "i8": pa.int8(),
+                 "i16": pa.int16(), "i32": pa.int32(), "i64": pa.int64(), "f16": pa.float16(), "f32": pa.float32(),
+                 "f64": pa.float64()}[self.ptype]
+            return pa.Array.from_buffers(t, self.len, [validity, pa.py_buffer(self.values.cpu().numpy().copy())],
+                                         null_count=nulls)
+        if self.kind == "bool":
+            bits = self.values.cpu().numpy()[: (self.len + 7) // 8].copy()
+            return pa.Array.from_buffers(pa.bool_(), self.len, [validity, pa.py_buffer(bits)], null_count=nulls)
+        data = self.data.cpu().numpy()
+        bufs = [pa.py_buffer(data[o: o + n].copy()) for o, n in self.data_buffers]
+        views = pa.py_buffer(self.views.cpu().numpy()[: 16 * self.len].copy())
+        return pa.Array.from_buffers(pa.binary_view() if self.binary else pa.string_view(), self.len,
+                                     [validity, views] + bufs, null_count=nulls)
 
     def numpy(self):
         """Host copy: values as the ptype's numpy dtype, a bool mask, or (views u8[n,16], data u8[])."""
@@ -551,7 +575,7 @@ def canonicalize(a: Array, ctx: Context, out_values=None, sync: bool = True) -> 
         _lib.check(st)
         break
     out = _lib.VxgCanonical()
-    res = Canonical(_kind(a), a.len, a.ptype)
+    res = Canonical(_kind(a), a.len, a.ptype, binary=a.dtype == DTYPE["BINARY"])
     nbits = ((a.len + 31) // 32) * 4
     valid_t = torch.empty(max(nbits, 4), dtype=torch.uint8, device=dev) if a.nullable else None
     if a.dtype in (DTYPE["PRIMITIVE"], DTYPE["BOOL"]):
@@ -650,7 +674,7 @@ def filter(a: Array, predicate: Array, ctx: Context) -> Canonical:
     out.data_buffers, out.data_buffers_cap = table, 1
     _lib.check(ctx.lib.vxg_filter_array(ctx.handle, C.byref(node), C.byref(pnode), C.byref(out), ctx.stream_ptr()))
     k = int(out.len)
-    res = Canonical(kind, k, a.ptype)
+    res = Canonical(kind, k, a.ptype, binary=a.dtype == DTYPE["BINARY"])
     if kind == "primitive":
         res.values = buf[: k * ptype_width(a.ptype)]
     elif kind == "bool":
@@ -690,7 +714,7 @@ def alloc_canonical(ctx: Context, node: _lib.VxgArray, keep: list, table_cap: in
     _lib.check(ctx.lib.vxg_canonical_layout(ctx.handle, C.byref(node), C.byref(vb), C.byref(db), table,
                                             table_cap, C.byref(nb)))
     n = int(node.len)
-    res = Canonical(_kind_of_node(node), n, PTYPES[node.ptype])
+    res = Canonical(_kind_of_node(node), n, PTYPES[node.ptype], binary=node.dtype == DTYPE["BINARY"])
     o = _lib.VxgCanonical()
     if node.dtype in (DTYPE["PRIMITIVE"], DTYPE["BOOL"]):
         vals = torch.empty(max(vb.value, 16), dtype=torch.uint8, device=dev)

@@ -188,6 +188,52 @@ def encode_dict(values, bitpack_codes: bool = True) -> Array:
     return A.dict_array(A.primitive(dv), c)
 
 
+def dict_encode_nullable(values, validity) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """dict_encode_typed_primitive over a NULLABLE array (dict/compress.rs:39-86): the dictionary
+    starts with a null slot (zero value, invalid) and every null row gets code 0 -> (codes u64,
+    values, values validity)."""
+    v = np.ascontiguousarray(values)
+    valid = np.asarray(validity, dtype=bool)
+    pos: dict = {}
+    dv = [v.dtype.type(0)]
+    codes = np.zeros(v.size, dtype=np.uint64)
+    for i in range(v.size):
+        if valid[i]:
+            key = v[i].tobytes()
+            if key not in pos:
+                pos[key] = len(dv)
+                dv.append(v[i])
+            codes[i] = pos[key]
+    vvalid = np.ones(len(dv), dtype=bool)
+    vvalid[0] = False
+    return codes, np.array(dv, dtype=v.dtype), vvalid
+
+
+def encode_dict_nullable(values, validity, bitpack_codes: bool = True) -> Array:
+    codes, dv, vvalid = dict_encode_nullable(values, validity)
+    c = encode_bitpacked(codes, allow_patches=False) if bitpack_codes else A.primitive(codes)
+    return A.dict_array(A.primitive(dv, validity=vvalid), c)
+
+
+def encode_dict_strings_nullable(strings: Sequence[Optional[bytes]], utf8: bool = True) -> Array:
+    """dict_encode_typed_varbin over a nullable VarBin (dict/compress.rs:118-143): slot 0 is the
+    null entry (empty bytes, invalid), null rows get code 0, u32 offsets."""
+    pos: dict = {}
+    codes = np.zeros(len(strings), dtype=np.uint64)
+    uniq: list = []
+    for i, s in enumerate(strings):
+        if s is not None:
+            if s not in pos:
+                pos[s] = len(uniq) + 1
+                uniq.append(s)
+            codes[i] = pos[s]
+    heap, offs, _ = strings_to_heap([b""] + uniq)
+    vvalid = np.ones(len(uniq) + 1, dtype=bool)
+    vvalid[0] = False
+    values = A.varbin(A.primitive(offs.astype(np.uint32)), A.primitive(heap), utf8=utf8, validity=vvalid)
+    return A.dict_array(values, encode_bitpacked(codes, allow_patches=False))
+
+
 def encode_delta(values, bitpack_deltas: bool = True) -> Array:
     """DeltaArray::try_from_primitive_array (delta/mod.rs:72-78, compress.rs:14-98)."""
     v = np.ascontiguousarray(values)
