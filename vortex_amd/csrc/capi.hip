@@ -76,6 +76,13 @@ static bool dict_rows_enabled() {
     return on;
 }
 
+// VXG_PLAN_VB_K1G=0 (read at every plan recording): an unbatched plan canonicalizes chunked
+// Dict(VarBin) string columns with a views launch + K14 instead of one K1g launch (A/B).
+static bool plan_vb_k1g() {
+    const char* e = std::getenv("VXG_PLAN_VB_K1G");
+    return !(e && e[0] == '0');
+}
+
 // VXG_FUSED_PATCHES=0 (read at every decode): ALP's outer patches take the separate scatter
 // launch instead of the K1w launch (A/B measurements, parity tests of both paths).
 static bool fused_patches_enabled() {
@@ -1706,8 +1713,10 @@ vxg_status Planner::strings_into(const vxg_array& a, uint8_t* views, uint8_t* da
                 // a plan batch with a small dictionary: K1g builds its views in LDS (no views
                 // launch); otherwise the views are built into dviews first
                 const vxg_array& codes = c.children[1];
-                const bool vb = defer(a) && v.len <= kGenVarBinDictMax && v.len > 0 && codes.len > 0 &&
-                                !codes.meta.bitpacked.has_patches;
+                // also in an unbatched plan (its own K1g launch per column instead of a views
+                // launch + K14: VXG_PLAN_VB_K1G=0 restores those)
+                const bool vb = (defer(a) || (plan_ && plan_vb_k1g())) && v.len <= kGenVarBinDictMax && v.len > 0 &&
+                                codes.len > 0 && !codes.meta.bitpacked.has_patches;
                 if (!vb) dicts.push_back(d);
                 UnpackArgs ua{};
                 ua.dict = vb ? nullptr : dviews;

@@ -617,6 +617,24 @@ __device__ __forceinline__ void unpack_chunk_w(const ChunkDev& c, uint64_t g, ui
         // profiles/r03_ubench_k1.txt)
         using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
         const u32x4* src = reinterpret_cast<const u32x4*>(c.packed + blk0 * (128 * W));
+#if VXG_K1W_BURST
+        // A/B variant (VXG_K1W_BURST=1 build): a full workgroup issues all PQ of its thread's
+        // loads before any LDS write (PQ * 4 VGPRs; the default loop keeps one load in flight)
+        constexpr int NQ = BPW * 8 * W, PQ = (NQ + 255) / 256;
+        if (nb == BPW) {
+            u32x4 v[PQ];
+#pragma unroll
+            for (int p = 0; p < PQ; p++) {
+                const int q = int(threadIdx.x) + 256 * p;
+                v[p] = __builtin_nontemporal_load(src + (q < NQ ? q : NQ - 1));
+            }
+#pragma unroll
+            for (int p = 0; p < PQ; p++) {
+                const int q = int(threadIdx.x) + 256 * p;
+                if (q < NQ) reinterpret_cast<uint4*>(s_pk)[q] = make_uint4(v[p][0], v[p][1], v[p][2], v[p][3]);
+            }
+        } else
+#endif
         for (int q = threadIdx.x; q < nb * 8 * W; q += 256) {
             const u32x4 v = __builtin_nontemporal_load(src + q);
             reinterpret_cast<uint4*>(s_pk)[q] = make_uint4(v[0], v[1], v[2], v[3]);

@@ -3,6 +3,7 @@
 // the K1g launch of a plan batch (k1g.hip), which hands it LDS of its own.
 #pragma once
 
+#include "fl_unpack_impl.hpp"
 #include "intcol.hpp"
 
 namespace vxg {
@@ -30,10 +31,48 @@ __device__ __forceinline__ V runend_value(const IntCol& c, uint64_t r) {
 
 constexpr int kRunsThreads = 256;
 constexpr int kRunsSpan = 4096;  // outputs per expansion window
-// LDS of one workgroup: run heads (kRunsSpan u32), run values (kRunEndRunsPerGroup V), scratch
+// Run heads are u16 entries padded by one every 16 (entry p at p + p / 16): thread t's 16
+// consecutive entries of the max-scan sit 17 entries apart from thread t + 1's, so the scan's
+// reads and writes hit 32 distinct banks (unpadded, 32-byte strides put 8 lanes on one bank).
+constexpr int kRunsHeadSlots = kRunsSpan + kRunsSpan / 16;
+__device__ __forceinline__ int runs_pad(int p) { return p + (p >> 4); }
+// LDS of one workgroup: run heads (u16, padded; 8.5 KiB, also the staging area of the ends'
+// packed words and the decoded ends), run values (kRunEndRunsPerGroup V; also the staging area
+// of the values' packed words), scratch
 template <typename V>
 constexpr size_t runs_lds_bytes() {
-    return kRunsSpan * 2 + kRunEndRunsPerGroup * sizeof(V) + 128;
+    return kRunsHeadSlots * 2 + kRunEndRunsPerGroup * sizeof(V) + 128;
+}
+
+// A child read block-wise: a packed [FoR](BitPacked) u32/u64 column (slice offset 0) whose block
+// the workgroup's 1024 runs are -- staged in LDS with coalesced 16-byte loads (no per-element
+// unpack_single: its index math and two global loads per element were most of K8r's VALU).
+__device__ __forceinline__ bool runs_blockwise(const IntCol& c, size_t stage_bytes) {
+    return c.packed && c.offset == 0 && (c.width == 4 || c.width == 8) && size_t(128) * c.W <= stage_bytes;
+}
+__device__ __forceinline__ void runs_stage(const IntCol& c, uint64_t blk, uint8_t* s) {
+    const uint32_t n16 = 8 * c.W;  // 128 * W bytes
+    const uint4* src = reinterpret_cast<const uint4*>(static_cast<const uint8_t*>(c.p) + blk * (128ull * c.W));
+    for (uint32_t q = threadIdx.x; q < n16; q += kRunsThreads) reinterpret_cast<uint4*>(s)[q] = src[q];
+}
+// values 256 k + threadIdx.x (k < 4) of the staged block, FoR applied, as intcol_get returns them
+__device__ __forceinline__ void runs_extract(const IntCol& c, const uint8_t* s, int64_t out[4]) {
+    if (c.width == 8) {
+        const RtRows<64> rows(c.W);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint64_t v = c.W ? rows.get(reinterpret_cast<const uint64_t*>(s), uint32_t(k)) : 0;
+            out[k] = int64_t((v << c.shift) + c.reference);
+        }
+    } else {
+        const RtRows<32> rows(c.W);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t v = c.W ? rows.get(reinterpret_cast<const uint32_t*>(s), uint32_t(k)) : 0;
+            const uint32_t r = uint32_t(v << c.shift) + uint32_t(c.reference);
+            out[k] = c.sgn ? int64_t(int32_t(r)) : int64_t(r);
+        }
+    }
 }
 
 // Workgroup g of the launch expands its 1024 runs of chunk c (c.first_group = its first
@@ -45,9 +84,11 @@ __device__ __forceinline__ void runend_runs_body(const RunEndChunk& c, uint64_t 
     // run heads as 16-bit run indices (<= 1024 runs per workgroup): 8 KiB instead of 16, so the
     // LDS of a u64 expansion (16.6 KiB) allows 8 workgroups per CU instead of 6
     static_assert(RPG < 65536, "run index must fit 16 bits");
+    static_assert(RPG == 4 * kBlock && RPT == 4, "one FastLanes block of runs per workgroup, 4 per thread");
+    constexpr size_t kHeadBytes = size_t(kRunsHeadSlots) * 2;
     uint16_t* const s_head = reinterpret_cast<uint16_t*>(lds);
-    V* const s_val = reinterpret_cast<V*>(lds + SPAN * 2);
-    uint8_t* const misc = lds + SPAN * 2 + RPG * sizeof(V);
+    V* const s_val = reinterpret_cast<V*>(lds + kHeadBytes);
+    uint8_t* const misc = lds + kHeadBytes + RPG * sizeof(V);
     uint64_t* const s_wlast = reinterpret_cast<uint64_t*>(misc);           // kBlock / 64
     uint64_t& s_lo = reinterpret_cast<uint64_t*>(misc)[4];
     uint64_t& s_hi = reinterpret_cast<uint64_t*>(misc)[5];
@@ -61,21 +102,49 @@ __device__ __forceinline__ void runend_runs_body(const RunEndChunk& c, uint64_t 
     // any is used
     uint64_t e[RPT];
     V v[RPT];
+    const uint64_t eprev = tid == 0 && r0 > 0 ? uint64_t(intcol_get(c.ends, r0 - 1)) : 0;
+    // block-wise children (uniform): the ends' words staged in the head area, the values' in the
+    // value area, extracted (value 256 k + t per thread), then exchanged through LDS into
+    // run order -- ends as u64 in the head area, values straight into s_val
+    const bool bwe = runs_blockwise(c.ends, kHeadBytes);
+    const bool bwv = (sizeof(V) == 4 || sizeof(V) == 8) && runs_blockwise(c.values, RPG * sizeof(V)) &&
+                     c.values.width == int(sizeof(V));
+    if (bwe || bwv) {
+        const uint64_t blk = r0 / uint64_t(RPG);
+        if (bwe) runs_stage(c.ends, blk, lds);
+        if (bwv) runs_stage(c.values, blk, reinterpret_cast<uint8_t*>(s_val));
+        __syncthreads();
+        int64_t xe[4], xv[4];
+        if (bwe) runs_extract(c.ends, lds, xe);
+        if (bwv) runs_extract(c.values, reinterpret_cast<const uint8_t*>(s_val), xv);
+        __syncthreads();
+        uint64_t* const s_e64 = reinterpret_cast<uint64_t*>(lds);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            if (bwe) s_e64[tid + kBlock * k] = uint64_t(xe[k]);
+            if (bwv) {
+                V x;
+                const uint64_t u = uint64_t(xv[k]);
+                __builtin_memcpy(&x, &u, sizeof(V));  // low bytes: the value's bits
+                s_val[tid + kBlock * k] = x;
+            }
+        }
+        __syncthreads();
+    }
 #pragma unroll
     for (int k = 0; k < RPT; k++) {
         const int i = RPT * tid + k;
         const uint64_t rr = r0 + uint64_t(i < nr ? i : 0);
-        e[k] = uint64_t(intcol_get(c.ends, rr));
-        v[k] = runend_value<V>(c.values, rr);
+        e[k] = bwe ? reinterpret_cast<const uint64_t*>(lds)[RPT * tid + k] : uint64_t(intcol_get(c.ends, rr));
+        if (!bwv) v[k] = runend_value<V>(c.values, rr);
     }
-    const uint64_t eprev = tid == 0 && r0 > 0 ? uint64_t(intcol_get(c.ends, r0 - 1)) : 0;
     uint64_t en[RPT], st[RPT];
 #pragma unroll
     for (int k = 0; k < RPT; k++) {
         const int i = RPT * tid + k;
         en[k] = trim(e[k]);
         if (i < nr) {
-            s_val[i] = v[k];
+            if (!bwv) s_val[i] = v[k];
             if (i == nr - 1) s_hi = en[k];
             if (r0 + uint64_t(i) + 1 == c.n_runs && en[k] < c.len)  // the ends do not reach the end of the array
                 __hip_atomic_fetch_or(err, kErrRunEnd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -98,13 +167,12 @@ __device__ __forceinline__ void runend_runs_body(const RunEndChunk& c, uint64_t 
     uint32_t carry = 0;
     for (uint64_t wb = lo; wb < hi; wb += SPAN) {
         const int wn = int(hi - wb < uint64_t(SPAN) ? hi - wb : uint64_t(SPAN));
-#pragma unroll
-        for (int k = 0; k < PER / 8; k++) reinterpret_cast<uint4*>(s_head)[tid * (PER / 8) + k] = make_uint4(0, 0, 0, 0);
+        for (int q = tid; q < kRunsHeadSlots / 8; q += kBlock) reinterpret_cast<uint4*>(s_head)[q] = make_uint4(0, 0, 0, 0);
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < RPT; k++)
             if (en[k] > st[k] && st[k] >= wb && st[k] < wb + uint64_t(wn))
-                s_head[st[k] - wb] = uint16_t(RPT * tid + k + 1);
+                s_head[runs_pad(int(st[k] - wb))] = uint16_t(RPT * tid + k + 1);
         __syncthreads();
         // inclusive max-scan of s_head (thread t owns entries [PER t, PER t + PER)), seeded
         // with the run carried over from the previous window
@@ -112,7 +180,7 @@ __device__ __forceinline__ void runend_runs_body(const RunEndChunk& c, uint64_t 
         uint32_t m = 0;
 #pragma unroll
         for (int k = 0; k < PER; k++) {
-            m = max(m, uint32_t(s_head[tid * PER + k]));
+            m = max(m, uint32_t(s_head[tid * (PER + 1) + k]));
             vv[k] = m;
         }
         uint32_t x = m;
@@ -130,7 +198,7 @@ __device__ __forceinline__ void runend_runs_body(const RunEndChunk& c, uint64_t 
             if (w < (tid >> 6)) before = max(before, s_wmax[w]);
         before = max(before, carry);
 #pragma unroll
-        for (int k = 0; k < PER; k++) s_head[tid * PER + k] = uint16_t(max(vv[k], before));
+        for (int k = 0; k < PER; k++) s_head[tid * (PER + 1) + k] = uint16_t(max(vv[k], before));
         __syncthreads();
         if constexpr (sizeof(V) == 4 || sizeof(V) == 8) {
             // two consecutive outputs per lane, one 8/16-byte store (half the per-output address
@@ -140,9 +208,9 @@ __device__ __forceinline__ void runend_runs_body(const RunEndChunk& c, uint64_t 
             const int a = int((reinterpret_cast<uintptr_t>(out + wb) / sizeof(V)) & 1);
             if (a && tid == 0 && wn > 0) nt_store(out + wb, s_val[s_head[0] - 1]);
             for (int i = a + 2 * tid; i < wn; i += 2 * kBlock) {
-                const V v0 = s_val[s_head[i] - 1];
+                const V v0 = s_val[s_head[runs_pad(i)] - 1];
                 if (i + 1 < wn) {
-                    const V v1 = s_val[s_head[i + 1] - 1];
+                    const V v1 = s_val[s_head[runs_pad(i + 1)] - 1];
                     P pv;
                     __builtin_memcpy(&pv, &v0, sizeof(V));
                     __builtin_memcpy(reinterpret_cast<uint8_t*>(&pv) + sizeof(V), &v1, sizeof(V));
@@ -152,9 +220,9 @@ __device__ __forceinline__ void runend_runs_body(const RunEndChunk& c, uint64_t 
                 }
             }
         } else {
-            for (int i = tid; i < wn; i += kBlock) nt_store(out + wb + i, s_val[s_head[i] - 1]);
+            for (int i = tid; i < wn; i += kBlock) nt_store(out + wb + i, s_val[s_head[runs_pad(i)] - 1]);
         }
-        if (tid == 0) s_carry = s_head[wn - 1];
+        if (tid == 0) s_carry = s_head[runs_pad(wn - 1)];
         __syncthreads();
         carry = s_carry;
     }
