@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--world", type=int, default=1)
     ap.add_argument("--rank", type=int, default=0)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--rotate", type=int, default=1,
+                    help="device copies of the file regions the plan-mode steps rotate through")
     ap.add_argument("--mark", action="store_true",
                     help="launch a torch kernel before every column (segments a rocprofv3 --pmc trace; tools/c5_traffic.py)")
     args = ap.parse_args()
@@ -39,9 +41,12 @@ def main():
     ctx = V.Context(0)
     f = VortexFile(host)
     dc = DeviceColumns(f, ctx, None, mine.start, mine.stop)
+    # --rotate K: K device copies of the column regions, the plan-mode steps cycle through them
+    # (one plan per copy) so a column's inputs come from HBM, not from the Infinity Cache
+    rot = [dc] + [DeviceColumns(f, ctx, None, mine.start, mine.stop) for _ in range(args.rotate - 1)]
     tot_t = tot_p = tot_b = 0.0
     marker = torch.zeros(1, device="cuda")
-    for col, node in zip(dc.columns, dc.nodes):
+    for ci, (col, node) in enumerate(zip(dc.columns, dc.nodes)):
         keep: list = []
         o, res = A.alloc_canonical(ctx, node, keep)
         if args.mark:  # after the output sizing (its length readback is not a decode step)
@@ -62,23 +67,24 @@ def main():
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / args.reps
         # the same column as its own vxg_plan (device chunk tables: one launch per kernel group)
-        plan = A.Plan([node], ctx)
-        for _ in range(3):
-            plan.launch()
+        plans = [A.Plan([r.nodes[ci]], ctx, measure=True) for r in rot]
+        for k in range(3):
+            plans[k % len(plans)].launch()
         ctx.sync()
         e0.record()
-        for _ in range(args.reps):
-            plan.launch()
+        for k in range(args.reps):
+            plans[k % len(plans)].launch()
         e1.record()
         torch.cuda.synchronize()
         plan_ms = e0.elapsed_time(e1) / args.reps
-        plan.close()
+        for p in plans:
+            p.close()
         rb = bench._tree_buffer_bytes(node)
         wb = sum(int(t.numel()) for t in (res.values, res.views, res.data) if t is not None)
         tot_t += ms
         tot_p += plan_ms
         tot_b += rb + wb
-        print(json.dumps({"column": f.columns[col].name, "chunks": len(mine), "ms": round(ms, 4),
+        print(json.dumps({"column": f.columns[col].name, "chunks": len(mine), "rotate": args.rotate, "ms": round(ms, 4),
                           "plan_ms": round(plan_ms, 4), "read_bytes": rb, "write_bytes": wb,
                           "hbm_frac": round((rb + wb) / ms / 1e6 / 8000, 3),
                           "plan_hbm_frac": round((rb + wb) / plan_ms / 1e6 / 8000, 3)}), flush=True)

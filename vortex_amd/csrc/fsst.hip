@@ -693,9 +693,10 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         }
         if (live) {
             const bool valid = (vbyte >> (tid & 7)) & 1;
-            views[first + tid] = valid ? lds_view(s_heap32, hshift + int(my_rel), uint32_t(my_len),
-                                                  uint32_t(tile_out0 + my_rel), bidx)
-                                       : make_uint4(0, 0, 0, 0);
+            // non-temporal like the heap copy-out: the views are written once and not re-read
+            nt_store(views + first + tid, valid ? lds_view(s_heap32, hshift + int(my_rel), uint32_t(my_len),
+                                                          uint32_t(tile_out0 + my_rel), bidx)
+                                                : make_uint4(0, 0, 0, 0));
         }
     } else {
         // direct path: per-string decode straight into HBM (codes of string i are

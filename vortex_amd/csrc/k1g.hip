@@ -221,11 +221,22 @@ int gen_kind(int T, int epi, int vw, bool varbin_dict) {
     return -1;
 }
 
+// Blocks per K1g workgroup: as many as kGenPackedLds of packed words hold, at most
+// VXG_K1G_BPW (default 4; read once).
+static uint32_t gen_bpw_max() {
+    static const uint32_t v = [] {
+        const char* e = std::getenv("VXG_K1G_BPW");
+        const long x = e ? std::strtol(e, nullptr, 10) : 4;
+        return uint32_t(x >= 1 && x <= 32 ? x : 4);
+    }();
+    return v;
+}
+
 uint32_t gen_bpw(int T, int W) {
     (void)T;
     const uint32_t per = 128u * uint32_t(W > 0 ? W : 1);
-    const uint32_t b = kGenPackedLds / per;
-    return b > 4 ? 4 : (b < 1 ? 1 : b);
+    const uint32_t b = kGenPackedLds / per, m = gen_bpw_max();
+    return b > m ? m : (b < 1 ? 1 : b);
 }
 
 uint32_t gen_runs_lds_bytes(int value_width) {
