@@ -536,124 +536,171 @@ __device__ __forceinline__ void fsst_segments(const uint8_t* __restrict__ s_code
     }
 }
 
-template <class OffAcc, class LenAcc, bool EXT>
-__global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) void fsst_decode(FsstTable tab, uint64_t total_tiles,
-                                                     const int64_t* __restrict__ tile_prefix_all,
-                                                     const int64_t* __restrict__ block_totals_all,
-                                                     const int64_t* __restrict__ tile_code_all,
-                                                     uint32_t* __restrict__ err,
-                                                     const uint32_t* __restrict__ wg_chunk) {
-    __shared__ uint64_t s_sym[256];
-    __shared__ uint8_t s_len[256];
-    __shared__ int ws_a[kTile / 64], ws_b[kTile / 64];
-    __shared__ unsigned ws_bad[kTile / 64], ws_esc[kTile / 64];
-    __shared__ int64_t ws64[kTile / 64];
-    __shared__ int64_t s_block_prefix;
-    // + slack: the straddling segment's dwords past the tile (masked in pass 1)
-    __shared__ __attribute__((aligned(16))) uint8_t s_codes[kCodeLds + 48];
-    // + slack: view reads past a string, and ORs of the (<= 3) dwords past the tile
-    __shared__ __attribute__((aligned(16))) uint32_t s_heap32[(kHeapLds + 96) / 4];
-    uint8_t* const s_heap = reinterpret_cast<uint8_t*>(s_heap32);
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 
-    // a recorded plan's device table: the workgroup's chunk from the plan's per-workgroup map
-    // (one scalar load) instead of the wave-wide count over the table
-    const FsstChunk& ch = EXT ? tab.ext[wg_chunk[blockIdx.x]] : fsst_chunk_of<false, EXT>(tab, blockIdx.x);
-    const unsigned n_symbols = ch.n_symbols;
+// The decode's LDS (declared by the kernel, handed to the tile functions).
+struct DecLds {
+    uint64_t* s_sym;
+    uint8_t* s_len;
+    int* ws_a;
+    int* ws_b;
+    unsigned* ws_bad;
+    unsigned* ws_esc;
+    int64_t* ws64;
+    int64_t* s_block_prefix;
+    uint8_t* s_codes;
+    uint32_t* s_heap32;
+};
+
+// Everything a tile's decode reads from memory before it can start, requested together (no
+// result used before all are issued): the pre-pass records (scalar), the thread's length word(s),
+// its validity byte and two 16-byte chunks of the tile's code range.  A workgroup that decodes
+// two tiles issues the second tile's loads with the first's, so their latency hides behind the
+// first tile's decode.
+template <class LenAcc>
+struct TileIn {
+    uint32_t tile;  // within the chunk
+    int64_t tp, cl, cf;
+    TileLen<LenAcc> tl;
+    uint8_t vbyte;
+    uint4 cx, cy;
+};
+
+template <class OffAcc, class LenAcc>
+__device__ __forceinline__ void tile_issue(const FsstChunk& ch, uint32_t tile, const int64_t* __restrict__ tile_prefix_all,
+                                           const int64_t* __restrict__ tile_code_all, TileIn<LenAcc>& in) {
+    const int tid = threadIdx.x;
+    const OffAcc code_offs(ch.offs);
+    const LenAcc lens(ch.lens);
+    const uint64_t n = ch.n;
+    in.tile = tile;
+    // the tile's code range [cf, cl) (absolute offsets into `codes`) comes from the pre-pass
+    // records, so the code bytes are requested in the same round trip as the other loads
+    const int64_t* __restrict__ tile_code = tile_code_all + ch.first_tile;
+    in.tp = tile_prefix_all[ch.first_tile + tile];
+    in.cl = tile_code[tile];
+    in.cf = tile > 0 ? tile_code[tile - 1] : code_offs(0);
+    const uint64_t first = uint64_t(tile) * kTile;
+    const bool live = first + uint64_t(tid) < n;
+    const uint32_t kc = live ? uint32_t(tid) : uint32_t(n - 1 - first);  // clamped index in the tile
+    in.tl.issue(lens, first, kc);
+    in.vbyte = ch.validity ? ch.validity[(first + kc) >> 3] : uint8_t(0xFF);
+    const int cshift = int((reinterpret_cast<uintptr_t>(ch.codes) + uintptr_t(in.cf)) & 15);
+    const int64_t span64 = in.cl - in.cf;
+    const int span = span64 >= 0 && span64 <= kCodeLds ? int(span64) : 0;
+    const uint4* const a0 = reinterpret_cast<const uint4*>(ch.codes + (in.cf - cshift));
+    // chunks tid and tid + 1 of the tile's aligned code range (funnel-shifted when staged), as
+    // bounds-checked buffer loads: no branch (a chunk past the range reads as zeros without a
+    // memory access), so they retire under one wait
+    const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint4*>(a0), short(0), span ? int((cshift + span + 15) & ~15) : 0, 0x00020000);
+    in.cx = as_uint4(__builtin_amdgcn_raw_buffer_load_b128(crs, 16 * tid, 0, 0));
+    in.cy = as_uint4(__builtin_amdgcn_raw_buffer_load_b128(crs, 16 * tid + 16, 0, 0));
+}
+
+// The chunk's symbol table: loads (symbol_load) and its LDS image (symbol_store).  Symbols are
+// stored zero-padded past their length, so a code can OR all 8 bytes; a length > 8 is corrupt
+// input (reported).  Slot 255 (the escape, never a symbol) has no bytes and the sentinel length
+// 16 (pass 1's escape detector); escapes are decoded explicitly.
+__device__ __forceinline__ void symbol_load(const FsstChunk& ch, uint64_t& sym_v, uint32_t& sl) {
+    sym_v = 0;
+    sl = 0;
+    if (ch.n_symbols) {  // (an empty table -- e.g. trained on null strings only -- may have null buffers)
+        const uint32_t sk = uint32_t(threadIdx.x) < ch.n_symbols ? uint32_t(threadIdx.x) : 0u;
+        sym_v = ch.symbols[sk];
+        sl = ch.sym_lens[sk];
+    }
+}
+__device__ __forceinline__ void symbol_store(const FsstChunk& ch, const DecLds& L, uint64_t sym_v, uint32_t sl,
+                                             uint32_t* __restrict__ err) {
+    const int tid = threadIdx.x;
+    const bool has = uint32_t(tid) < ch.n_symbols;
+    L.s_sym[tid] = has ? (sl >= 8 ? sym_v : sym_v & ((1ull << (8 * sl)) - 1)) : 0;
+    L.s_len[tid] = has ? uint8_t(min(sl, 8u)) : uint8_t(tid == 255 ? 16 : 0);
+    if (has && sl > 8) __hip_atomic_fetch_or(err, kErrFsst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Prefix of the scan blocks before the tile's (<= a few hundred totals), by wave 0 into
+// s_block_prefix: four loads per lane in flight per round (clamped index, no per-element
+// branch), so a tile deep in a large chunk pays one memory round trip here, not one per 64 blocks.
+__device__ __forceinline__ void block_prefix(const FsstChunk& ch, uint32_t tile, const int64_t* __restrict__ block_totals_all,
+                                             const DecLds& L) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t nb = tile / kScanTiles;
+    if (wave != 0) return;
+    if (nb == 0) {
+        if (lane == 0) *L.s_block_prefix = 0;
+        return;
+    }
+    const int64_t* __restrict__ block_totals = block_totals_all + ch.first_scan;
+    int64_t acc = 0;
+    for (uint32_t b0 = 0; b0 < nb; b0 += 256) {
+        int64_t v[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t b = b0 + 64 * k + lane;
+            v[k] = block_totals[b < nb ? b : nb - 1];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) acc += b0 + 64 * k + lane < nb ? v[k] : 0;
+    }
+    acc = wave_total64(acc);
+    if (lane == 0) *L.s_block_prefix = acc;
+}
+
+// Ablation mask (diagnostics only, VXG_FSST_ABL read once by the host; outputs are then WRONG):
+// 1 skips the segment passes, 2 the copy-out, 4 the views, 8 everything after the prologue.
+__constant__ uint32_t g_fsst_abl = 0;
+
+// One tile's decode once its loads are in flight and its symbol table and s_block_prefix have been
+// written (the length scan's barrier publishes them): length scan, staging, segments, copy-out,
+// views -- or the per-string direct path.
+template <class OffAcc, class LenAcc>
+__device__ __forceinline__ void tile_run(const FsstChunk& ch, const TileIn<LenAcc>& in, const DecLds& L,
+                                         uint32_t* __restrict__ err) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const uint8_t* __restrict__ codes = ch.codes;
     const OffAcc code_offs(ch.offs);
     const LenAcc lens(ch.lens);
     const uint64_t n = ch.n;
-    const uint8_t* __restrict__ validity = ch.validity;
-    const int64_t* __restrict__ tile_prefix = tile_prefix_all + ch.first_tile;
-    const int64_t* __restrict__ block_totals = block_totals_all + ch.first_scan;
-    const int64_t* __restrict__ tile_code = tile_code_all + ch.first_tile;
     uint8_t* __restrict__ heap = ch.heap;
     uint4* __restrict__ views = reinterpret_cast<uint4*>(ch.views);
     const uint32_t bidx = ch.bidx;
-    const uint32_t tile = uint32_t(blockIdx.x - ch.first_tile);
-    // Prologue: the scalar records first (their latency overlaps the vector loads below), then
-    // every vector load issued before any result is used -- indices clamped, results selected
-    // afterwards, no atomic or branch between a load and its use -- so they retire under one
-    // wait.  The tile's code range [cf, cl) (absolute offsets into `codes`) comes from the
-    // pre-pass records, so the code bytes are requested in this same round trip.
-    const int64_t tp = tile_prefix[tile];
-    const int64_t cl = tile_code[tile];
-    const int64_t cf = tile > 0 ? tile_code[tile - 1] : code_offs(0);
-    const uint64_t first = uint64_t(tile) * kTile;
+    const uint64_t first = uint64_t(in.tile) * kTile;
     const bool live = first + uint64_t(tid) < n;
-    const uint32_t kc = live ? uint32_t(tid) : uint32_t(n - 1 - first);  // clamped index in the tile
-    const bool has = uint32_t(tid) < n_symbols;
-    uint64_t sym_v = 0;
-    uint32_t sl = 0;
-    if (n_symbols) {  // (an empty table -- e.g. trained on null strings only -- may have null buffers)
-        const uint32_t sk = has ? uint32_t(tid) : 0u;
-        sym_v = ch.symbols[sk];
-        sl = ch.sym_lens[sk];
-    }
-    TileLen<LenAcc> tl;
-    tl.issue(lens, first, kc);
-    const uint8_t vbyte = validity ? validity[(first + kc) >> 3] : uint8_t(0xFF);
-    const int cshift = int((reinterpret_cast<uintptr_t>(codes) + uintptr_t(cf)) & 15);
-    const int64_t span64 = cl - cf;
+    const uint8_t vbyte = in.vbyte;
+    const int cshift = int((reinterpret_cast<uintptr_t>(codes) + uintptr_t(in.cf)) & 15);
+    const int64_t span64 = in.cl - in.cf;
     const bool span_ok = span64 >= 0 && span64 <= kCodeLds;
     const int span = span_ok ? int(span64) : 0;  // tile codes at s_codes[0, span) once staged
-    const uint4* const a0 = reinterpret_cast<const uint4*>(codes + (cf - cshift));  // (pointer arithmetic: global loads)
+    const uint4* const a0 = reinterpret_cast<const uint4*>(codes + (in.cf - cshift));  // (pointer arithmetic: global loads)
     const int nchunk = (span + 15) >> 4;
-    // chunks tid and tid + 1 of the tile's aligned code range (funnel-shifted when staged), as
-    // bounds-checked buffer loads: no branch (a chunk past the range reads as zeros without a
-    // memory access), so they retire under the prologue's one wait
-    const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint4*>(a0), short(0), span ? int((cshift + span + 15) & ~15) : 0, 0x00020000);
-    const uint4 cx = as_uint4(__builtin_amdgcn_raw_buffer_load_b128(crs, 16 * tid, 0, 0));
-    const uint4 cy = as_uint4(__builtin_amdgcn_raw_buffer_load_b128(crs, 16 * tid + 16, 0, 0));
-    const uint32_t nb = tile / kScanTiles;
-    if (wave == 0 && nb == 0 && lane == 0) s_block_prefix = 0;
-    if (wave == 0 && nb > 0) {  // prefix of the preceding scan blocks (<= a few hundred totals), one wave
-        // four loads per lane in flight per round (clamped index, no per-element branch), so a
-        // tile deep in a large chunk pays one memory round trip here, not one per 64 blocks
-        int64_t acc = 0;
-        for (uint32_t b0 = 0; b0 < nb; b0 += 256) {
-            int64_t v[4];
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const uint32_t b = b0 + 64 * k + lane;
-                v[k] = block_totals[b < nb ? b : nb - 1];
-            }
-#pragma unroll
-            for (int k = 0; k < 4; k++) acc += b0 + 64 * k + lane < nb ? v[k] : 0;
-        }
-        acc = wave_total64(acc);
-        if (lane == 0) s_block_prefix = acc;
-    }
-    // symbols are stored zero-padded past their length, so a code can OR all 8 bytes; a length
-    // > 8 is corrupt input (reported after the scan).  Slot 255 (the escape, never a symbol) has no
-    // bytes and the sentinel length 16 (pass 1's escape detector); escapes are decoded explicitly.
-    s_sym[tid] = has ? (sl >= 8 ? sym_v : sym_v & ((1ull << (8 * sl)) - 1)) : 0;
-    s_len[tid] = has ? uint8_t(min(sl, 8u)) : uint8_t(tid == 255 ? 16 : 0);
-    const int64_t my_len = live ? tl.value(lens) : 0;
+    uint8_t* const s_codes = L.s_codes;
+    uint32_t* const s_heap32 = L.s_heap32;
+    uint8_t* const s_heap = reinterpret_cast<uint8_t*>(s_heap32);
+    const int64_t my_len = live ? in.tl.value(lens) : 0;
     const bool bad = my_len < 0 || my_len > kHeapLds;
 
     // (a) length scan: int32 with DPP when every length is in [0, kHeapLds] (then a staged
     // tile is possible), int64 otherwise (direct path).
     const unsigned long long bm = __ballot(bad);
-    if (lane == 0) ws_bad[wave] = bm != 0;
+    if (lane == 0) L.ws_bad[wave] = bm != 0;
     int t32;
-    const int rel32 = block_excl_scan32(bad ? 0 : int(my_len), ws_a, t32);
-    const bool any_bad = (ws_bad[0] | ws_bad[1] | ws_bad[2] | ws_bad[3]) != 0;
+    const int rel32 = block_excl_scan32(bad ? 0 : int(my_len), L.ws_a, t32);
+    const bool any_bad = (L.ws_bad[0] | L.ws_bad[1] | L.ws_bad[2] | L.ws_bad[3]) != 0;
     int64_t my_rel = rel32, tile_total = t32;
-    if (any_bad) my_rel = block_exclusive_scan<kTile / 64>(my_len, ws64, tile_total);  // uniform branch
-    if (has && sl > 8) __hip_atomic_fetch_or(err, kErrFsst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int64_t tile_out0 = tp + s_block_prefix;
+    if (any_bad) my_rel = block_exclusive_scan<kTile / 64>(my_len, L.ws64, tile_total);  // uniform branch
+    const int64_t tile_out0 = in.tp + *L.s_block_prefix;
     const bool stage = !any_bad && span_ok && tile_total <= kHeapLds;
 
+    const uint32_t abl = g_fsst_abl;
+    if (abl & 8) return;
     if (stage) {
         // (b) stage the tile's code bytes into LDS shifted so that the tile's first code is
-        // s_codes[0] (chunk tid was loaded in the prologue; larger tiles load the rest here),
+        // s_codes[0] (chunk tid was loaded with the prologue; larger tiles load the rest here),
         // and zero the image
         const int hshift = int((reinterpret_cast<uintptr_t>(heap) + tile_out0) & 15);  // image byte hshift = heap[tile_out0]
         const int ttot = int(tile_total);
-        if (tid < nchunk) *reinterpret_cast<uint4*>(s_codes + 16 * tid) = funnel16(cx, cy, cshift);
+        if (tid < nchunk) *reinterpret_cast<uint4*>(s_codes + 16 * tid) = funnel16(in.cx, in.cy, cshift);
         for (int q = tid + kTile; q < nchunk; q += kTile) {  // tiles of > 4 KiB of codes
             const uint4 x = a0[q];
             uint4 y = make_uint4(0, 0, 0, 0);
@@ -663,14 +710,14 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         const int nz = (hshift + ttot + 16 + 15) >> 4;
         for (int q = tid; q < nz; q += kTile) reinterpret_cast<uint4*>(s_heap32)[q] = make_uint4(0, 0, 0, 0);
         __syncthreads();
-        switch ((span + 4 * kTile - 1) / (4 * kTile)) {  // dwords per thread, tile-uniform
+        if (!(abl & 1)) switch ((span + 4 * kTile - 1) / (4 * kTile)) {  // dwords per thread, tile-uniform
         case 0:
-        case 1: fsst_segments<1>(s_codes, span, s_sym, s_len, s_heap32, hshift, ttot, ws_b, ws_esc, err); break;
-        case 2: fsst_segments<2>(s_codes, span, s_sym, s_len, s_heap32, hshift, ttot, ws_b, ws_esc, err); break;
-        case 3: fsst_segments<3>(s_codes, span, s_sym, s_len, s_heap32, hshift, ttot, ws_b, ws_esc, err); break;
-        case 4: fsst_segments<4>(s_codes, span, s_sym, s_len, s_heap32, hshift, ttot, ws_b, ws_esc, err); break;
-        case 5: fsst_segments<5>(s_codes, span, s_sym, s_len, s_heap32, hshift, ttot, ws_b, ws_esc, err); break;
-        default: fsst_segments<6>(s_codes, span, s_sym, s_len, s_heap32, hshift, ttot, ws_b, ws_esc, err); break;
+        case 1: fsst_segments<1>(s_codes, span, L.s_sym, L.s_len, s_heap32, hshift, ttot, L.ws_b, L.ws_esc, err); break;
+        case 2: fsst_segments<2>(s_codes, span, L.s_sym, L.s_len, s_heap32, hshift, ttot, L.ws_b, L.ws_esc, err); break;
+        case 3: fsst_segments<3>(s_codes, span, L.s_sym, L.s_len, s_heap32, hshift, ttot, L.ws_b, L.ws_esc, err); break;
+        case 4: fsst_segments<4>(s_codes, span, L.s_sym, L.s_len, s_heap32, hshift, ttot, L.ws_b, L.ws_esc, err); break;
+        case 5: fsst_segments<5>(s_codes, span, L.s_sym, L.s_len, s_heap32, hshift, ttot, L.ws_b, L.ws_esc, err); break;
+        default: fsst_segments<6>(s_codes, span, L.s_sym, L.s_len, s_heap32, hshift, ttot, L.ws_b, L.ws_esc, err); break;
         }
         static_assert(kCodeLds <= 6 * 4 * kTile, "six dwords per thread cover the staged codes");
         __syncthreads();
@@ -679,7 +726,7 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         // stores; the <= 15 + 15 bytes of the ragged first/last chunk (shared with the
         // neighbouring tiles) are one byte store per lane of wave 0 (lanes 0-15 the head, 16-31
         // the tail) instead of a per-thread loop of byte/short/dword stores.
-        {
+        if (!(abl & 2)) {
             uint8_t* const gbase = heap + (tile_out0 - hshift);
             const int end = hshift + ttot;
             const int qa = (hshift + 15) >> 4, qb = end >> 4;
@@ -687,11 +734,11 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) v
                 nt_store(reinterpret_cast<uint4*>(gbase + 16 * q), *reinterpret_cast<const uint4*>(s_heap + 16 * q));
             if (tid < 32) {
                 const int a = tid < 16 ? tid : 16 * qb + (tid - 16);
-                const bool in = tid < 16 ? (a >= hshift && a < min(16 * qa, end)) : (a >= max(16 * qb, 16 * qa) && a < end);
-                if (in) gbase[a] = s_heap[a];
+                const bool inr = tid < 16 ? (a >= hshift && a < min(16 * qa, end)) : (a >= max(16 * qb, 16 * qa) && a < end);
+                if (inr) gbase[a] = s_heap[a];
             }
         }
-        if (live) {
+        if (live && !(abl & 4)) {
             const bool valid = (vbyte >> (tid & 7)) & 1;
             // non-temporal like the heap copy-out: the views are written once and not re-read
             nt_store(views + first + tid, valid ? lds_view(s_heap32, hshift + int(my_rel), uint32_t(my_len),
@@ -713,11 +760,11 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) v
                 if (o < o_end) heap[o] = codes[k];
                 o++;
             } else {
-                const uint64_t sym = s_sym[c];
-                const int L = s_len[c];
-                for (int b = 0; b < L; b++)
+                const uint64_t sym = L.s_sym[c];
+                const int Ln = L.s_len[c];
+                for (int b = 0; b < Ln; b++)
                     if (o + b < o_end) heap[o + b] = uint8_t(sym >> (8 * b));
-                o += L;
+                o += Ln;
             }
         }
         if (o != o_end) __hip_atomic_fetch_or(err, kErrFsst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -728,6 +775,79 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) v
             views[i] = valid ? build_view(vlen, uint32_t(o_start), bidx,
                                           [&](int b) { return uint32_t(b) < vlen ? hp[b] : uint8_t(0); })
                              : make_uint4(0, 0, 0, 0);
+        }
+    }
+}
+
+// NT tiles per workgroup (global tiles NT g .. NT g + NT - 1): every tile's loads are issued in
+// the prologue, the tiles are decoded one after the other in the same LDS.  NT = 2 hides the
+// second tile's load latency behind the first tile's decode (the decode is latency-bound: a
+// 256-string tile is two dependent memory round trips and ~2 us of work).
+template <class OffAcc, class LenAcc, bool EXT, int NT>
+__global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(NT == 1 ? 8 : 6, 8))) void fsst_decode(
+    FsstTable tab, uint64_t total_tiles, const int64_t* __restrict__ tile_prefix_all,
+    const int64_t* __restrict__ block_totals_all, const int64_t* __restrict__ tile_code_all, uint32_t* __restrict__ err,
+    const uint32_t* __restrict__ wg_chunk) {
+    __shared__ uint64_t s_sym[256];
+    __shared__ uint8_t s_len[256];
+    __shared__ int ws_a[kTile / 64], ws_b[kTile / 64];
+    __shared__ unsigned ws_bad[kTile / 64], ws_esc[kTile / 64];
+    __shared__ int64_t ws64[kTile / 64];
+    __shared__ int64_t s_block_prefix;
+    // + slack: the straddling segment's dwords past the tile (masked in pass 1)
+    __shared__ __attribute__((aligned(16))) uint8_t s_codes[kCodeLds + 48];
+    // + slack: view reads past a string, and ORs of the (<= 3) dwords past the tile
+    __shared__ __attribute__((aligned(16))) uint32_t s_heap32[(kHeapLds + 96) / 4];
+    const DecLds L{s_sym, s_len, ws_a, ws_b, ws_bad, ws_esc, ws64, &s_block_prefix, s_codes, s_heap32};
+
+    // the tiles' chunks: a recorded plan's device table through the plan's per-tile map (one
+    // scalar load), else the workgroup-uniform search of the kernel-argument table
+    // (chunk INDICES, not pointers: a pointer into the kernel-argument table would force the
+    // table into scratch)
+    auto chunk_index = [&](uint64_t t) -> uint32_t {
+        if constexpr (EXT) {
+            return wg_chunk[t];
+        } else {
+            uint32_t lo = 0, hi = tab.n;
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (tab.c[mid].first_tile <= t) lo = mid; else hi = mid;
+            }
+            return lo;
+        }
+    };
+    auto chunk = [&](uint32_t ci) -> const FsstChunk& { return EXT ? tab.ext[ci] : tab.c[ci]; };
+    const uint64_t g0 = uint64_t(blockIdx.x) * NT;
+    const uint32_t ci0 = chunk_index(g0);
+    TileIn<LenAcc> in0;
+    tile_issue<OffAcc, LenAcc>(chunk(ci0), uint32_t(g0 - chunk(ci0).first_tile), tile_prefix_all, tile_code_all, in0);
+    uint32_t ci1 = ci0;
+    TileIn<LenAcc> in1;
+    const bool two = NT == 2 && g0 + 1 < total_tiles;  // workgroup-uniform
+    if constexpr (NT == 2) {
+        if (two) {
+            ci1 = chunk_index(g0 + 1);
+            tile_issue<OffAcc, LenAcc>(chunk(ci1), uint32_t(g0 + 1 - chunk(ci1).first_tile), tile_prefix_all,
+                                       tile_code_all, in1);
+        }
+    }
+    uint64_t sym_v;
+    uint32_t sl;
+    symbol_load(chunk(ci0), sym_v, sl);
+    block_prefix(chunk(ci0), in0.tile, block_totals_all, L);
+    symbol_store(chunk(ci0), L, sym_v, sl, err);
+    tile_run<OffAcc, LenAcc>(chunk(ci0), in0, L, err);
+    if constexpr (NT == 2) {
+        if (two) {
+            __syncthreads();  // every LDS read of the first tile is done
+            const bool new_chunk = ci1 != ci0;
+            if (new_chunk) {  // a chunk boundary between the tiles (rare): its own symbol table
+                symbol_load(chunk(ci1), sym_v, sl);
+                symbol_store(chunk(ci1), L, sym_v, sl, err);
+            }
+            if (new_chunk || in1.tile / kScanTiles != in0.tile / kScanTiles)
+                block_prefix(chunk(ci1), in1.tile, block_totals_all, L);
+            tile_run<OffAcc, LenAcc>(chunk(ci1), in1, L, err);
         }
     }
 }
@@ -779,8 +899,21 @@ bool with_acc(int kind, F&& f) {
 
 }  // namespace
 
+// Tiles per decode workgroup (VXG_FSST_TILES = 1 or 2, read at every launch; A/B).
+static int fsst_tiles_per_wg() {
+    const char* e = std::getenv("VXG_FSST_TILES");
+    return e && e[0] == '1' ? 1 : 2;
+}
+
 vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint32_t* err, hipStream_t s,
                              DevTables* dt) {
+    static const bool abl_set = [] {
+        const char* e = std::getenv("VXG_FSST_ABL");
+        if (!e) return false;
+        const uint32_t m = uint32_t(std::strtoul(e, nullptr, 10));
+        return hipMemcpyToSymbol(HIP_SYMBOL(g_fsst_abl), &m, sizeof m) == hipSuccess;
+    }();
+    (void)abl_set;
     for (const FsstChunk& c : chunks) {
         if (c.n_symbols > 255) return set_error(VXG_ERR_INVALID_ARGUMENT, "FSST symbol table > 255 entries");
         if ((c.n + kTS - 1) / kTS > 0xFFFFFFFFull) return set_error(VXG_ERR_INVALID_ARGUMENT, "FSST array too long");
@@ -848,8 +981,12 @@ vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint
                         if (std::get<2>(key) < 0)
                             hipLaunchKernelGGL((fsst_tile_scan<LA, X>), dim3(unsigned(scans)), dim3(kTile), 0, s, tab,
                                                tp, bt, tc);
-                        hipLaunchKernelGGL((fsst_decode<OA, LA, X>), dim3(unsigned(tiles)), dim3(kTile), 0, s, tab,
-                                           tiles, tp, bt, tc, err, wg_chunk);
+                        if (fsst_tiles_per_wg() == 2)
+                            hipLaunchKernelGGL((fsst_decode<OA, LA, X, 2>), dim3(unsigned((tiles + 1) / 2)), dim3(kTile), 0,
+                                               s, tab, tiles, tp, bt, tc, err, wg_chunk);
+                        else
+                            hipLaunchKernelGGL((fsst_decode<OA, LA, X, 1>), dim3(unsigned(tiles)), dim3(kTile), 0, s, tab,
+                                               tiles, tp, bt, tc, err, wg_chunk);
                     };
                     if (tab.ext) go(std::true_type{});
                     else go(std::false_type{});
