@@ -624,6 +624,37 @@ def test_fsst_many_scan_blocks(ctx, compress_children):
     assert_string_parity(arr, ctx)
 
 
+@pytest.mark.parametrize("tiles", ["1", "2"])
+def test_fsst_two_tiles_per_workgroup_boundaries(ctx, tiles, monkeypatch):
+    """A decode workgroup may take two consecutive tiles (VXG_FSST_TILES): pairs that straddle a
+    chunk boundary (each chunk its own symbol table), a scan-block boundary inside a chunk (chunk-
+    relative tiles 127 | 128: a different block prefix), a chunk's direct-path tile next to a staged
+    one, and an odd total (the last workgroup has one tile) -- in a chunked array and in a plan."""
+    import torch
+    monkeypatch.setenv("VXG_FSST_TILES", tiles)
+    rng = np.random.default_rng(31)
+    sizes = [100, 40_000, 256 * 3, 513, 70]  # tiles 1, 157, 3, 3, 1 -> 165 in total (odd)
+    chunks, strings = [], []
+    for c, n in enumerate(sizes):
+        ss = _comment_strings(rng, n, vocab=15 + 3 * c)
+        if c == 3:  # long strings: one tile of this chunk overflows the LDS images (direct path)
+            for i in range(256, 400):
+                ss[i] = bytes(rng.integers(97, 123, 90).astype(np.uint8))
+        if c in (1, 4):
+            for i in rng.choice(n, n // 9, replace=False):
+                ss[i] = None
+        chunks.append(E.encode_fsst(ss))
+        strings.extend(ss)
+    arr = A.chunked(chunks)
+    assert_string_parity(arr, ctx, strings)
+    plan = V.Plan([arr.to(torch.device("cuda", 0))], ctx)
+    res = plan.launch(sync=True)[0]
+    (rv, rh), _ = canon(arr)
+    assert res.numpy()[0].tobytes() == rv.tobytes()
+    assert [b.tobytes() for b in res.buffers()] == [h.tobytes() for h in rh]
+    plan.close()
+
+
 def test_fsst_inconsistent_lengths_is_an_error(ctx):
     strings = [b"carefully final deposits"] * 600
     arr = E.encode_fsst(strings, compress_children=False)
