@@ -624,16 +624,13 @@ def test_fsst_many_scan_blocks(ctx, compress_children):
     assert_string_parity(arr, ctx)
 
 
-@pytest.mark.parametrize("tiles", ["1", "2"])
-def test_fsst_two_tiles_per_workgroup_boundaries(ctx, tiles, monkeypatch):
-    """A decode workgroup may take two consecutive tiles (VXG_FSST_TILES): pairs that straddle a
-    chunk boundary (each chunk its own symbol table), a scan-block boundary inside a chunk (chunk-
-    relative tiles 127 | 128: a different block prefix), a chunk's direct-path tile next to a staged
-    one, and an odd total (the last workgroup has one tile) -- in a chunked array and in a plan."""
+def test_fsst_chunk_and_scan_block_boundaries(ctx):
+    """FSST tiles next to a chunk boundary (each chunk its own symbol table), a scan-block boundary
+    inside a chunk (chunk-relative tiles 127 | 128: a different block prefix), a chunk's direct-path
+    tile next to a staged one, and one-tile chunks -- in a chunked array and in a plan."""
     import torch
-    monkeypatch.setenv("VXG_FSST_TILES", tiles)
     rng = np.random.default_rng(31)
-    sizes = [100, 40_000, 256 * 3, 513, 70]  # tiles 1, 157, 3, 3, 1 -> 165 in total (odd)
+    sizes = [100, 40_000, 256 * 3, 513, 70]  # tiles 1, 157, 3, 3, 1
     chunks, strings = [], []
     for c, n in enumerate(sizes):
         ss = _comment_strings(rng, n, vocab=15 + 3 * c)

@@ -553,9 +553,7 @@ struct DecLds {
 
 // Everything a tile's decode reads from memory before it can start, requested together (no
 // result used before all are issued): the pre-pass records (scalar), the thread's length word(s),
-// its validity byte and two 16-byte chunks of the tile's code range.  A workgroup that decodes
-// two tiles issues the second tile's loads with the first's, so their latency hides behind the
-// first tile's decode.
+// its validity byte and two 16-byte chunks of the tile's code range.
 template <class LenAcc>
 struct TileIn {
     uint32_t tile;  // within the chunk
@@ -779,15 +777,14 @@ __device__ __forceinline__ void tile_run(const FsstChunk& ch, const TileIn<LenAc
     }
 }
 
-// NT tiles per workgroup (global tiles NT g .. NT g + NT - 1): every tile's loads are issued in
-// the prologue, the tiles are decoded one after the other in the same LDS.  NT = 2 hides the
-// second tile's load latency behind the first tile's decode (the decode is latency-bound: a
-// 256-string tile is two dependent memory round trips and ~2 us of work).
-template <class OffAcc, class LenAcc, bool EXT, int NT>
-__global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(NT == 1 ? 8 : 6, 8))) void fsst_decode(
-    FsstTable tab, uint64_t total_tiles, const int64_t* __restrict__ tile_prefix_all,
-    const int64_t* __restrict__ block_totals_all, const int64_t* __restrict__ tile_code_all, uint32_t* __restrict__ err,
-    const uint32_t* __restrict__ wg_chunk) {
+// One tile per workgroup: the tile's loads (tile_issue) are all in flight before the symbol
+// table and the scan-block prefix are loaded.  (Two consecutive tiles per workgroup with both
+// tiles' loads issued in the prologue was measured 10 % slower on C4 -- 6 instead of 8 waves per
+// SIMD; profiles/r04_fsst_decode.md.)
+template <class OffAcc, class LenAcc, bool EXT>
+__global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) void fsst_decode(
+    FsstTable tab, const int64_t* __restrict__ tile_prefix_all, const int64_t* __restrict__ block_totals_all,
+    const int64_t* __restrict__ tile_code_all, uint32_t* __restrict__ err, const uint32_t* __restrict__ wg_chunk) {
     __shared__ uint64_t s_sym[256];
     __shared__ uint8_t s_len[256];
     __shared__ int ws_a[kTile / 64], ws_b[kTile / 64];
@@ -800,56 +797,31 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(NT == 1 ?
     __shared__ __attribute__((aligned(16))) uint32_t s_heap32[(kHeapLds + 96) / 4];
     const DecLds L{s_sym, s_len, ws_a, ws_b, ws_bad, ws_esc, ws64, &s_block_prefix, s_codes, s_heap32};
 
-    // the tiles' chunks: a recorded plan's device table through the plan's per-tile map (one
-    // scalar load), else the workgroup-uniform search of the kernel-argument table
-    // (chunk INDICES, not pointers: a pointer into the kernel-argument table would force the
-    // table into scratch)
-    auto chunk_index = [&](uint64_t t) -> uint32_t {
-        if constexpr (EXT) {
-            return wg_chunk[t];
-        } else {
-            uint32_t lo = 0, hi = tab.n;
-            while (hi - lo > 1) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (tab.c[mid].first_tile <= t) lo = mid; else hi = mid;
-            }
-            return lo;
+    // the tile's chunk: a recorded plan's device table through the plan's per-tile map (one
+    // scalar load), else the workgroup-uniform search of the kernel-argument table (a chunk
+    // INDEX, not a pointer: a pointer into the kernel-argument table would force the table into
+    // scratch)
+    const uint64_t g = blockIdx.x;
+    uint32_t ci;
+    if constexpr (EXT) {
+        ci = wg_chunk[g];
+    } else {
+        uint32_t lo = 0, hi = tab.n;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (tab.c[mid].first_tile <= g) lo = mid; else hi = mid;
         }
-    };
-    auto chunk = [&](uint32_t ci) -> const FsstChunk& { return EXT ? tab.ext[ci] : tab.c[ci]; };
-    const uint64_t g0 = uint64_t(blockIdx.x) * NT;
-    const uint32_t ci0 = chunk_index(g0);
-    TileIn<LenAcc> in0;
-    tile_issue<OffAcc, LenAcc>(chunk(ci0), uint32_t(g0 - chunk(ci0).first_tile), tile_prefix_all, tile_code_all, in0);
-    uint32_t ci1 = ci0;
-    TileIn<LenAcc> in1;
-    const bool two = NT == 2 && g0 + 1 < total_tiles;  // workgroup-uniform
-    if constexpr (NT == 2) {
-        if (two) {
-            ci1 = chunk_index(g0 + 1);
-            tile_issue<OffAcc, LenAcc>(chunk(ci1), uint32_t(g0 + 1 - chunk(ci1).first_tile), tile_prefix_all,
-                                       tile_code_all, in1);
-        }
+        ci = lo;
     }
+    const FsstChunk& ch = EXT ? tab.ext[ci] : tab.c[ci];
+    TileIn<LenAcc> in;
+    tile_issue<OffAcc, LenAcc>(ch, uint32_t(g - ch.first_tile), tile_prefix_all, tile_code_all, in);
     uint64_t sym_v;
     uint32_t sl;
-    symbol_load(chunk(ci0), sym_v, sl);
-    block_prefix(chunk(ci0), in0.tile, block_totals_all, L);
-    symbol_store(chunk(ci0), L, sym_v, sl, err);
-    tile_run<OffAcc, LenAcc>(chunk(ci0), in0, L, err);
-    if constexpr (NT == 2) {
-        if (two) {
-            __syncthreads();  // every LDS read of the first tile is done
-            const bool new_chunk = ci1 != ci0;
-            if (new_chunk) {  // a chunk boundary between the tiles (rare): its own symbol table
-                symbol_load(chunk(ci1), sym_v, sl);
-                symbol_store(chunk(ci1), L, sym_v, sl, err);
-            }
-            if (new_chunk || in1.tile / kScanTiles != in0.tile / kScanTiles)
-                block_prefix(chunk(ci1), in1.tile, block_totals_all, L);
-            tile_run<OffAcc, LenAcc>(chunk(ci1), in1, L, err);
-        }
-    }
+    symbol_load(ch, sym_v, sl);
+    block_prefix(ch, in.tile, block_totals_all, L);
+    symbol_store(ch, L, sym_v, sl, err);
+    tile_run<OffAcc, LenAcc>(ch, in, L, err);
 }
 
 uint64_t fsst_scratch_bytes(uint64_t n) {
@@ -898,12 +870,6 @@ bool with_acc(int kind, F&& f) {
 }
 
 }  // namespace
-
-// Tiles per decode workgroup (VXG_FSST_TILES = 1 or 2, read at every launch; A/B).
-static int fsst_tiles_per_wg() {
-    const char* e = std::getenv("VXG_FSST_TILES");
-    return e && e[0] == '1' ? 1 : 2;
-}
 
 vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint32_t* err, hipStream_t s,
                              DevTables* dt) {
@@ -981,12 +947,8 @@ vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint
                         if (std::get<2>(key) < 0)
                             hipLaunchKernelGGL((fsst_tile_scan<LA, X>), dim3(unsigned(scans)), dim3(kTile), 0, s, tab,
                                                tp, bt, tc);
-                        if (fsst_tiles_per_wg() == 2)
-                            hipLaunchKernelGGL((fsst_decode<OA, LA, X, 2>), dim3(unsigned((tiles + 1) / 2)), dim3(kTile), 0,
-                                               s, tab, tiles, tp, bt, tc, err, wg_chunk);
-                        else
-                            hipLaunchKernelGGL((fsst_decode<OA, LA, X, 1>), dim3(unsigned(tiles)), dim3(kTile), 0, s, tab,
-                                               tiles, tp, bt, tc, err, wg_chunk);
+                        hipLaunchKernelGGL((fsst_decode<OA, LA, X>), dim3(unsigned(tiles)), dim3(kTile), 0, s, tab, tp,
+                                           bt, tc, err, wg_chunk);
                     };
                     if (tab.ext) go(std::true_type{});
                     else go(std::false_type{});
