@@ -1,0 +1,29 @@
+#!/bin/bash
+# K1g VarBin-dictionary bytes staged in LDS (one round trip with the offsets) + FSST views NT
+# again: parity subset, C4/C5 twice, C5 per column (rotated).
+set -o pipefail
+ROOTDIR="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+cd "$ROOTDIR"
+O="$ROOTDIR/gpurun_out"; mkdir -p "$O"
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+TAG="${1:-r04}"
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q -k "fsst or FSST or string or dict or Dict or plan or file or lineitem or varbin or VarBin or arrow or kat" --timeout 300 --timeout-method thread -p no:cacheprovider > "$O/pytest_$TAG.log" 2>&1
+rc=$?; echo "pytest exit $rc"; tail -3 "$O/pytest_$TAG.log"
+[ $rc -eq 0 ] || exit 3
+for i in 1 2; do
+  timeout -k 10 300 python -u bench.py --workloads c4,c5 --no-cpu-baseline > "$O/b${i}_$TAG.json" 2> "$O/b${i}_$TAG.err" || exit 4
+done
+python - "$O" "$TAG" <<'PY'
+import json, sys, glob
+o, tag = sys.argv[1], sys.argv[2]
+for f in sorted(glob.glob(f"{o}/b[12]_{tag}.json")):
+    d = json.loads(open(f).read().strip().splitlines()[-1])
+    print(f.split('/')[-1], {k: (v['kernel_ms_mean'], v['hbm_frac_algorithmic'], v['verified']) for k, v in d['encodings'].items()})
+PY
+timeout -k 10 300 python tools/c5_columns.py --reps 10 --rotate 4 > "$O/c5_columns_$TAG.jsonl" 2> "$O/c5_columns_$TAG.err" || exit 5
+python - "$O/c5_columns_$TAG.jsonl" <<'PY'
+import json, sys
+for l in open(sys.argv[1]):
+    d = json.loads(l); print(d['column'], d.get('plan_ms'), d.get('plan_hbm_frac'))
+PY
+echo "vbh done"

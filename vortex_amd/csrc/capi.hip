@@ -255,7 +255,7 @@ vxg_status launch_k1_jobs(std::vector<K1Job>& jobs, uint32_t* err, hipStream_t s
             groups += (jb.d.n_blocks + g.bpw - 1) / g.bpw;
             packed_bytes = std::max(packed_bytes, g.bpw * 128u * uint32_t(jb.W));
             if (jb.vb) {
-                dict_bytes = std::max(dict_bytes, uint32_t(16 * jb.d.dict_len));
+                dict_bytes = std::max(dict_bytes, gen_vb_stage_bytes(jb.d.dict_len, jb.vbc.bytes));
                 g.vb_src = jb.vbc.src;
                 g.vb_offs = jb.vbc.offsets;
                 g.vb_offs_width = jb.vbc.offs_width;
@@ -2046,14 +2046,28 @@ static uint32_t plan_branches_env() {
 // whose replays are faster (3 interleaved timed replays each after one warm-up).  The knob
 // VXG_PLAN_BATCH (read at every create) is a diagnostic: "0" unbatched, "1" batched, "mixed"
 // (arrays whose output is <= VXG_PLAN_BATCH_MAX_BYTES batched, the others not), unset = measured.
-enum class BatchMode { Auto, Off, On, Mixed };
+// "s" batches only the string-dictionary columns (one K1g launch for all of them on a branch
+// of its own, the other columns unbatched).
+enum class BatchMode { Auto, Off, On, Mixed, Strings };
 static BatchMode plan_batch_mode() {
     const char* e = std::getenv("VXG_PLAN_BATCH");
     if (!e || !*e) return BatchMode::Auto;
     if (e[0] == '0') return BatchMode::Off;
     if (e[0] == '1') return BatchMode::On;
     if (e[0] == 'm') return BatchMode::Mixed;
+    if (e[0] == 's') return BatchMode::Strings;
     return BatchMode::Auto;
+}
+// A string column whose leading encoding is Dict (C5's four Dict(VarBin) columns).
+static bool dict_string_column(const vxg_array& a) {
+    const bool str = a.dtype == VXG_DTYPE_UTF8 || a.dtype == VXG_DTYPE_BINARY;
+    if (!str) return false;
+    if (a.encoding == VXG_ENC_CHUNKED) {
+        for (uint32_t i = 1; i < a.n_children; i++)
+            if (a.children[i].encoding != VXG_ENC_DICT) return false;
+        return a.n_children > 1;
+    }
+    return a.encoding == VXG_ENC_DICT;
 }
 static uint64_t env_bytes(const char* name, uint64_t dflt) {
     const char* e = std::getenv(name);
@@ -2194,7 +2208,7 @@ static vxg_status record_plan(vxg_ctx* ctx, const vxg_array* arrays, vxg_canonic
         for (uint32_t k = 0; k < n && st == VXG_OK; k++) {
             const uint32_t i = order[k];
             const uint32_t b = uint32_t(std::min_element(load.begin(), load.end()) - load.begin());
-            load[b] += cost[i];
+            if (!(own && batched[i])) load[b] += cost[i];  // (a batched array's launches run on the batch branch)
             Planner p(ctx, br[b], &pl->store, batched[i] ? &batch : nullptr);
             st = p.canonical(arrays[i], outs[i]);
         }
@@ -2292,6 +2306,12 @@ vxg_status vxg_plan_create_ex(vxg_ctx* ctx, const vxg_array* arrays, vxg_canonic
     case BatchMode::Off: cand.emplace_back(none, env_br ? env_br : 2u); break;
     case BatchMode::On: cand.emplace_back(all, env_br ? env_br : 1u); break;
     case BatchMode::Mixed: cand.emplace_back(mixed, env_br ? env_br : 2u); break;
+    case BatchMode::Strings: {
+        std::vector<bool> strs(n);
+        for (uint32_t i = 0; i < n; i++) strs[i] = dict_string_column(arrays[i]);
+        cand.emplace_back(strs, env_br ? env_br : 2u);
+        break;
+    }
     case BatchMode::Auto:
         if (measure) {
             cand.emplace_back(none, env_br ? env_br : 2u);

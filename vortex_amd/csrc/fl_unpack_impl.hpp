@@ -90,6 +90,14 @@ __device__ __forceinline__ Vec16<T> load16(const uint8_t* p) {
     __builtin_memcpy(v.w, &q, 16);
     return v;
 }
+// load16 from global memory through a pointer the compiler cannot place (read from a table)
+template <int T>
+__device__ __forceinline__ Vec16<T> load16_global(const uint8_t* p) {
+    Vec16<T> v;
+    const uint4 q = gload(reinterpret_cast<const uint4*>(p));
+    __builtin_memcpy(v.w, &q, 16);
+    return v;
+}
 
 
 // Extract row R of W-bit values from the register-resident word rows (SWAR over lanes).
@@ -128,6 +136,7 @@ struct EpiParams {
     const void* dict;
     uint64_t dict_len;
     uint32_t* err;
+    bool dict_lds = false;  // dict points into LDS (a staged dictionary), else global memory
 };
 
 inline EpiParams to_epi(const UnpackArgs& a) {
@@ -178,7 +187,8 @@ __device__ __forceinline__ typename EpiOut<T, EPI, VW>::type apply_epi(typename 
         const uint64_t c = uint64_t(e);
         const bool bad = c >= ep.dict_len;
         oob |= bad;
-        return static_cast<const VT*>(ep.dict)[bad ? 0 : c];
+        const VT* p = static_cast<const VT*>(ep.dict) + (bad ? 0 : c);
+        return ep.dict_lds ? lds_load(p) : gload(p);
     }
 }
 
@@ -234,29 +244,24 @@ constexpr int kOutNT = 1;
 // Store N bytes (compile-time) from a register array using the widest aligned stores.
 // NT = 1: non-temporal (streaming) 16-byte stores for the decoded output.
 template <int NBYTES, int NT = 0>
-__device__ __forceinline__ void store_bytes(uint8_t* dst, const void* src) {
+__device__ __forceinline__ void store_bytes(uint8_t* dst, const void* src) {  // dst: global memory
+    using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
     if constexpr (NBYTES >= 16) {
 #pragma unroll
         for (int i = 0; i < NBYTES / 16; i++) {
-            uint4 q;
-            __builtin_memcpy(&q, static_cast<const uint8_t*>(src) + 16 * i, 16);
-            if constexpr (NT) {
-                using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
-                u32x4 vv;
-                __builtin_memcpy(&vv, &q, 16);
-                __builtin_nontemporal_store(vv, reinterpret_cast<u32x4*>(dst) + i);
-            } else {
-                reinterpret_cast<uint4*>(dst)[i] = q;
-            }
+            u32x4 vv;
+            __builtin_memcpy(&vv, static_cast<const uint8_t*>(src) + 16 * i, 16);
+            if constexpr (NT) __builtin_nontemporal_store(vv, (gptr<u32x4>)dst + i);
+            else ((gptr<u32x4>)dst)[i] = vv;
         }
     } else if constexpr (NBYTES == 8) {
-        uint2 q; __builtin_memcpy(&q, src, 8); *reinterpret_cast<uint2*>(dst) = q;
+        uint64_t q; __builtin_memcpy(&q, src, 8); *(gptr<uint64_t>)dst = q;
     } else if constexpr (NBYTES == 4) {
-        uint32_t q; __builtin_memcpy(&q, src, 4); *reinterpret_cast<uint32_t*>(dst) = q;
+        uint32_t q; __builtin_memcpy(&q, src, 4); *(gptr<uint32_t>)dst = q;
     } else if constexpr (NBYTES == 2) {
-        uint16_t q; __builtin_memcpy(&q, src, 2); *reinterpret_cast<uint16_t*>(dst) = q;
+        uint16_t q; __builtin_memcpy(&q, src, 2); *(gptr<uint16_t>)dst = q;
     } else {
-        *dst = *static_cast<const uint8_t*>(src);
+        *(gptr<uint8_t>)dst = *static_cast<const uint8_t*>(src);
     }
 }
 
@@ -285,7 +290,7 @@ __device__ __forceinline__ void process_row(const Vec16<T>* p, int lane0,
 #pragma unroll
         for (int j = 0; j < EPV; j++) {
             const int64_t o = out_base + idx + j;
-            if (o >= 0 && uint64_t(o) < len) out[o] = apply_epi<T, EPI, VW>(v.elem(j), ep, oob);
+            if (o >= 0 && uint64_t(o) < len) gstore(out + o, apply_epi<T, EPI, VW>(v.elem(j), ep, oob));
         }
     }
 }
@@ -402,6 +407,7 @@ __device__ __forceinline__ void unpack_chunk(const ChunkDev& c, uint64_t g, uint
         __shared__ __attribute__((aligned(16))) uint8_t s_dict[kDictLdsBytes];
         stage_dict<VW>(s_dict, c.dict, c.dict_len);
         ep.dict = s_dict;
+        ep.dict_lds = true;
     }
     if (blk >= c.n_blocks) return;
     const int64_t out_base = int64_t(blk * 1024) - int64_t(c.offset);
@@ -517,7 +523,7 @@ __device__ __forceinline__ void kw_block(const uint8_t* pk, int gq, int t, typen
 #pragma unroll
             for (int j = 0; j < EPV; j++) {
                 const int64_t o = out_base + idx + j;
-                if (o >= 0 && uint64_t(o) < len) out[o] = apply_epi<T, EPI, VW>(v.elem(j), ep, oob);
+                if (o >= 0 && uint64_t(o) < len) gstore(out + o, apply_epi<T, EPI, VW>(v.elem(j), ep, oob));
             }
         }
     }
@@ -573,6 +579,7 @@ __device__ __forceinline__ void unpack_chunk_w(const ChunkDev& c, uint64_t g, ui
         uint8_t* const s_dict = k1w_lds + kw_packed_lds<W, LDSD>();
         stage_dict<VW>(s_dict, c.dict, c.dict_len);
         ep.dict = s_dict;
+        ep.dict_lds = true;
     }
     const uint64_t blk0 = (g - c.first_group) * BPW;
     const int nb = c.n_blocks - blk0 < uint64_t(BPW) ? int(c.n_blocks - blk0) : BPW;
@@ -616,7 +623,7 @@ __device__ __forceinline__ void unpack_chunk_w(const ChunkDev& c, uint64_t g, ui
         // non-temporal: every packed byte is read once (a copy with this shape: 55.1 -> 53.0 us,
         // profiles/r03_ubench_k1.txt)
         using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
-        const u32x4* src = reinterpret_cast<const u32x4*>(c.packed + blk0 * (128 * W));
+        const gptr<const u32x4> src = (gptr<const u32x4>)(c.packed + blk0 * (128 * W));
 #if VXG_K1W_BURST
         // A/B variant (VXG_K1W_BURST=1 build): a full workgroup issues all PQ of its thread's
         // loads before any LDS write (PQ * 4 VGPRs; the default loop keeps one load in flight)
@@ -686,7 +693,7 @@ __device__ __forceinline__ void unpack_chunk_w(const ChunkDev& c, uint64_t g, ui
         __builtin_amdgcn_s_waitcnt(0);
         __syncthreads();
         if (s_pscr[0] && s_pscr[1]) {
-            if (pin) out[pkey] = pval;
+            if (pin) gstore(out + pkey, pval);
         } else {
             const uint64_t ps = patch_lower_bound(pc, olo, s_pscr + 4);
             const uint64_t pe = patch_lower_bound(pc, ohi, s_pscr + 4);
@@ -695,7 +702,7 @@ __device__ __forceinline__ void unpack_chunk_w(const ChunkDev& c, uint64_t g, ui
             bool bad = false;
             for (uint64_t i = ps + threadIdx.x; i < pe; i += 256) {
                 const uint64_t key = uint64_t(intcol_get(pc.idx, i)) - pc.idx_off;
-                if (key >= olo && key < ohi) out[key] = static_cast<const O*>(pc.vals)[i];
+                if (key >= olo && key < ohi) gstore(out + key, gload(static_cast<const O*>(pc.vals) + i));
                 else bad = true;
             }
             if (bad) __hip_atomic_fetch_or(err, kErrPatchOrder, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

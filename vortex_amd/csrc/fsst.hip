@@ -326,7 +326,7 @@ __global__ __launch_bounds__(kTile) void fsst_tile_scan_fl32(FsstTable tab, int6
             Vec16<32> p[W > 0 ? W : 1];
             if constexpr (W > 0) {
 #pragma unroll
-                for (int w = 0; w < W; w++) p[w] = load16<32>(packed + blk * (128 * W) + 128 * w + 16 * t);
+                for (int w = 0; w < W; w++) p[w] = load16_global<32>(packed + blk * (128 * W) + 128 * w + 16 * t);
             }
             fl32_tile_rows<W>(p, t, blk * 1024, n, shift, reference, sgn, acc, std::make_integer_sequence<int, 32>{});
         }
@@ -581,7 +581,7 @@ __device__ __forceinline__ void tile_issue(const FsstChunk& ch, uint32_t tile, c
     const bool live = first + uint64_t(tid) < n;
     const uint32_t kc = live ? uint32_t(tid) : uint32_t(n - 1 - first);  // clamped index in the tile
     in.tl.issue(lens, first, kc);
-    in.vbyte = ch.validity ? ch.validity[(first + kc) >> 3] : uint8_t(0xFF);
+    in.vbyte = ch.validity ? gload(ch.validity + ((first + kc) >> 3)) : uint8_t(0xFF);
     const int cshift = int((reinterpret_cast<uintptr_t>(ch.codes) + uintptr_t(in.cf)) & 15);
     const int64_t span64 = in.cl - in.cf;
     const int span = span64 >= 0 && span64 <= kCodeLds ? int(span64) : 0;
@@ -604,8 +604,8 @@ __device__ __forceinline__ void symbol_load(const FsstChunk& ch, uint64_t& sym_v
     sl = 0;
     if (ch.n_symbols) {  // (an empty table -- e.g. trained on null strings only -- may have null buffers)
         const uint32_t sk = uint32_t(threadIdx.x) < ch.n_symbols ? uint32_t(threadIdx.x) : 0u;
-        sym_v = ch.symbols[sk];
-        sl = ch.sym_lens[sk];
+        sym_v = gload(ch.symbols + sk);
+        sl = gload(ch.sym_lens + sk);
     }
 }
 __device__ __forceinline__ void symbol_store(const FsstChunk& ch, const DecLds& L, uint64_t sym_v, uint32_t sl,
@@ -700,9 +700,9 @@ __device__ __forceinline__ void tile_run(const FsstChunk& ch, const TileIn<LenAc
         const int ttot = int(tile_total);
         if (tid < nchunk) *reinterpret_cast<uint4*>(s_codes + 16 * tid) = funnel16(in.cx, in.cy, cshift);
         for (int q = tid + kTile; q < nchunk; q += kTile) {  // tiles of > 4 KiB of codes
-            const uint4 x = a0[q];
+            const uint4 x = gload(a0 + q);
             uint4 y = make_uint4(0, 0, 0, 0);
-            if (cshift != 0 && 16 * (q + 1) - cshift < span) y = a0[q + 1];
+            if (cshift != 0 && 16 * (q + 1) - cshift < span) y = gload(a0 + q + 1);
             *reinterpret_cast<uint4*>(s_codes + 16 * q) = funnel16(x, y, cshift);
         }
         const int nz = (hshift + ttot + 16 + 15) >> 4;
@@ -733,7 +733,7 @@ __device__ __forceinline__ void tile_run(const FsstChunk& ch, const TileIn<LenAc
             if (tid < 32) {
                 const int a = tid < 16 ? tid : 16 * qb + (tid - 16);
                 const bool inr = tid < 16 ? (a >= hshift && a < min(16 * qa, end)) : (a >= max(16 * qb, 16 * qa) && a < end);
-                if (inr) gbase[a] = s_heap[a];
+                if (inr) gstore(gbase + a, s_heap[a]);
             }
         }
         if (live && !(abl & 4)) {
@@ -752,16 +752,16 @@ __device__ __forceinline__ void tile_run(const FsstChunk& ch, const TileIn<LenAc
         int64_t o = tile_out0 + my_rel;
         const int64_t o_start = o, o_end = o + my_len;
         for (int64_t k = my_c0; k < my_c1; k++) {
-            const uint8_t c = codes[k];
+            const uint8_t c = gload(codes + k);
             if (c == 255) {
                 ++k;
-                if (o < o_end) heap[o] = codes[k];
+                if (o < o_end) gstore(heap + o, gload(codes + k));
                 o++;
             } else {
                 const uint64_t sym = L.s_sym[c];
                 const int Ln = L.s_len[c];
                 for (int b = 0; b < Ln; b++)
-                    if (o + b < o_end) heap[o + b] = uint8_t(sym >> (8 * b));
+                    if (o + b < o_end) gstore(heap + o + b, uint8_t(sym >> (8 * b)));
                 o += Ln;
             }
         }
@@ -770,9 +770,11 @@ __device__ __forceinline__ void tile_run(const FsstChunk& ch, const TileIn<LenAc
             const bool valid = (vbyte >> (i & 7)) & 1;
             const uint32_t vlen = valid ? uint32_t(my_len) : 0u;
             const uint8_t* hp = heap + o_start;
-            views[i] = valid ? build_view(vlen, uint32_t(o_start), bidx,
-                                          [&](int b) { return uint32_t(b) < vlen ? hp[b] : uint8_t(0); })
-                             : make_uint4(0, 0, 0, 0);
+            // (non-temporal like the staged path's view store: the compiler merges the two stores
+            // after the branch and keeps the hint only if both carry it)
+            nt_store(views + i, valid ? build_view(vlen, uint32_t(o_start), bidx,
+                                                   [&](int b) { return uint32_t(b) < vlen ? gload(hp + b) : uint8_t(0); })
+                                      : make_uint4(0, 0, 0, 0));
         }
     }
 }

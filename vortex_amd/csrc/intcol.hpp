@@ -11,12 +11,14 @@ namespace vxg {
 
 // Integer load with compile-time width/signedness.  (A runtime width switch compiles to a
 // branch nest that waits vmcnt(0) after every load.)
+// (Column pointers address global memory; they are often read from a device table, where the
+// compiler would otherwise emit flat loads: gload.)
 template <int WIDTH, bool SGN>
 __device__ __forceinline__ int64_t ld(const void* p, uint64_t i) {
-    if constexpr (WIDTH == 1) return SGN ? int64_t(static_cast<const int8_t*>(p)[i]) : int64_t(static_cast<const uint8_t*>(p)[i]);
-    else if constexpr (WIDTH == 2) return SGN ? int64_t(static_cast<const int16_t*>(p)[i]) : int64_t(static_cast<const uint16_t*>(p)[i]);
-    else if constexpr (WIDTH == 4) return SGN ? int64_t(static_cast<const int32_t*>(p)[i]) : int64_t(static_cast<const uint32_t*>(p)[i]);
-    else return static_cast<const int64_t*>(p)[i];
+    if constexpr (WIDTH == 1) return SGN ? int64_t(gload(static_cast<const int8_t*>(p) + i)) : int64_t(gload(static_cast<const uint8_t*>(p) + i));
+    else if constexpr (WIDTH == 2) return SGN ? int64_t(gload(static_cast<const int16_t*>(p) + i)) : int64_t(gload(static_cast<const uint16_t*>(p) + i));
+    else if constexpr (WIDTH == 4) return SGN ? int64_t(gload(static_cast<const int32_t*>(p) + i)) : int64_t(gload(static_cast<const uint32_t*>(p) + i));
+    else return gload(static_cast<const int64_t*>(p) + i);
 }
 
 // Value `idx` (< 1024) of the FastLanes block at `blk` (T-bit words, bit width 0 < W <= T):
@@ -33,7 +35,7 @@ __device__ __forceinline__ std::conditional_t<T == 32, uint32_t, uint64_t> fl_wo
     const uint32_t row = (((fl & 1) << 2) | (fl & 2) | (fl >> 2)) * 8 + s;  // FL_ORDER[fl]*8 + s
     const uint32_t start = __umul24(row, W), word = start / T, sh = start % T;
     const uint32_t word2 = word + 1 < W ? word + 1 : word;
-    const E lo = blk[LANES * word + lane], hi = blk[LANES * word2 + lane];
+    const E lo = gload(blk + LANES * word + lane), hi = gload(blk + LANES * word2 + lane);
     const E mask = W >= uint32_t(T) ? E(~E(0)) : E((E(1) << W) - 1);
     if constexpr (T == 32) {
         return __builtin_amdgcn_alignbit(hi, lo, sh) & mask;

@@ -25,28 +25,68 @@ __device__ __forceinline__ uint32_t fl_order_rt(uint32_t i) { return ((i & 1u) <
 template <typename O>
 __device__ __forceinline__ void gen_store(O* p, const O& v) {
     if constexpr (sizeof(O) >= 4) nt_store(p, v);
-    else *p = v;
+    else gstore(p, v);
 }
 
-__device__ __forceinline__ uint64_t vb_offset(const void* p, uint32_t w, uint64_t i) {
-    switch (w) {  // VarBin offsets are non-negative: signedness does not matter
-    case 1: return static_cast<const uint8_t*>(p)[i];
-    case 2: return static_cast<const uint16_t*>(p)[i];
-    case 4: return static_cast<const uint32_t*>(p)[i];
-    default: return static_cast<const uint64_t*>(p)[i];
-    }
-}
-
-// arrow-array 53.2 make_view (as kernels.hip: len <= 12 inline, else prefix + buffer + offset)
-__device__ __forceinline__ uint4 vb_view(const uint8_t* __restrict__ heap, uint64_t start, uint32_t len, uint32_t bidx) {
-    const uint8_t* p = heap + start;
+// arrow-array 53.2 make_view (as kernels.hip: len <= 12 inline, else prefix + buffer + offset);
+// byte(j) = the dictionary's byte j (global memory or its LDS copy)
+template <class Byte>
+__device__ __forceinline__ uint4 vb_view(Byte byte, uint64_t start, uint32_t len, uint32_t bidx) {
     uint32_t w[3] = {0, 0, 0};
     if (len <= 12) {
-        for (uint32_t j = 0; j < len; j++) w[j >> 2] |= uint32_t(p[j]) << (8 * (j & 3));
+        for (uint32_t j = 0; j < len; j++) w[j >> 2] |= uint32_t(byte(start + j)) << (8 * (j & 3));
         return make_uint4(len, w[0], w[1], w[2]);
     }
-    for (uint32_t j = 0; j < 4; j++) w[0] |= uint32_t(p[j]) << (8 * j);
+    for (uint32_t j = 0; j < 4; j++) w[0] |= uint32_t(byte(start + j)) << (8 * j);
     return make_uint4(len, w[0], bidx, uint32_t(start));
+}
+
+// The views of a VarBin dictionary (<= kGenVarBinDictMax entries) into s_views.  Bytes staged
+// (gen_vb_heap_lds): every thread's offsets (entries tid + 256 k, clamped) and dictionary bytes
+// are requested before any is used -- one memory round trip -- then the bytes go to s_vbh and,
+// after a barrier, the views are built from LDS.  Otherwise the views read the bytes from global
+// memory (a second, dependent round trip).
+template <class Off>
+__device__ __forceinline__ void vb_views(const GenChunk& gc, uint64_t dict_len, uint4* s_views, uint8_t* s_vbh, bool hl,
+                                         uint32_t* err) {
+    constexpr int KO = int(kGenVarBinDictMax / kGenThreads), KB = int(kGenVarBinHeapLds / kGenThreads);
+    const uint32_t tid = threadIdx.x;
+    const Off* const offs = static_cast<const Off*>(gc.vb_offs);
+    uint64_t oa[KO], oe[KO];
+#pragma unroll
+    for (int k = 0; k < KO; k++) {
+        const uint64_t i = tid + uint64_t(kGenThreads) * k, ic = i < dict_len ? i : 0;
+        oa[k] = gload(offs + ic);
+        oe[k] = gload(offs + ic + 1);
+    }
+    auto build = [&](auto byte) {
+#pragma unroll
+        for (int k = 0; k < KO; k++) {
+            const uint64_t i = tid + uint64_t(kGenThreads) * k;
+            if (i >= dict_len) continue;
+            if (oa[k] > oe[k] || oe[k] > gc.vb_bytes) {  // malformed offsets: zero view + error bit
+                __hip_atomic_fetch_or(err, kErrVarBin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                s_views[i] = make_uint4(0, 0, 0, 0);
+            } else {
+                s_views[i] = vb_view(byte, oa[k], uint32_t(oe[k] - oa[k]), gc.vb_bidx);
+            }
+        }
+    };
+    if (hl) {
+        uint8_t hb[KB];
+#pragma unroll
+        for (int k = 0; k < KB; k++) {
+            const uint64_t b = tid + uint64_t(kGenThreads) * k;
+            hb[k] = b < gc.vb_bytes ? gload(gc.vb_src + b) : uint8_t(0);
+        }
+#pragma unroll
+        for (int k = 0; k < KB; k++)
+            if (tid + uint64_t(kGenThreads) * k < gc.vb_bytes) s_vbh[tid + kGenThreads * k] = hb[k];
+        __syncthreads();
+        build([&](uint64_t j) { return s_vbh[j]; });
+    } else {
+        build([&](uint64_t j) { return gload(gc.vb_src + j); });
+    }
 }
 
 template <int T, Epi EPI, int VW, bool VB = false>
@@ -62,7 +102,7 @@ __device__ __forceinline__ void gen_body(const GenChunk& gc, uint64_t g, uint8_t
     E* const s_packed = reinterpret_cast<E*>(lds);
     const uint32_t q16 = nb * 8 * W;
     for (uint32_t q = tid; q < q16; q += kGenThreads)
-        reinterpret_cast<uint4*>(s_packed)[q] = reinterpret_cast<const uint4*>(c.packed + blk0 * (128ull * W))[q];
+        reinterpret_cast<uint4*>(s_packed)[q] = gload(reinterpret_cast<const uint4*>(c.packed + blk0 * (128ull * W)) + q);
     EpiParams ep;
     ep.reference = c.reference;
     ep.shift = c.shift;
@@ -77,27 +117,27 @@ __device__ __forceinline__ void gen_body(const GenChunk& gc, uint64_t g, uint8_t
         const uint64_t ng = (c.n_blocks + gc.bpw - 1) / gc.bpw, lg = g - c.first_group;
         const uint64_t per = (gc.vb_bytes + ng - 1) / ng;
         const uint64_t b1 = (lg + 1) * per < gc.vb_bytes ? (lg + 1) * per : gc.vb_bytes;
-        for (uint64_t b = lg * per + tid; b < b1; b += kGenThreads) gc.vb_dst[b] = gc.vb_src[b];
-        // the dictionary's views, in LDS
+        for (uint64_t b = lg * per + tid; b < b1; b += kGenThreads) gstore(gc.vb_dst + b, gload(gc.vb_src + b));
+        // the dictionary's views, in LDS (offsets width: a uniform switch outside the loads)
         uint4* const s_views = reinterpret_cast<uint4*>(lds + dict_off);
-        for (uint32_t k = tid; k < c.dict_len; k += kGenThreads) {
-            const uint64_t a = vb_offset(gc.vb_offs, gc.vb_offs_width, k);
-            const uint64_t e = vb_offset(gc.vb_offs, gc.vb_offs_width, k + 1);
-            if (a > e || e > gc.vb_bytes) {  // malformed offsets: zero view + error bit
-                __hip_atomic_fetch_or(err, kErrVarBin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                s_views[k] = make_uint4(0, 0, 0, 0);
-            } else {
-                s_views[k] = vb_view(gc.vb_src, a, uint32_t(e - a), gc.vb_bidx);
-            }
+        uint8_t* const s_vbh = lds + dict_off + 16 * c.dict_len;
+        const bool hl = gen_vb_heap_lds(c.dict_len, gc.vb_bytes);
+        switch (gc.vb_offs_width) {  // VarBin offsets are non-negative: signedness does not matter
+        case 1: vb_views<uint8_t>(gc, c.dict_len, s_views, s_vbh, hl, err); break;
+        case 2: vb_views<uint16_t>(gc, c.dict_len, s_views, s_vbh, hl, err); break;
+        case 4: vb_views<uint32_t>(gc, c.dict_len, s_views, s_vbh, hl, err); break;
+        default: vb_views<uint64_t>(gc, c.dict_len, s_views, s_vbh, hl, err); break;
         }
         ep.dict = s_views;
+        ep.dict_lds = true;
     } else if constexpr (EPI == Epi::Dict) {
         if (dict_lds) {
             uint8_t* const s_dict = lds + dict_off;
             const uint32_t n16 = uint32_t((c.dict_len * VW + 15) / 16);
             for (uint32_t q = tid; q < n16; q += kGenThreads)
-                reinterpret_cast<uint4*>(s_dict)[q] = static_cast<const uint4*>(c.dict)[q];
+                reinterpret_cast<uint4*>(s_dict)[q] = gload(static_cast<const uint4*>(c.dict) + q);
             ep.dict = s_dict;
+            ep.dict_lds = true;
         }
     }
     __syncthreads();

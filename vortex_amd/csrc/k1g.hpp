@@ -40,6 +40,17 @@ int gen_kind(int T, int epi, int vw, bool varbin_dict = false);
 int gen_runs_kind(int value_width);
 // Largest VarBin dictionary a K1g job builds in LDS.
 constexpr uint64_t kGenVarBinDictMax = 1024;
+// A VarBin dictionary's bytes, when at most this many and they fit the 16 KiB stage beside its
+// views, are staged in LDS too: loaded in the same round trip as the offsets (a view needs both),
+// instead of a second dependent round of byte loads.
+constexpr uint64_t kGenVarBinHeapLds = 2048;
+__host__ __device__ constexpr bool gen_vb_heap_lds(uint64_t dict_len, uint64_t bytes) {
+    return bytes <= kGenVarBinHeapLds && 16 * dict_len + ((bytes + 15) & ~15ull) <= 16 * 1024;
+}
+// LDS of a Dict-over-VarBin job's dictionary stage: the views (+ the bytes when staged)
+__host__ __device__ constexpr uint32_t gen_vb_stage_bytes(uint64_t dict_len, uint64_t bytes) {
+    return uint32_t(16 * dict_len + (gen_vb_heap_lds(dict_len, bytes) ? ((bytes + 15) & ~15ull) : 0));
+}
 // Blocks per workgroup of a job (its packed words staged in <= 16 KiB of LDS).
 uint32_t gen_bpw(int T, int W);
 // LDS a short-run RunEnd expansion of `value_width`-byte values needs.

@@ -31,10 +31,10 @@ inline unsigned grid_for(uint64_t n_threads) {
 
 __device__ __forceinline__ uint64_t load_uint(const void* p, int width, bool sgn, uint64_t i) {
     switch (width) {
-    case 1: return sgn ? uint64_t(int64_t(static_cast<const int8_t*>(p)[i])) : static_cast<const uint8_t*>(p)[i];
-    case 2: return sgn ? uint64_t(int64_t(static_cast<const int16_t*>(p)[i])) : static_cast<const uint16_t*>(p)[i];
-    case 4: return sgn ? uint64_t(int64_t(static_cast<const int32_t*>(p)[i])) : static_cast<const uint32_t*>(p)[i];
-    default: return static_cast<const uint64_t*>(p)[i];
+    case 1: return sgn ? uint64_t(int64_t(gload(static_cast<const int8_t*>(p) + i))) : gload(static_cast<const uint8_t*>(p) + i);
+    case 2: return sgn ? uint64_t(int64_t(gload(static_cast<const int16_t*>(p) + i))) : gload(static_cast<const uint16_t*>(p) + i);
+    case 4: return sgn ? uint64_t(int64_t(gload(static_cast<const int32_t*>(p) + i))) : gload(static_cast<const uint32_t*>(p) + i);
+    default: return gload(static_cast<const uint64_t*>(p) + i);
     }
 }
 
@@ -653,7 +653,7 @@ __global__ __launch_bounds__(kBlock) void runend_chunks_kernel(RunEndTable tab) 
 #pragma unroll
     for (int k = 0; k < PER; k++) s_head[tid * PER + k] = max(v[k], before);
     __syncthreads();
-    for (int i = tid; i < jn; i += kBlock) nt_store(out + j0 + i, values[r0 + s_head[i]]);
+    for (int i = tid; i < jn; i += kBlock) nt_store(out + j0 + i, gload(values + r0 + s_head[i]));
 }
 
 template <typename V>
@@ -754,14 +754,14 @@ __device__ __forceinline__ uint4 make_view(const uint8_t* __restrict__ heap, uin
     if (len <= 12) {
 #pragma unroll
         for (int j = 0; j < 12; j++) {
-            const uint32_t b = uint32_t(j) < len ? uint32_t(p[j]) : 0u;
+            const uint32_t b = uint32_t(j) < len ? uint32_t(gload(p + j)) : 0u;
             if (j < 4) w1 |= b << (8 * j);
             else if (j < 8) w2 |= b << (8 * (j - 4));
             else w3 |= b << (8 * (j - 8));
         }
     } else {
 #pragma unroll
-        for (int j = 0; j < 4; j++) w1 |= uint32_t(p[j]) << (8 * j);
+        for (int j = 0; j < 4; j++) w1 |= uint32_t(gload(p + j)) << (8 * j);
         w2 = bidx;
         w3 = uint32_t(start);
     }
@@ -820,12 +820,12 @@ __global__ __launch_bounds__(kBlock) void varbin_chunks_kernel(VarBinTable tab) 
     const uint64_t lg = g - c.first_group;
     const uint64_t ng = (c.n + kBlock - 1) / kBlock > 0 ? (c.n + kBlock - 1) / kBlock : 1;
     const uint64_t per = (c.bytes + ng - 1) / ng;
-    for (uint64_t b = lg * per + threadIdx.x; b < c.bytes && b < (lg + 1) * per; b += kBlock) c.dst[b] = c.src[b];
+    for (uint64_t b = lg * per + threadIdx.x; b < c.bytes && b < (lg + 1) * per; b += kBlock) gstore(c.dst + b, gload(c.src + b));
     const uint64_t i = lg * kBlock + threadIdx.x;
     if (i < c.n) {
         const uint64_t a = load_uint(c.offsets, int(c.offs_width), c.offs_width < 8, i);
         const uint64_t e = load_uint(c.offsets, int(c.offs_width), c.offs_width < 8, i + 1);
-        reinterpret_cast<uint4*>(c.views)[i] = checked_view(c.src, c.bytes, a, e, c.bidx, tab.err);
+        gstore(reinterpret_cast<uint4*>(c.views) + i, checked_view(c.src, c.bytes, a, e, c.bidx, tab.err));
     }
 }
 

@@ -26,7 +26,7 @@ __device__ __forceinline__ V runend_value(const IntCol& c, uint64_t r) {
     if constexpr (sizeof(V) == 4 || sizeof(V) == 8) {
         if (c.packed) return V(uint64_t(intcol_get(c, r)));  // low bytes: the value's bits
     }
-    return static_cast<const V*>(c.p)[r];
+    return gload(static_cast<const V*>(c.p) + r);
 }
 
 constexpr int kRunsThreads = 256;
@@ -53,7 +53,7 @@ __device__ __forceinline__ bool runs_blockwise(const IntCol& c, size_t stage_byt
 __device__ __forceinline__ void runs_stage(const IntCol& c, uint64_t blk, uint8_t* s) {
     const uint32_t n16 = 8 * c.W;  // 128 * W bytes
     const uint4* src = reinterpret_cast<const uint4*>(static_cast<const uint8_t*>(c.p) + blk * (128ull * c.W));
-    for (uint32_t q = threadIdx.x; q < n16; q += kRunsThreads) reinterpret_cast<uint4*>(s)[q] = src[q];
+    for (uint32_t q = threadIdx.x; q < n16; q += kRunsThreads) reinterpret_cast<uint4*>(s)[q] = gload(src + q);
 }
 // values 256 k + threadIdx.x (k < 4) of the staged block, FoR applied, as intcol_get returns them
 __device__ __forceinline__ void runs_extract(const IntCol& c, const uint8_t* s, int64_t out[4]) {

@@ -5,6 +5,7 @@
 
 #include <cstdint>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/vortex_gpu.h"
@@ -21,17 +22,62 @@ __host__ __device__ constexpr int fl_index(int row, int lane) {
     return fl_order(row / 8) * 16 + (row % 8) * 128 + lane;
 }
 
-// Non-temporal (streaming) store of one value: decoded outputs are written once and not
-// re-read by the producing launch (uint4 via a native vector type; scalars directly).
+// Address-space-qualified accesses through generic pointers.  A pointer read from memory (a
+// plan's device chunk table, the FSST chunk of a tile) is generic to the compiler, which then
+// emits FLAT instructions for it: those also count against the LDS wait counter (every LDS wait
+// then waits for the outstanding flat loads and stores as well) and take the aperture check.
+// gload / gstore: the pointer addresses global memory (chunk buffers, outputs); lds_load: LDS.
+template <class T>
+using gptr = __attribute__((address_space(1))) T*;
+// (a 16-byte struct such as uint4 moves as a native vector: its copy constructor would bind a
+// generic reference and bring the flat access back)
+template <class T>
+__device__ __forceinline__ T gload(const T* p) {
+    if constexpr (sizeof(T) == 16 && !std::is_scalar_v<T>) {
+        using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
+        const u32x4 x = *(gptr<const u32x4>)p;
+        T r;
+        __builtin_memcpy(&r, &x, 16);
+        return r;
+    } else {
+        return *(gptr<const T>)p;
+    }
+}
+template <class T>
+__device__ __forceinline__ void gstore(T* p, const T& v) {
+    if constexpr (sizeof(T) == 16 && !std::is_scalar_v<T>) {
+        using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
+        u32x4 x;
+        __builtin_memcpy(&x, &v, 16);
+        *(gptr<u32x4>)p = x;
+    } else {
+        *(gptr<T>)p = v;
+    }
+}
+template <class T>
+__device__ __forceinline__ T lds_load(const T* p) {
+    if constexpr (sizeof(T) == 16 && !std::is_scalar_v<T>) {
+        using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
+        const u32x4 x = *(__attribute__((address_space(3))) const u32x4*)p;
+        T r;
+        __builtin_memcpy(&r, &x, 16);
+        return r;
+    } else {
+        return *(__attribute__((address_space(3))) const T*)p;
+    }
+}
+
+// Non-temporal (streaming) store of one value to global memory: decoded outputs are written once
+// and not re-read by the producing launch (uint4 via a native vector type; scalars directly).
 template <typename V>
 __device__ __forceinline__ void nt_store(V* p, const V& v) {
     if constexpr (sizeof(V) == 16) {
         using u32x4 = unsigned int __attribute__((ext_vector_type(4)));
         u32x4 vv;
         __builtin_memcpy(&vv, &v, 16);
-        __builtin_nontemporal_store(vv, reinterpret_cast<u32x4*>(p));
+        __builtin_nontemporal_store(vv, (gptr<u32x4>)p);
     } else {
-        __builtin_nontemporal_store(v, p);
+        __builtin_nontemporal_store(v, (gptr<V>)p);
     }
 }
 
