@@ -1,0 +1,22 @@
+#!/bin/bash
+# Quick C4/C5 check: FSST parity subset, then C4+C5 bench twice.
+set -o pipefail
+ROOTDIR="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+cd "$ROOTDIR"
+O="$ROOTDIR/gpurun_out"; mkdir -p "$O"
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+TAG="${1:-r04}"
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -q -k "fsst or FSST or full_size_c4 or lineitem" --timeout 300 --timeout-method thread -p no:cacheprovider > "$O/pytest_$TAG.log" 2>&1
+rc=$?; echo "pytest exit $rc"; tail -3 "$O/pytest_$TAG.log"
+[ $rc -eq 0 ] || exit 3
+for i in 1 2; do
+  timeout -k 10 300 python -u bench.py --workloads c4,c5 --no-cpu-baseline > "$O/b${i}_$TAG.json" 2> "$O/b${i}_$TAG.err" || exit 4
+done
+python - "$O" "$TAG" <<'PY'
+import json, sys, glob
+o, tag = sys.argv[1], sys.argv[2]
+for f in sorted(glob.glob(f"{o}/b[12]_{tag}.json")):
+    d = json.loads(open(f).read().strip().splitlines()[-1])
+    print(f.split('/')[-1], {k: (v['kernel_ms_mean'], v['hbm_frac_algorithmic'], v['verified']) for k, v in d['encodings'].items()})
+PY
+echo "c45 done"

@@ -507,12 +507,16 @@ __device__ __forceinline__ void fsst_segments(const uint8_t* __restrict__ s_code
         o8 += L8;
     };
     if (fast) {
+        // the next code dword is requested before this dword's ORs: waiting for it then does not
+        // also wait for the ORs (LDS requests complete in order)
+        uint32_t xn = c32[s0 >> 2];
 #pragma unroll
         for (int d = 0; d < ND; d++) {
-            const uint32_t x = c32[(s0 >> 2) + d];
+            const uint32_t x = xn;
             uint64_t sy[4];
 #pragma unroll
             for (int j = 0; j < 4; j++) sy[j] = s_sym[(x >> (8 * j)) & 0xFFu];
+            if (d + 1 < ND) xn = c32[(s0 >> 2) + d + 1];
 #pragma unroll
             for (int j = 0; j < 4; j++) put(sy[j], (pk[d] >> (8 * j)) & 0xFFu);
         }
