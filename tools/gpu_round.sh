@@ -11,7 +11,7 @@ cd "$ROOTDIR"
 O="$ROOTDIR/gpurun_out"; mkdir -p "$O"
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 TAG="${1:-r03}"
-timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > "$O/pytest_gpu_$TAG.log" 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > "$O/pytest_gpu_$TAG.log" 2>&1
 rc=$?; echo "pytest exit $rc"; tail -3 "$O/pytest_gpu_$TAG.log"
 [ $rc -eq 0 ] || exit 3
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke_$TAG.log" 2>&1 && \

@@ -17,14 +17,20 @@ import json
 from pathlib import Path
 
 
-def counters(d: Path, counter: str, substr: str) -> list[float]:
-    vals = []
+def counters(d: Path, counter: str, substr: str, max_grid: bool = False) -> list[float]:
+    """Per-dispatch values of `counter` for kernels matching `substr`; max_grid keeps only the
+    dispatches of the largest grid (the full-size workload, not the smaller launches of other
+    configs -- plan measurements, C5 chunks -- that match the same kernel name)."""
+    rows = []
     for f in sorted(d.rglob("*counter_collection.csv")):
         with f.open() as fh:
             for row in csv.DictReader(fh):
                 if row.get("Counter_Name") == counter and substr in row.get("Kernel_Name", ""):
-                    vals.append(float(row["Counter_Value"]))
-    return vals
+                    rows.append(row)
+    if max_grid and rows:
+        g = max(int(r.get("Grid_Size") or 0) for r in rows)
+        rows = [r for r in rows if int(r.get("Grid_Size") or 0) == g]
+    return [float(r["Counter_Value"]) for r in rows]
 
 
 def main():
@@ -35,9 +41,10 @@ def main():
     ap.add_argument("--name", required=True)
     ap.add_argument("--algorithmic-bytes", type=float, default=None)
     ap.add_argument("--out", default="profiles/pmc_traffic.json")
+    ap.add_argument("--max-grid", action="store_true", help="only the largest-grid dispatches")
     a = ap.parse_args()
-    fetch = counters(Path(a.fetch), "FETCH_SIZE", a.kernel_substr)
-    write = counters(Path(a.write), "WRITE_SIZE", a.kernel_substr)
+    fetch = counters(Path(a.fetch), "FETCH_SIZE", a.kernel_substr, a.max_grid)
+    write = counters(Path(a.write), "WRITE_SIZE", a.kernel_substr, a.max_grid)
     if not fetch or not write:
         raise SystemExit(f"no samples (fetch={len(fetch)}, write={len(write)})")
     f_kib = sum(fetch) / len(fetch)
@@ -46,7 +53,8 @@ def main():
            "FETCH_SIZE_KiB_mean": f_kib, "WRITE_SIZE_KiB_mean": w_kib,
            "read_bytes_corrected": 2 * f_kib * 1024, "write_bytes": w_kib * 1024,
            "hbm_bytes_per_launch": (2 * f_kib + w_kib) * 1024,
-           "correction": "gfx950 FETCH_SIZE x2 (MI355X_MICROARCH.md §HBM); KiB -> bytes"}
+           "correction": "gfx950 FETCH_SIZE x2 (MI355X_MICROARCH.md §HBM); KiB -> bytes",
+           "dispatches": "largest grid only" if a.max_grid else "all matching"}
     if a.algorithmic_bytes:
         rec["algorithmic_bytes"] = a.algorithmic_bytes
         rec["traffic_over_algorithmic"] = rec["hbm_bytes_per_launch"] / a.algorithmic_bytes
