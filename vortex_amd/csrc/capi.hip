@@ -1894,6 +1894,7 @@ vxg_status vxg_open(int device, vxg_ctx** out) {
         if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess)
             (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
     }
+    if (e == hipSuccess) e = fsst_diag_init();  // (a synchronous copy: never inside a plan's capture)
     if (e != hipSuccess) {
         vxg_close(c);
         return hip_check(e, "context setup");

@@ -699,7 +699,8 @@ __device__ __forceinline__ void tile_run(const FsstChunk& ch, const TileIn<LenAc
     if (stage) {
         // (b) stage the tile's code bytes into LDS shifted so that the tile's first code is
         // s_codes[0] (chunk tid was loaded with the prologue; larger tiles load the rest here),
-        // and zero the image
+        // and zero the image.  (Doing this before the length scan, so that one barrier publishes
+        // both, measured the same: profiles/r04_fsst_decode.md.)
         const int hshift = int((reinterpret_cast<uintptr_t>(heap) + tile_out0) & 15);  // image byte hshift = heap[tile_out0]
         const int ttot = int(tile_total);
         if (tid < nchunk) *reinterpret_cast<uint4*>(s_codes + 16 * tid) = funnel16(in.cx, in.cy, cshift);
@@ -877,15 +878,17 @@ bool with_acc(int kind, F&& f) {
 
 }  // namespace
 
+hipError_t fsst_diag_init() {
+    static const hipError_t st = [] {
+        const char* e = std::getenv("VXG_FSST_ABL");
+        const uint32_t m = e ? uint32_t(std::strtoul(e, nullptr, 10)) : 0u;
+        return m ? hipMemcpyToSymbol(HIP_SYMBOL(g_fsst_abl), &m, sizeof m) : hipSuccess;
+    }();
+    return st;
+}
+
 vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint32_t* err, hipStream_t s,
                              DevTables* dt) {
-    static const bool abl_set = [] {
-        const char* e = std::getenv("VXG_FSST_ABL");
-        if (!e) return false;
-        const uint32_t m = uint32_t(std::strtoul(e, nullptr, 10));
-        return hipMemcpyToSymbol(HIP_SYMBOL(g_fsst_abl), &m, sizeof m) == hipSuccess;
-    }();
-    (void)abl_set;
     for (const FsstChunk& c : chunks) {
         if (c.n_symbols > 255) return set_error(VXG_ERR_INVALID_ARGUMENT, "FSST symbol table > 255 entries");
         if ((c.n + kTS - 1) / kTS > 0xFFFFFFFFull) return set_error(VXG_ERR_INVALID_ARGUMENT, "FSST array too long");

@@ -386,6 +386,9 @@ uint64_t fsst_scratch_bytes(uint64_t n);
 uint64_t fsst_batch_scratch_bytes(const FsstChunk* chunks, size_t n_chunks);
 // Decode every chunk: grouped by accessor kinds, kFsstArgChunks per launch pair (pre-pass +
 // decode).  `scratch` >= fsst_batch_scratch_bytes.
+// The FSST decode's diagnostics mask (VXG_FSST_ABL, read once per process) into its __constant__;
+// called by vxg_open.
+hipError_t fsst_diag_init();
 vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint32_t* err, hipStream_t s,
                              DevTables* dt = nullptr);
 // Views carry `bidx` as the buffer_index of non-inlined rows.
