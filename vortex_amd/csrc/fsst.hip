@@ -878,6 +878,17 @@ bool with_acc(int kind, F&& f) {
 
 }  // namespace
 
+// Extra (unused) dynamic LDS per decode workgroup, VXG_FSST_PAD_LDS bytes (diagnostics: the
+// occupancy sensitivity of the decode -- 16 KiB more leaves 4 instead of 8 workgroups per CU).
+static size_t fsst_pad_lds() {
+    static const size_t v = [] {
+        const char* e = std::getenv("VXG_FSST_PAD_LDS");
+        const long x = e ? std::strtol(e, nullptr, 10) : 0;
+        return size_t(x > 0 && x <= 65536 ? x : 0);
+    }();
+    return v;
+}
+
 hipError_t fsst_diag_init() {
     static const hipError_t st = [] {
         const char* e = std::getenv("VXG_FSST_ABL");
@@ -956,8 +967,8 @@ vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint
                         if (std::get<2>(key) < 0)
                             hipLaunchKernelGGL((fsst_tile_scan<LA, X>), dim3(unsigned(scans)), dim3(kTile), 0, s, tab,
                                                tp, bt, tc);
-                        hipLaunchKernelGGL((fsst_decode<OA, LA, X>), dim3(unsigned(tiles)), dim3(kTile), 0, s, tab, tp,
-                                           bt, tc, err, wg_chunk);
+                        hipLaunchKernelGGL((fsst_decode<OA, LA, X>), dim3(unsigned(tiles)), dim3(kTile), fsst_pad_lds(), s,
+                                           tab, tp, bt, tc, err, wg_chunk);
                     };
                     if (tab.ext) go(std::true_type{});
                     else go(std::false_type{});
