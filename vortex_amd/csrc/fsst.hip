@@ -568,19 +568,22 @@ struct TileIn {
 };
 
 template <class OffAcc, class LenAcc>
-__device__ __forceinline__ void tile_issue(const FsstChunk& ch, uint32_t tile, const int64_t* __restrict__ tile_prefix_all,
+__device__ __forceinline__ void tile_issue(const FsstChunk& ch, uint64_t g, const int64_t* __restrict__ tile_prefix_all,
                                            const int64_t* __restrict__ tile_code_all, TileIn<LenAcc>& in) {
     const int tid = threadIdx.x;
     const OffAcc code_offs(ch.offs);
     const LenAcc lens(ch.lens);
     const uint64_t n = ch.n;
+    const uint32_t tile = uint32_t(g - ch.first_tile);  // within the chunk
     in.tile = tile;
     // the tile's code range [cf, cl) (absolute offsets into `codes`) comes from the pre-pass
-    // records, so the code bytes are requested in the same round trip as the other loads
-    const int64_t* __restrict__ tile_code = tile_code_all + ch.first_tile;
-    in.tp = tile_prefix_all[ch.first_tile + tile];
-    in.cl = tile_code[tile];
-    in.cf = tile > 0 ? tile_code[tile - 1] : code_offs(0);
+    // records, so the code bytes are requested in the same round trip as the other loads.  The
+    // records are indexed by the launch-global tile g (= first_tile + tile): their loads do not
+    // wait for the chunk's fields
+    in.tp = tile_prefix_all[g];
+    in.cl = tile_code_all[g];
+    const int64_t prev = tile_code_all[g > 0 ? g - 1 : 0];
+    in.cf = tile > 0 ? prev : code_offs(0);
     const uint64_t first = uint64_t(tile) * kTile;
     const bool live = first + uint64_t(tid) < n;
     const uint32_t kc = live ? uint32_t(tid) : uint32_t(n - 1 - first);  // clamped index in the tile
@@ -805,9 +808,11 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     const DecLds L{s_sym, s_len, ws_a, ws_b, ws_bad, ws_esc, ws64, &s_block_prefix, s_codes, s_heap32};
 
     // the tile's chunk: a recorded plan's device table through the plan's per-tile map (one
-    // scalar load), else the workgroup-uniform search of the kernel-argument table (a chunk
-    // INDEX, not a pointer: a pointer into the kernel-argument table would force the table into
-    // scratch)
+    // scalar load; the chunk's entry is then shared by its ~255 tiles' workgroups in the scalar
+    // cache -- a per-tile copy of the entry, which saves that dependent load but always misses,
+    // measured 1-2 % slower on C5: profiles/r04_fsst_decode.md), else the workgroup-uniform
+    // search of the kernel-argument table (a chunk INDEX, not a pointer: a pointer into the
+    // kernel-argument table would force the table into scratch)
     const uint64_t g = blockIdx.x;
     uint32_t ci;
     if constexpr (EXT) {
@@ -822,7 +827,7 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     }
     const FsstChunk& ch = EXT ? tab.ext[ci] : tab.c[ci];
     TileIn<LenAcc> in;
-    tile_issue<OffAcc, LenAcc>(ch, uint32_t(g - ch.first_tile), tile_prefix_all, tile_code_all, in);
+    tile_issue<OffAcc, LenAcc>(ch, g, tile_prefix_all, tile_code_all, in);
     uint64_t sym_v;
     uint32_t sl;
     symbol_load(ch, sym_v, sl);
