@@ -1,15 +1,15 @@
 #!/bin/bash
 # Same-box A/B of two builds of the library: the in-tree libvortex_gpu.so (new) against
-# VXG_GPU_LIB=$2 (old); C4+C5 alternating, 3 runs each.
+# VXG_GPU_LIB=$2 (old); workloads $3 (default c4,c5) alternating, 3 runs each.
 set -o pipefail
 ROOTDIR="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$ROOTDIR"
 O="$ROOTDIR/gpurun_out"; mkdir -p "$O"
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-TAG="${1:-r04}"; OLD="$2"
+TAG="${1:-r04}"; OLD="$2"; WL="${3:-c4,c5}"
 for i in 1 2 3; do
-  timeout -k 10 300 python -u bench.py --workloads c4,c5 --no-cpu-baseline > "$O/new_${i}_$TAG.json" 2> "$O/new_${i}_$TAG.err" || exit 4
-  VXG_GPU_LIB="$ROOTDIR/$OLD" timeout -k 10 300 python -u bench.py --workloads c4,c5 --no-cpu-baseline > "$O/old_${i}_$TAG.json" 2> "$O/old_${i}_$TAG.err" || exit 5
+  timeout -k 10 300 python -u bench.py --workloads "$WL" --no-cpu-baseline > "$O/new_${i}_$TAG.json" 2> "$O/new_${i}_$TAG.err" || exit 4
+  VXG_GPU_LIB="$ROOTDIR/$OLD" timeout -k 10 300 python -u bench.py --workloads "$WL" --no-cpu-baseline > "$O/old_${i}_$TAG.json" 2> "$O/old_${i}_$TAG.err" || exit 5
 done
 python - "$O" "$TAG" <<'PY'
 import json, sys, glob

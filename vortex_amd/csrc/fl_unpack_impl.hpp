@@ -238,8 +238,12 @@ struct RtRows {
     }
 };
 
-// Output store policy of the K1 launches (1 = non-temporal streaming stores).
-constexpr int kOutNT = 1;
+// Output store policy of the K1 launches (1 = non-temporal streaming stores; a
+// -DVXG_OUT_NT=0 build is the A/B variant with plain stores).
+#ifndef VXG_OUT_NT
+#define VXG_OUT_NT 1
+#endif
+constexpr int kOutNT = VXG_OUT_NT;
 
 // Store N bytes (compile-time) from a register array using the widest aligned stores.
 // NT = 1: non-temporal (streaming) 16-byte stores for the decoded output.
