@@ -23,7 +23,8 @@ Contract:
     this rank's chunk range, read from a Vortex file's bytes) are measured the same way and
     reported under "encodings".
 Inputs are rotated across several HBM copies so every step reads from HBM, not from the
-256 MiB Infinity Cache.
+256 MiB Infinity Cache; every copy decodes into its own outputs (plans and direct calls alike),
+so no step rewrites the buffer the previous one wrote.
 """
 from __future__ import annotations
 
@@ -454,20 +455,25 @@ class Workload:
         if graph:
             self.plans = [A.Plan(trees, ctx, measure=True) for trees in self.copies]
         else:
+            # every rotated copy decodes into its own outputs too: rewriting one output buffer
+            # step after step would let the Infinity Cache absorb part of the writes
             self.keep = []
             self.cols = []
-            self.shared = []
+            self.outs = [[] for _ in range(copies)]
             for j, arr in enumerate(arrs):
                 nodes = [A.flatten(trees[j], self.keep) for trees in self.copies]
-                o, res = A.alloc_canonical(ctx, nodes[0], self.keep)
-                self.cols.append((nodes, o))
-                self.shared.append(res)
+                outs = []
+                for k in range(copies):
+                    o, res = A.alloc_canonical(ctx, nodes[k], self.keep)
+                    outs.append(o)
+                    self.outs[k].append(res)
+                self.cols.append((nodes, outs))
         self.i = 0
         self.input_bytes = sum(a.nbytes() for a in arrs)
 
     def results(self, k: int):
-        """Canonical outputs of copy k (direct calls share one output across copies)."""
-        return self.plans[k].results if self.graph else self.shared
+        """Canonical outputs of copy k."""
+        return self.plans[k].results if self.graph else self.outs[k]
 
     def run_copy(self, k: int):
         self.i = k
@@ -479,9 +485,9 @@ class Workload:
         if self.graph:
             self.plans[k % len(self.plans)].launch()
             return
-        for nodes, out in self.cols:
-            chk(self.ctx.lib.vxg_canonicalize(self.ctx.handle, C.byref(nodes[k % len(nodes)]), C.byref(out),
-                                              self.ctx.stream_ptr()))
+        for nodes, outs in self.cols:
+            chk(self.ctx.lib.vxg_canonicalize(self.ctx.handle, C.byref(nodes[k % len(nodes)]),
+                                              C.byref(outs[k % len(outs)]), self.ctx.stream_ptr()))
 
     def nodes0(self):
         self.keep0 = []
