@@ -281,8 +281,11 @@ vxg_status launch_k1_jobs(std::vector<K1Job>& jobs, uint32_t* err, hipStream_t s
             groups += (r.n_runs + kRunEndRunsPerGroup - 1) / kRunEndRunsPerGroup;
             runs_bytes = std::max(runs_bytes, gen_runs_lds_bytes(w));
         }
+        std::vector<uint64_t> cnt(gen.size() + n_runs);  // workgroups per job (direct job lookup when equal)
+        for (size_t k = 0; k < cnt.size(); k++)
+            cnt[k] = (k + 1 < cnt.size() ? host[k + 1].d.first_group : groups) - host[k].d.first_group;
         VXG_TRY_S(launch_k1_generic(ext, uint32_t(gen.size() + n_runs), groups, dict_lds, packed_bytes, dict_bytes,
-                                    runs_bytes, err, s));
+                                    runs_bytes, err, s, common_groups(cnt.data(), cnt.size())));
     }
     return VXG_OK;
 }

@@ -223,10 +223,11 @@ __device__ __forceinline__ void gen_dispatch(int kind, const GenChunk& gc, uint6
 static_assert(kGenKinds == 43, "gen_dispatch's switch lists every kind");
 
 __global__ __launch_bounds__(kGenThreads) void k1_generic_kernel(const GenChunk* __restrict__ tab, uint32_t n,
-                                                                 uint32_t dict_off, bool dict_lds, uint32_t* err) {
+                                                                 uint32_t dict_off, bool dict_lds, uint32_t* err,
+                                                                 uint64_t gpe) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const uint64_t g = blockIdx.x;
-    const GenChunk& gc = tab[ext_chunk_index(tab, n, g, [](const GenChunk& d) { return d.d.first_group; })];
+    const GenChunk& gc = tab[ext_chunk_index_gpe(tab, n, g, gpe, [](const GenChunk& d) { return d.d.first_group; })];
     gen_dispatch(int(gc.kind), gc, g, lds, dict_off, dict_lds, err);
 }
 
@@ -290,7 +291,8 @@ uint32_t gen_runs_lds_bytes(int value_width) {
 }
 
 vxg_status launch_k1_generic(const GenChunk* ext, uint32_t n, uint64_t groups, bool dict_lds, uint32_t packed_bytes,
-                             uint32_t dict_bytes, uint32_t runs_bytes, uint32_t* err, hipStream_t s) {
+                             uint32_t dict_bytes, uint32_t runs_bytes, uint32_t* err, hipStream_t s,
+                             uint64_t gpe) {
     static_assert(kGenVarBinDictMax * 16 <= uint64_t(kDictLdsBytes), "VarBin views must fit the dictionary stage");
     if (n == 0 || groups == 0) return VXG_OK;
     if (groups > 0xFFFFFFFFull) return set_error(VXG_ERR_INVALID_ARGUMENT, "array too long for one launch");
@@ -301,7 +303,7 @@ vxg_status launch_k1_generic(const GenChunk* ext, uint32_t n, uint64_t groups, b
     const uint32_t dict_off = (packed_bytes + 15) & ~15u;
     const size_t shm = std::max<size_t>({size_t(dict_off) + dict_bytes, size_t(runs_bytes), 16});
     hipLaunchKernelGGL(k1_generic_kernel, dim3(unsigned(groups)), dim3(kGenThreads), shm, s, ext, n, dict_off, dict_lds,
-                       err);
+                       err, gpe);
     return hip_check(hipGetLastError(), "k1_generic_kernel launch");
 }
 

@@ -60,6 +60,7 @@ uint32_t gen_runs_lds_bytes(int value_width);
 // runs_bytes = the largest packed stage (bpw * 128 * W), dictionary stage (staged dictionaries,
 // VarBin views) and RunEnd expansion LDS of the launch's jobs.
 vxg_status launch_k1_generic(const GenChunk* ext, uint32_t n, uint64_t groups, bool dict_lds, uint32_t packed_bytes,
-                             uint32_t dict_bytes, uint32_t runs_bytes, uint32_t* err, hipStream_t s);
+                             uint32_t dict_bytes, uint32_t runs_bytes, uint32_t* err, hipStream_t s,
+                             uint64_t gpe = 0);
 
 }  // namespace vxg

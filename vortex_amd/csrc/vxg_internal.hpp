@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 #include <string>
 #include <type_traits>
 #include <vector>
@@ -165,6 +166,38 @@ __device__ __forceinline__ uint32_t ext_chunk_index(const E* __restrict__ ext, u
         }
     }
     return cnt ? cnt - 1 : 0;
+}
+
+// As ext_chunk_index, when the planner knows that every entry but the last spans `gpe`
+// workgroups (a chunked column's equal chunks; 0 = unknown): entry g / gpe is taken directly and
+// checked against its first workgroup and the next entry's -- both read in the round trip that
+// also brings the entry's other fields -- so the lookup costs no dependent round trip of its own;
+// any mismatch falls back to the wave-wide count.
+template <class E, class Key>
+__device__ __forceinline__ uint32_t ext_chunk_index_gpe(const E* __restrict__ ext, uint32_t n, uint64_t g, uint64_t gpe,
+                                                        Key key) {
+    if (gpe) {
+        // (32-bit: grids and per-entry counts are < 2^32; readfirstlane keeps the index -- computed
+        // on the vector ALU -- visibly uniform, so the entry is read with scalar loads)
+        const uint32_t q = uint32_t(g) / uint32_t(gpe);
+        const uint32_t ci = __builtin_amdgcn_readfirstlane(q < n - 1 ? q : n - 1);
+        const uint64_t f0 = uint64_t(key(ext[ci]));
+        const uint64_t f1 = ci + 1 < n ? uint64_t(key(ext[ci + 1])) : ~0ull;
+        if (f0 <= g && g < f1) return ci;
+    }
+    return ext_chunk_index(ext, n, g, key);
+}
+// Host side: the common workgroup count of a table's entries (all but the last equal, the last
+// not larger), else 0.  VXG_EXT_GPE=0 (read once) disables the direct lookup (A/B).
+inline uint64_t common_groups(const uint64_t* counts, size_t n) {
+    static const bool on = [] {
+        const char* e = std::getenv("VXG_EXT_GPE");
+        return !(e && e[0] == '0');
+    }();
+    if (!on || n == 0 || counts[0] == 0) return 0;
+    for (size_t i = 1; i + 1 < n; i++)
+        if (counts[i] != counts[0]) return 0;
+    return counts[n - 1] <= counts[0] ? counts[0] : 0;
 }
 
 // ---- launchers implemented in the .hip translation units -----------------------------
