@@ -1035,6 +1035,26 @@ def test_plan_k1g_every_kind(ctx):
     plan.close()
 
 
+@pytest.mark.parametrize("sizes", [[8192] * 6 + [5000], [8192] * 5 + [12288], [8192], [8192, 4096, 8192]])
+def test_plan_string_dict_job_lookup(ctx, sizes):
+    """Unbatched plans run each chunked Dict(VarBin) column as one K1g launch whose workgroups
+    find their chunk directly when every chunk but the last spans the same workgroups (last chunk
+    smaller: direct; a larger last chunk, a single chunk or unequal chunks: the fallback count).
+    Every view and byte equals the oracle."""
+    import torch
+    rng = np.random.default_rng(88)
+    words = [b"DELIVER IN PERSON", b"NONE", b"TAKE BACK RETURN", b"COLLECT COD", b"x" * 30]
+    strs = [[words[i] for i in rng.integers(0, len(words), n)] for n in sizes]
+    sarr = A.chunked([E.encode_dict_strings(s) for s in strs])
+    with plan_mode("0"):
+        plan = V.Plan([sarr.to(torch.device("cuda", 0))], ctx)
+    res = plan.launch(sync=True)[0]
+    (rviews, rbufs), _ = canon(sarr)
+    assert res.numpy()[0].tobytes() == rviews.tobytes()
+    assert [b.tobytes() for b in res.buffers()] == [b.tobytes() for b in rbufs]
+    plan.close()
+
+
 def test_plan_mixed_large_and_small_arrays(ctx):
     """A plan with a 21 MB chunked array (22 K1 chunks) next to small columns of every K1g body:
     batched together (K1 launch groups for the large group, one K1g launch for the rest), every
