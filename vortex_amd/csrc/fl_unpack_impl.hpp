@@ -813,9 +813,12 @@ vxg_status launch_one(const ChunkTable& tab, uint64_t groups32, hipStream_t s) {
     }
     // Dict gathers keep the register-resident K1 by default: C3 (u64 codes W=10, 8-byte values,
     // dictionary in LDS) measured 0.65 of 8 TB/s with K1w against 0.70 with the row split
+    // Device-table launches (a plan's chunked columns) take K1w at any size: C5's 48 MB numeric
+    // columns (~183 workgroups of 32 blocks, under the row-split threshold) measured C5 0.52 ->
+    // 0.555 of 8 TB/s with K1w instead of the row split (session r04kw)
     const int mode = k1_wave_mode();
-    const bool wave = mode == 2 || (mode == 1 && !split && EPI != Epi::Dict);  // large launches: K1w
-    if (tab.ext) {  // device table (plans): K1w, or the row split for small T = 32/64 launches
+    const bool wave = mode == 2 || (mode == 1 && (!split || tab.ext) && EPI != Epi::Dict);  // large launches: K1w
+    if (tab.ext) {  // device table (plans): K1w, or the register-resident K1 for Dict gathers
         if (wave) {
             if constexpr (EPI == Epi::Dict) {
                 if (lds) return launch_w<T, W, EPI, VW, true, true>(tab, s);
