@@ -813,11 +813,14 @@ vxg_status launch_one(const ChunkTable& tab, uint64_t groups32, hipStream_t s) {
     }
     // Dict gathers keep the register-resident K1 by default: C3 (u64 codes W=10, 8-byte values,
     // dictionary in LDS) measured 0.65 of 8 TB/s with K1w against 0.70 with the row split
-    // Device-table launches (a plan's chunked columns) take K1w at any size: C5's 48 MB numeric
-    // columns (~183 workgroups of 32 blocks, under the row-split threshold) measured C5 0.52 ->
-    // 0.555 of 8 TB/s with K1w instead of the row split (session r04kw)
+    // Device-table launches (a plan's chunked columns) take K1w from kExtWaveGroups workgroups of
+    // 32 blocks: C5's 48 MB numeric columns (183) measured C5 0.52 -> 0.556 of 8 TB/s with K1w
+    // instead of the row split (sessions r04kw, r04c), but the 2-GPU shard's halves (92) 0.506 ->
+    // 0.429 (too few K1w workgroups for 256 CUs)
+    constexpr uint64_t kExtWaveGroups = 128;
     const int mode = k1_wave_mode();
-    const bool wave = mode == 2 || (mode == 1 && (!split || tab.ext) && EPI != Epi::Dict);  // large launches: K1w
+    const bool big = !split || (tab.ext && groups32 >= kExtWaveGroups);
+    const bool wave = mode == 2 || (mode == 1 && big && EPI != Epi::Dict);  // large launches: K1w
     if (tab.ext) {  // device table (plans): K1w, or the register-resident K1 for Dict gathers
         if (wave) {
             if constexpr (EPI == Epi::Dict) {
