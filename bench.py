@@ -388,6 +388,43 @@ def run_file_e2e(host, ctx, c0: int, c1: int, reps: int = 5) -> dict:
                 e2e_decoded_GBps=round(out_bytes / times[i] / 1e9, 2))
 
 
+def c5_verify(results, chunks):
+    """C5 outputs (the 16 lineitem columns' canonicals, in L.COLUMNS order) of the chunk range
+    `chunks`, column by column against the generator's plain values: numeric columns byte for
+    byte, string columns row by row (logical value of each view), row counts exact, no nulls."""
+    from tools import lineitem as L
+    host_res = []
+    for r in results:
+        if r.kind == "primitive":
+            host_res.append(("p", _host(r.values)))
+        else:
+            host_res.append(("s", _host(r.views).reshape(-1, 16), _host(r.data), r.data_buffers))
+        if r.validity is not None and not _host(r.validity).all():
+            raise AssertionError("C5: unexpected nulls")
+    row = 0
+    for c in chunks:
+        vals = L.chunk_values(c)
+        n = vals["l_orderkey"].size
+        for (name, _), hr in zip(L.COLUMNS, host_res):
+            v = vals[name]
+            if hr[0] == "p":
+                w = v.dtype.itemsize
+                if hr[1][row * w: (row + n) * w].tobytes() != v.tobytes():
+                    raise AssertionError(f"C5 {name}: chunk {c} differs")
+            else:
+                width = max(len(x) for x in v)
+                gl, gs = strings_of(hr[1][row: row + n], hr[2], hr[3], max(width, 1))
+                el, es = plain_strings(v, max(width, 1))
+                if not (np.array_equal(gl, el) and np.array_equal(gs, es)):
+                    raise AssertionError(f"C5 {name}: chunk {c} strings differ")
+        row += n
+    for (name, kind), hr in zip(L.COLUMNS, host_res):
+        n_out = hr[1].size // {"i64": 8, "f64": 8, "i32": 4}[kind] if hr[0] == "p" else hr[1].shape[0]
+        if n_out != row:
+            raise AssertionError(f"C5 {name}: {n_out} rows out, {row} expected")
+    return row
+
+
 def make_c5(rng, world, rank, dist=None):
     """C5: bench-vortex's TPC-H lineitem scan -> canonicalize "via vortex-serde": the table is
     read from a Vortex file's bytes (c5_file) by the engine's reader.  The table is fixed
@@ -398,37 +435,7 @@ def make_c5(rng, world, rank, dist=None):
     host = c5_file(dist, rank)
 
     def check(results):
-        """Column by column against the generator's plain values of this rank's chunks:
-        numeric columns byte for byte, string columns row by row (logical value of each view)."""
-        host_res = []
-        for r in results:
-            if r.kind == "primitive":
-                host_res.append(("p", _host(r.values)))
-            else:
-                host_res.append(("s", _host(r.views).reshape(-1, 16), _host(r.data), r.data_buffers))
-            if r.validity is not None and not _host(r.validity).all():
-                raise AssertionError("C5: unexpected nulls")
-        row = 0
-        for c in mine:
-            vals = L.chunk_values(c)
-            n = vals["l_orderkey"].size
-            for (name, _), hr in zip(L.COLUMNS, host_res):
-                v = vals[name]
-                if hr[0] == "p":
-                    w = v.dtype.itemsize
-                    if hr[1][row * w: (row + n) * w].tobytes() != v.tobytes():
-                        raise AssertionError(f"C5 {name}: chunk {c} differs")
-                else:
-                    width = max(len(x) for x in v)
-                    gl, gs = strings_of(hr[1][row: row + n], hr[2], hr[3], max(width, 1))
-                    el, es = plain_strings(v, max(width, 1))
-                    if not (np.array_equal(gl, el) and np.array_equal(gs, es)):
-                        raise AssertionError(f"C5 {name}: chunk {c} strings differ")
-            row += n
-        for (name, kind), hr in zip(L.COLUMNS, host_res):
-            n_out = hr[1].size // {"i64": 8, "f64": 8, "i32": 4}[kind] if hr[0] == "p" else hr[1].shape[0]
-            if n_out != row:
-                raise AssertionError(f"C5 {name}: {n_out} rows out, {row} expected")
+        c5_verify(results, mine)
 
     return ("file", host, mine.start, mine.stop), dict(expect=check,
         name="C5", encoding="lineitem scan from Vortex file bytes: 16 x vortex.chunked[<per-column cascades>] -> canonical",

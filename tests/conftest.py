@@ -23,3 +23,11 @@ def ctx():
     c = V.Context(0)
     yield c
     c.close()
+
+
+@pytest.fixture(scope="session")
+def lineitem_file_bytes():
+    """BASELINE C5's whole file (92 chunks x 16 columns, bench.c5_file), written once per
+    session and shared by the tests that read it."""
+    import bench
+    return bench.c5_file(None, 0)

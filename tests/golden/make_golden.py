@@ -128,6 +128,41 @@ def kats() -> list[dict]:
     out.append(dict(
         name="delta_u8_overflow", ref="encodings/fastlanes/src/delta/compress.rs:177-184",
         kind="delta", ptype="u8", gen="i % 255", n=10_000, expect="roundtrip"))
+    # Delta slices (delta/compute.rs:162-405).  DeltaArray::try_from_vec keeps the deltas as a
+    # plain PrimitiveArray.  The first slice is SliceFn::slice itself (no bounds check: the
+    # reference's jagged "empty" test slices 4096..4096 of a 4000-row array); later ones go
+    # through compute::slice.  "expect" is [lo, hi) of the u32 range the slice must equal.
+    R = "encodings/fastlanes/src/delta/compute.rs"
+    out.append(dict(
+        name="delta_slices", ref=f"{R}:162-405", kind="delta_slice", ptype="u32",
+        cases=[dict(test="non_jagged_first_chunk_of_two", n=2048, slices=[[10, 250]], expect=[10, 250], line=163),
+               dict(test="non_jagged_second_chunk_of_two", n=2048, slices=[[1034, 1274]], expect=[1034, 1274],
+                    line=177),
+               dict(test="non_jagged_span_two_chunks_chunk_of_two", n=2048, slices=[[1000, 1048]],
+                    expect=[1000, 1048], line=191),
+               dict(test="non_jagged_span_two_chunks_chunk_of_four", n=4096, slices=[[2040, 2050]],
+                    expect=[2040, 2050], line=205),
+               dict(test="non_jagged_whole", n=4096, slices=[[0, 4096]], expect=[0, 4096], line=219),
+               dict(test="non_jagged_empty_0", n=4096, slices=[[0, 0]], expect=[0, 0], line=233),
+               dict(test="non_jagged_empty_4096", n=4096, slices=[[4096, 4096]], expect=[0, 0], line=233),
+               dict(test="non_jagged_empty_1024", n=4096, slices=[[1024, 1024]], expect=[0, 0], line=233),
+               dict(test="jagged_second_chunk_of_two", n=2000, slices=[[1034, 1274]], expect=[1034, 1274],
+                    line=265),
+               dict(test="jagged_empty_0", n=4000, slices=[[0, 0]], expect=[0, 0], line=279),
+               dict(test="jagged_empty_4096", n=4000, slices=[[4096, 4096]], expect=[0, 0], line=279),
+               dict(test="jagged_empty_1024", n=4000, slices=[[1024, 1024]], expect=[0, 0], line=279),
+               dict(test="slice_of_slice_of_non_jagged", n=2048, slices=[[10, 1013], [0, 2]], expect=[10, 12],
+                    line=311),
+               dict(test="slice_of_slice_of_jagged", n=2000, slices=[[10, 1013], [0, 2]], expect=[10, 12],
+                    line=327),
+               dict(test="slice_of_slice_second_chunk_of_non_jagged", n=2048, slices=[[1034, 1050], [0, 2]],
+                    expect=[1034, 1036], line=343),
+               dict(test="slice_of_slice_second_chunk_of_jagged", n=2000, slices=[[1034, 1050], [0, 2]],
+                    expect=[1034, 1036], line=359),
+               dict(test="slice_of_slice_spanning_two_chunks_of_non_jagged", n=2048, slices=[[1010, 1050], [5, 20]],
+                    expect=[1015, 1030], line=375),
+               dict(test="slice_of_slice_spanning_two_chunks_of_jagged", n=2000, slices=[[1010, 1050], [5, 20]],
+                    expect=[1015, 1030], line=391)]))
     # ---- RunEnd ----------------------------------------------------------------------------
     out.append(dict(
         name="runend_encode", ref="encodings/runend/src/compress.rs:159-166",
@@ -137,6 +172,76 @@ def kats() -> list[dict]:
         name="runend_decode", ref="encodings/runend/src/compress.rs:168-178",
         kind="runend_decode", ptype="i32", ends=[2, 5, 10], run_values=[1, 2, 3], offset=0, len=10,
         expect_decoded=[1, 1, 2, 2, 2, 3, 3, 3, 3, 3]))
+    out.append(dict(
+        name="runend_decode_nullable", ref="encodings/runend/src/compress.rs:180-210",
+        kind="runend_nullable", ptype="i32", ends_ptype="u32", ends=[2, 5, 10], run_values=[1, 2, 3],
+        values_validity="ALL_VALID", validity=[True, True, False, True, True, True, True, False, True, True],
+        expect_decoded=[1, 1, 2, 2, 2, 3, 3, 3, 3, 3],
+        expect_validity=[True, True, False, True, True, True, True, False, True, True]))
+    # RunEnd compute (runend/compute.rs:132-353).  ree_array() = RunEndArray::encode of
+    # [1,1,1,4,4,4,2,2,5,5,5,5] (ends [3,6,8,12] u64, values [1,4,2,5]).  A case either slices
+    # ("slices": SliceFn applied in order), takes ("take": compute::take indices), or both; the
+    # expected canonical is "expect" with "expect_validity" where the reference checks it;
+    # "expect_error" names the VortexError the reference raises.
+    R = "encodings/runend/src/compute.rs"
+    REE = dict(values=[1, 1, 1, 4, 4, 4, 2, 2, 5, 5, 5, 5])
+    out.append(dict(
+        name="runend_compute", ref=f"{R}:132-353", kind="runend_compute", ptype="i32",
+        cases=[dict(test="ree_take", line=133, build=REE, take=[9, 8, 1, 3], expect=[5, 5, 1, 4]),
+               dict(test="ree_take_end", line=146, build=REE, take=[11], expect=[5]),
+               dict(test="ree_take_out_of_bounds", line=160, build=REE, take=[12], expect_error="OutOfBounds"),
+               dict(test="ree_scalar_at_end", line=169, build=REE, take=[11], expect=[5]),
+               dict(test="ree_null_scalar", line=175, build=dict(REE, validity="ALL_INVALID"), take=[11], expect=[None]),
+               dict(test="slice_with_nulls", line=188, ends_ptype="u32",
+                    build=dict(ends=[3, 6, 8, 12], run_values=[1, 4, 2, 5], values_validity="ALL_VALID",
+                               validity=[False, False, False, False, True, True, False, False, False, False,
+                                         True, True]),
+                    slices=[[4, 10]], expect=[4, 4, 2, 2, 5, 5],
+                    expect_validity=[True, True, False, False, False, False]),
+               dict(test="slice_array", line=217, ends_ptype="u32",
+                    build=dict(ends=[2, 5, 10], run_values=[1, 2, 3]), slices=[[3, 8]], expect=[2, 2, 3, 3, 3]),
+               dict(test="double_slice", line=243, ends_ptype="u32",
+                    build=dict(ends=[2, 5, 10], run_values=[1, 2, 3]), slices=[[3, 8], [0, 3]], expect=[2, 2, 3]),
+               dict(test="slice_end_inclusive", line=270, ends_ptype="u32",
+                    build=dict(ends=[2, 5, 10], run_values=[1, 2, 3]), slices=[[4, 10]],
+                    expect=[2, 3, 3, 3, 3, 3]),
+               dict(test="decompress", line=296, ends_ptype="u32",
+                    build=dict(ends=[2, 5, 10], run_values=[1, 2, 3]), expect=[1, 1, 2, 2, 2, 3, 3, 3, 3, 3]),
+               dict(test="take_with_nulls", line=311, ends_ptype="u32",
+                    build=dict(ends=[2, 5, 10], run_values=[1, 0, 3], values_validity="ALL_VALID",
+                               validity=[True, True, False, False, False, True, True, True, True, True]),
+                    take=[0, 2, 4, 6], expect=[1, None, None, 3]),
+               dict(test="sliced_take", line=341, build=REE, slices=[[4, 9]], take=[1, 3, 4], expect=[4, 2, 5])]))
+    # ---- Sparse (vortex-array/src/array/sparse) ---------------------------------------------
+    out.append(dict(
+        name="sparse_slices", ref="vortex-array/src/array/sparse/compute/slice.rs:29-70",
+        kind="sparse_slice", ptype="u32", indices=[10, 11, 50, 100], values=[15, 135, 13531, 42], len=101, fill=0,
+        cases=[dict(test="test_slice", line=30, slices=[[15, 100]], expect_len=85, expect_values=[13531],
+                    expect_at=[[35, 13531]]),
+               dict(test="doubly_sliced", line=50, slices=[[15, 100], [35, 36]], expect_len=1,
+                    expect_values=[13531], expect_at=[[0, 13531]])]))
+    # sparse_array(): indices [0,37,47,99] u64, values f64 AllValid, len 100, fill null.  take
+    # returns a SparseArray (positions of the taken patches, their values), len = indices len.
+    out.append(dict(
+        name="sparse_take", ref="vortex-array/src/array/sparse/compute/take.rs:114-200",
+        kind="sparse_take", ptype="f64", indices=[0, 37, 47, 99],
+        values_bits=[f64bits(v) for v in (1.23, 0.47, 9.99, 3.5)], len=100,
+        cases=[dict(test="sparse_take", line=115, take=[0, 47, 47, 0, 99], expect_indices=[0, 1, 2, 3, 4],
+                    expect_values_bits=[f64bits(v) for v in (1.23, 9.99, 9.99, 1.23, 3.5)]),
+               dict(test="nonexistent_take", line=139, take=[69], expect_indices=[], expect_values_bits=[]),
+               dict(test="ordered_take", line=157, take=[69, 37], expect_indices=[1],
+                    expect_values_bits=[f64bits(0.47)], expect_len=2)]))
+    out.append(dict(
+        name="sparse_bool", ref="vortex-array/src/array/sparse/flatten.rs:108-117 (+ :44-66)",
+        kind="sparse_bool", indices=[0], values=[True], len=10, fill=True,
+        # the test asserts Bool dtype / Canonical::Bool; the canonical's bits and validity follow
+        # canonicalize_sparse_bools (:44-66): fill everywhere, validity set exactly at the indices
+        expect=[True] * 10, expect_validity=[True] + [False] * 9))
+    # ---- Chunked ---------------------------------------------------------------------------
+    out.append(dict(
+        name="chunked_pack_sliced_varbin", ref="vortex-array/src/array/chunked/canonical.rs:254-273",
+        kind="pack_sliced_views", strings=["foo", "bar", "baz", "quak"], slices=[[1, 3], [2, 4]],
+        expect=["bar", "baz", "baz", "quak"]))
     # ---- RunEndBool (encodings/runend-bool/src/{compress.rs,array.rs} tests) ----------------
     out.append(dict(
         name="runend_bool_encode", ref="encodings/runend-bool/src/compress.rs:107-129",

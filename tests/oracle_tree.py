@@ -387,11 +387,122 @@ def slice_bitpacked(a: Array, start: int, stop: int) -> Array:
                        validity=None if a.validity == VALIDITY["NON_NULLABLE"] else "ALL_VALID")
 
 
+def _slice_validity(a: Array, start: int, stop: int):
+    """Validity::slice (validity.rs): the metadata kinds stay, an Array child is sliced."""
+    if a.validity == VALIDITY["NON_NULLABLE"]:
+        return None
+    if a.validity == VALIDITY["ALL_VALID"]:
+        return "ALL_VALID"
+    if a.validity == VALIDITY["ALL_INVALID"]:
+        return "ALL_INVALID"
+    return _validity(a)[start:stop]
+
+
+def slice_bool(a: Array, start: int, stop: int) -> Array:
+    """bool/compute/slice.rs:7-15 + BoolArray::try_new (bool/mod.rs:59-82): the bit buffer
+    sliced, first_byte_bit_offset = the buffer's bit offset % 8."""
+    from vortex_amd import arrays as A
+    off = a.meta.get("first_byte_bit_offset", 0)
+    bits = canon_bool(a)[start:stop]
+    return A.bool_array(bits, validity=_slice_validity(a, start, stop), bit_offset=(off + start) % 8)
+
+
+def slice_delta(a: Array, start: int, stop: int) -> Array:
+    """delta/compute.rs:36-73 (SliceFn::slice, no bounds check -- the reference's jagged "empty"
+    KAT slices past the end): whole 1024-value chunks of bases (LANES per chunk, one for the
+    remainder) and deltas around the physical range, offset = physical start % 1024."""
+    from vortex_amd import arrays as A
+    lanes = 1024 // (8 * ptype_width(a.ptype))
+    bases, deltas = a.children[0], a.children[1]
+    ps, pe = start + a.meta["offset"], stop + a.meta["offset"]
+    c0, c1 = ps // 1024, (pe + 1023) // 1024
+    nb = bases.len
+    nd = a.meta["deltas_len"]
+    new_bases = slice_any(bases, min(c0 * lanes, nb), min(c1 * lanes, nb))
+    new_deltas = slice_any(deltas, min(c0 * 1024, nd), min(c1 * 1024, nd))
+    v = _slice_validity(a, start, stop)
+    return A.delta(new_bases, new_deltas, offset=ps % 1024, length=stop - start, validity=v)
+
+
+def find_physical_index(a: Array, index: int) -> int:
+    """RunEndArray::find_physical_index (runend/array.rs:95-98): search_sorted(ends, index +
+    offset, Right).to_ends_index(len) (search_sorted.rs:78-85)."""
+    ends = canon(a.children[0])[0].astype(np.uint64)
+    i = int(np.searchsorted(ends, np.uint64(index + a.meta["offset"]), side="right"))
+    return i - 1 if i == ends.size else i
+
+
+def slice_runend(a: Array, start: int, stop: int) -> Array:
+    """runend/compute.rs:104-119: ends and values [begin, end + 1) of the runs holding start and
+    stop, validity sliced, offset = start + old offset, len = stop - start."""
+    from vortex_amd import arrays as A
+    b, e = find_physical_index(a, start), find_physical_index(a, stop)
+    return A.run_end(slice_any(a.children[0], b, e + 1), slice_any(a.children[1], b, e + 1),
+                     length=stop - start, offset=start + a.meta["offset"],
+                     validity=_slice_validity(a, start, stop))
+
+
+def slice_varbinview(a: Array, start: int, stop: int) -> Array:
+    """varbinview/compute.rs:49-65: views [start, stop) (16 bytes each), every data buffer kept,
+    validity sliced."""
+    from vortex_amd import arrays as A
+    views = _buf(a.children[0].buffers[0])[16 * start: 16 * stop]
+    bufs = [_buf(c.buffers[0]) for c in a.children[1: 1 + a.meta["n_buffers"]]]
+    return A.varbinview(views, bufs, utf8=a.dtype == DTYPE["UTF8"], validity=_slice_validity(a, start, stop))
+
+
 def slice_any(a: Array, start: int, stop: int) -> Array:
+    """SliceFn restatements of the encodings the reference's slice KATs build."""
     if a.encoding == ENC["FL_BITPACKED"]:
         return slice_bitpacked(a, start, stop)
     if a.encoding == ENC["PRIMITIVE"]:
         return slice_primitive(a, start, stop)
     if a.encoding == ENC["SPARSE"]:
         return slice_sparse(a, start, stop)
+    if a.encoding == ENC["FL_DELTA"]:
+        return slice_delta(a, start, stop)
+    if a.encoding == ENC["RUN_END"]:
+        return slice_runend(a, start, stop)
+    if a.encoding == ENC["VARBINVIEW"]:
+        return slice_varbinview(a, start, stop)
+    if a.encoding == ENC["BOOL"]:
+        return slice_bool(a, start, stop)
     raise NotImplementedError(f"slice of encoding {a.encoding}")
+
+
+def slice_checked(a: Array, start: int, stop: int) -> Array:
+    """compute::slice (compute/slice.rs:21-48): bounds checked, then SliceFn."""
+    if start > a.len or stop > a.len:
+        raise IndexError(f"OutOfBounds: {max(start, stop)} not in [0, {a.len}]")
+    if start > stop:
+        raise ValueError(f"start ({start}) must be <= stop ({stop})")
+    return slice_any(a, start, stop)
+
+
+def sparse_take(sp: Array, indices) -> Array:
+    """SparseArray's TakeFn (sparse/compute/take.rs:13-86): positions of the taken indices that
+    hit a patch and the patch values at them, as a new SparseArray of len(indices) with the same
+    fill (take_search_sorted; take_map gives the same pairs above 128 indices)."""
+    from vortex_amd import arrays as A
+    off = sp.meta["indices_offset"]
+    resolved = canon(sp.children[0])[0].astype(np.int64) - off
+    vals, vvalid = canon(sp.children[1])
+    pos, phys = [], []
+    lo = int(resolved.min()) if resolved.size else 0
+    hi = int(resolved.max()) if resolved.size else 0
+    for p, i in enumerate(np.asarray(indices, dtype=np.int64).tolist()):
+        if i < lo or i > hi:
+            continue
+        j = int(np.searchsorted(resolved, i, side="left"))
+        if j < resolved.size and resolved[j] == i:
+            pos.append(p)
+            phys.append(j)
+    pv = vals[np.array(phys, dtype=np.int64)]
+    pvalid = None if vvalid is None else vvalid[np.array(phys, dtype=np.int64)]
+    fill = None if sp.meta["fill_is_null"] else np.frombuffer(
+        sp.meta["fill"][: ptype_width(sp.ptype)], NP_OF_PTYPE[sp.ptype])[0]
+    return A.sparse(A.primitive(np.array(pos, dtype=np.uint64)),
+                    A.primitive(pv, sp.children[1].ptype,
+                                validity=None if not sp.children[1].nullable else
+                                ("ALL_VALID" if pvalid is None else pvalid)),
+                    len(np.asarray(indices)), fill=fill, ptype=sp.ptype)

@@ -95,3 +95,30 @@ def test_missing_library_fails_loudly(tmp_path, monkeypatch):
     monkeypatch.setattr(L, "GPU_LIB_PATH", tmp_path / "absent.so")
     with pytest.raises(ImportError, match="no CPU fallback"):
         L.gpu_lib()
+
+
+def test_plan_select_tie_rule():
+    """vxg_plan_select (host-only): the faster candidate unless another is within 3 % and its
+    graph is smaller; unmeasured -> the smaller graph; deterministic on equal cost (VERDICT r04
+    item 6: C3's candidates were 0.1871 vs 0.1907 ms, a coin flip before)."""
+    import ctypes as C
+    lib = L.gpu_lib()
+
+    def sel(ms, cost):
+        n = len(cost)
+        s = C.c_uint32(99)
+        msa = None if ms is None else (C.c_float * n)(*ms)
+        best = lib.vxg_plan_select(msa, (C.c_uint32 * n)(*cost), n, C.byref(s))
+        return best, L.PLAN_SELECTION[s.value]
+
+    assert sel([0.2], [5]) == (0, "single")
+    assert sel([0.1871, 0.1907], [3, 1]) == (1, "tie_fewer_nodes")   # within 3 %: smaller graph
+    assert sel([0.1907, 0.1871], [1, 3]) == (0, "tie_fewer_nodes")
+    assert sel([0.1871, 0.1907], [1, 3]) == (0, "tie_fewer_nodes")   # the faster is also smaller
+    assert sel([0.2899, 0.3886], [40, 4]) == (0, "faster")            # C5 at 1 GPU: 34 % apart
+    assert sel([0.120, 0.060], [40, 4]) == (1, "faster")
+    assert sel([0.100, 0.1029], [7, 7]) == (0, "tie_fewer_nodes")     # equal cost: lowest index
+    assert sel([0.1029, 0.100], [7, 7]) == (0, "tie_fewer_nodes")
+    assert sel([0.100, 0.1031], [9, 1]) == (0, "faster")              # 3.1 % apart: not a tie
+    assert sel(None, [9, 4]) == (1, "unmeasured")
+    assert sel(None, [4, 4]) == (0, "unmeasured")

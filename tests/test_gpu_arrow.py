@@ -108,7 +108,7 @@ def test_c4_full_size_is_valid_arrow(ctx):
         assert got[i].as_py() == heap[offs[i]: offs[i + 1]].tobytes().decode()
 
 
-def test_lineitem_string_columns_are_valid_arrow(ctx):
+def test_lineitem_string_columns_are_valid_arrow(ctx, lineitem_file_bytes):
     """The lineitem scan's string columns (4 Dict(VarBin) + l_comment FSST, chunked) read from
     file bytes and canonicalized by one plan: every column validates and equals the generator's
     strings."""
@@ -116,8 +116,7 @@ def test_lineitem_string_columns_are_valid_arrow(ctx):
     import bench
     from tools import lineitem as L
     from vortex_amd.file import DeviceColumns, VortexFile
-    host = bench.c5_file(None, 0)
-    f = VortexFile(torch.from_numpy(host).pin_memory())
+    f = VortexFile(torch.from_numpy(lineitem_file_bytes).pin_memory())
     chunks = range(0, 4)
     dc = DeviceColumns(f, ctx, None, chunks.start, chunks.stop)
     plan = A.Plan(dc.nodes, ctx)

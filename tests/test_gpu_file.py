@@ -88,3 +88,53 @@ def test_file_reader_rejects_uncovered_region(ctx):
         f.column_tree(0, 0, 2, region.data_ptr(), 0, 64)
     assert ei.value.kind == "InvalidArgument"
     f.close()
+
+
+def test_c5_full_size_plan(ctx, lineitem_file_bytes):
+    """BASELINE C5 at full size through the exact path the bench times: all
+    92 chunks x 16 columns read from the file's bytes, one H2D per column region
+    (DeviceColumns), one measuring vxg_plan (its kept graph) replayed twice; plus the same
+    columns recorded unbatched (device-table K1 launches of >= 128 workgroups take K1w) and
+    batched (K1g).  Every numeric column's bytes and every string row equal the generator's
+    plain values (bench.c5_verify); three chunks also equal the oracle's canonicalize of the
+    written arrays; the forced modes' outputs equal the verified ones byte for byte."""
+    import time
+    import torch
+    import bench
+    from test_gpu_parity import plan_mode
+    t0 = time.perf_counter()
+    f = VortexFile(torch.from_numpy(lineitem_file_bytes).pin_memory())
+    n = LI.n_chunks()
+    dc = DeviceColumns(f, ctx, None, 0, n)
+    plan = A.Plan(dc.nodes, ctx, measure=True)
+    plan.launch()
+    res = plan.launch(sync=True)
+    assert bench.c5_verify(res, range(n)) == f.row_count
+    ref = [(r.kind, [bytes(t.cpu().numpy()) for t in (r.values, r.views, r.data) if t is not None]) for r in res]
+    # oracle on a sample of chunks: each column's chunk arrays as written, canonicalized on the CPU
+    from oracle_tree import view_bytes
+    sample = (0, 45, n - 1)
+    cols, _ = LI.lineitem_columns(sample)
+    for (name, kind), r in zip(LI.COLUMNS, res):
+        for j, c in enumerate(sample):
+            chunk = cols[name].children[1 + j]
+            o, _ = canon(chunk)
+            row0 = c * LI.CHUNK_ROWS
+            if r.kind == "primitive":
+                assert r.numpy()[row0: row0 + chunk.len].tobytes() == o.tobytes(), (name, c)
+            else:
+                views, bufs = r.numpy()[0], r.buffers()
+                rv, rh = o
+                for i in range(0, chunk.len, 97):
+                    assert view_bytes(views, bufs, row0 + i) == view_bytes(rv, rh, i), (name, c, i)
+    plan.close()
+    for mode in ("0", "1"):
+        with plan_mode(mode):
+            p = A.Plan(dc.nodes, ctx)
+        out = p.launch(sync=True)
+        assert p.info()["batched"] == (mode == "1")
+        for (kind, bufs), r in zip(ref, out):
+            assert [bytes(t.cpu().numpy()) for t in (r.values, r.views, r.data) if t is not None] == bufs
+        p.close()
+    f.close()
+    assert time.perf_counter() - t0 < 120

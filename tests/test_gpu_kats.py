@@ -116,3 +116,158 @@ def test_kat_dict_nullable_on_gpu(ctx):
     assert [view_bytes(views, heap, i) if s is not None else None for i, s in enumerate(strs)] == strs
     (rv, rh), _ = canon(arr)
     assert views.tobytes() == rv.tobytes()
+
+
+# ---------------------------------------------------------------- round 5: slices, nulls, take
+def _apply_slices(arr, slices):
+    """First slice = SliceFn::slice as the KAT calls it (no bounds check), then compute::slice."""
+    from oracle_tree import slice_checked
+    for j, s in enumerate(slices):
+        arr = (slice_any if j == 0 else slice_checked)(arr, *s)
+    return arr
+
+
+@pytest.mark.parametrize("bitpack", [False, True], ids=["primitive_deltas", "bitpacked_deltas"])
+@pytest.mark.parametrize("case", [c["test"] for c in KATS["delta_slices"]["cases"]])
+def test_kat_delta_slices_on_gpu(ctx, case, bitpack):
+    """delta/compute.rs:162-405: jagged (remainder chunk with one scalar base) and non-jagged
+    arrays, empty slices, slices inside / across 1024-value chunks and slices of slices,
+    canonicalized by the engine from the sliced metadata (offset, partial bases/deltas).  The
+    reference keeps the deltas plain; the BitPacked-deltas variant sends the same slices
+    through the fused K1 -> K3 path."""
+    k = next(c for c in KATS["delta_slices"]["cases"] if c["test"] == case)
+    arr = _apply_slices(E.encode_delta(np.arange(k["n"], dtype=np.uint32), bitpack_deltas=bitpack), k["slices"])
+    lo, hi = k["expect"]
+    got = _gpu(arr, ctx).numpy()
+    assert got.tolist() == list(range(lo, hi))
+    assert got.tobytes() == canon(arr)[0].tobytes()
+
+
+def _ree(b, ends_ptype="u64"):
+    if "values" in b:
+        ends, rv = E.runend_encode(np.array(b["values"], np.int32))
+        ends = ends.astype(A.NP_OF_PTYPE[ends_ptype])
+    else:
+        ends = np.array(b["ends"], A.NP_OF_PTYPE[ends_ptype])
+        rv = np.array(b["run_values"], np.int32)
+    vv, validity = b.get("values_validity"), b.get("validity")
+    if validity is not None and vv is None:
+        vv = "ALL_VALID"
+    return A.run_end(A.primitive(ends), A.primitive(rv, validity=vv), validity=validity)
+
+
+def _masked(vals, valid):
+    return [None if (valid is not None and not ok) else int(v)
+            for v, ok in zip(vals, valid if valid is not None else [True] * len(vals))]
+
+
+def test_kat_runend_nullable_on_gpu(ctx):
+    """runend/compress.rs:180-210 decode_nullable: values and the validity bitmap."""
+    k = KATS["runend_decode_nullable"]
+    arr = _ree(dict(ends=k["ends"], run_values=k["run_values"], values_validity=k["values_validity"],
+                    validity=k["validity"]), k["ends_ptype"])
+    res = _gpu(arr, ctx)
+    assert res.numpy().tolist() == k["expect_decoded"]
+    assert res.validity_mask().tolist() == k["expect_validity"]
+
+
+@pytest.mark.parametrize("case", [c["test"] for c in KATS["runend_compute"]["cases"]])
+def test_kat_runend_compute_on_gpu(ctx, case):
+    """runend/compute.rs:132-353: take (vxg_take_array), slices (SliceFn metadata: ends/values of
+    the covering runs, offset, length) and slice-then-take, incl. nulls and the out-of-bounds
+    take, all on the GPU."""
+    k = next(c for c in KATS["runend_compute"]["cases"] if c["test"] == case)
+    arr = _apply_slices(_ree(k["build"], k.get("ends_ptype", "u64")), k.get("slices", []))
+    full = _gpu(arr, ctx)
+    ref, rvalid = canon(arr)
+    assert full.numpy().tobytes() == ref.tobytes()
+    if "take" not in k:
+        assert full.numpy().tolist() == k["expect"]
+        if "expect_validity" in k:
+            assert full.validity_mask().tolist() == k["expect_validity"]
+        return
+    idx = np.array(k["take"], np.int64)
+    if "expect_error" in k:
+        with pytest.raises(A.VortexError, match="OutOfBounds|out of bounds"):
+            A.take(arr.to(_dev()), idx, ctx)
+        return
+    res = A.take(arr.to(_dev()), idx, ctx)
+    assert _masked(res.numpy(), res.validity_mask()) == k["expect"]
+
+
+def _sparse_kat(k):
+    idx = A.primitive(np.array(k["indices"], np.uint64))
+    if "values_bits" in k:
+        vals = np.array([struct.unpack("<d", bytes.fromhex(h))[0] for h in k["values_bits"]])
+        return A.sparse(idx, A.primitive(vals, validity="ALL_VALID"), k["len"])
+    return A.sparse(idx, A.primitive(np.array(k["values"], A.NP_OF_PTYPE[k["ptype"]])), k["len"], fill=k["fill"])
+
+
+@pytest.mark.parametrize("case", [c["test"] for c in KATS["sparse_slices"]["cases"]])
+def test_kat_sparse_slices_on_gpu(ctx, case):
+    """sparse/compute/slice.rs:29-70: the sliced SparseArray (indices by search_sorted, new
+    indices_offset) canonicalizes on the GPU to the fill with the one kept patch."""
+    from oracle_tree import slice_checked
+    k0 = KATS["sparse_slices"]
+    k = next(c for c in k0["cases"] if c["test"] == case)
+    arr = _sparse_kat(k0)
+    for s in k["slices"]:
+        arr = slice_checked(arr, *s)
+    got = _gpu(arr, ctx).numpy()
+    assert got.size == k["expect_len"]
+    for i, v in k["expect_at"]:
+        assert int(got[i]) == v
+    assert int(np.count_nonzero(got)) == len(k["expect_values"])
+    assert got.tobytes() == canon(arr)[0].tobytes()
+
+
+@pytest.mark.parametrize("case", [c["test"] for c in KATS["sparse_take"]["cases"]])
+def test_kat_sparse_take_on_gpu(ctx, case):
+    """sparse/compute/take.rs:114-200: take on a null-filled f64 SparseArray.  The reference
+    returns a SparseArray (positions, values); its canonical -- the taken values, null where no
+    patch was hit -- is what vxg_take_array produces, and the restated SparseArray result
+    canonicalizes to the same bytes on the GPU."""
+    from oracle_tree import sparse_take
+    k0 = KATS["sparse_take"]
+    k = next(c for c in k0["cases"] if c["test"] == case)
+    sp = _sparse_kat(k0)
+    res = A.take(sp.to(_dev()), np.array(k["take"], np.int64), ctx)
+    got, valid = res.numpy(), res.validity_mask()
+    pos = k["expect_indices"]
+    assert valid.tolist() == [i in pos for i in range(len(k["take"]))]
+    assert [struct.pack("<d", got[i]).hex() for i in pos] == k["expect_values_bits"]
+    taken = sparse_take(sp, k["take"])
+    t = _gpu(taken, ctx)
+    assert t.validity_mask().tolist() == valid.tolist()
+    assert t.numpy()[valid].tobytes() == got[valid].tobytes()
+
+
+def test_kat_sparse_bool_on_gpu(ctx):
+    """sparse/flatten.rs:108-117: Sparse(Bool) with a true fill canonicalizes to Canonical::Bool;
+    bits = fill with the patches, validity set exactly at the indices (:44-66)."""
+    k = KATS["sparse_bool"]
+    arr = A.sparse_bool(A.primitive(np.array(k["indices"], np.uint64)), A.bool_array(k["values"]), k["len"],
+                        fill=k["fill"])
+    res = _gpu(arr, ctx)
+    assert res.kind == "bool"
+    assert res.numpy().tolist() == k["expect"]
+    assert res.validity_mask().tolist() == k["expect_validity"]
+
+
+def test_kat_chunked_pack_sliced_varbin_on_gpu(ctx):
+    """chunked/canonical.rs:254-273 pack_sliced_varbin: two sliced VarBinView chunks packed into
+    one VarBinView (pack_views) read back as ["bar", "baz", "baz", "quak"]; a variant with
+    out-of-line strings checks the rebased buffer_index of sliced chunks."""
+    from oracle_tree import slice_checked
+    k = KATS["chunked_pack_sliced_varbin"]
+    for strs in ([s.encode() for s in k["strings"]],
+                 [s.encode() * 5 for s in k["strings"]]):
+        base = E.encode_varbinview(strs)
+        arr = A.chunked([slice_checked(base, *s) for s in k["slices"]])
+        res = _gpu(arr, ctx)
+        views, _ = res.numpy()
+        heap = res.buffers()
+        expect = [s.encode() * (1 if strs[0] == b"foo" else 5) for s in k["expect"]]
+        assert [view_bytes(views, heap, i) for i in range(views.shape[0])] == expect
+        (rv, rb), _ = canon(arr)
+        assert [view_bytes(rv, rb, i) for i in range(rv.shape[0])] == expect

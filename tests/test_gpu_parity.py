@@ -354,6 +354,38 @@ def test_plan_measure_flag_and_info(ctx):
     p2.close()
 
 
+def test_plan_measure_leaves_pending_caller_error(ctx):
+    """a measuring create must not take over an error of the caller's earlier,
+    unsynced work.  A bad decode is left pending (no sync), then a good plan is created with
+    VXG_PLAN_MEASURE: create succeeds without measuring (selection "unmeasured", the smaller
+    graph kept), and the caller's next sync still reports the pending error."""
+    import torch
+    rng = np.random.default_rng(81)
+    bad = _alp_patched(rng, 50_000, np.array([5, 70, 900]))[0]
+    bad.children[1].children[0] = A.primitive(np.array([5, 70, 50_000], np.uint64))
+    A.canonicalize(bad.to(torch_dev()), ctx, sync=False)  # pending, not synced
+    good = [E.encode_for_bitpacked(rng.integers(-99, 99, 50_000).astype(np.int64)),
+            E.encode_dict_strings([b"row-%d" % (i % 37) for i in range(20_000)])]
+    dev = [a.to(torch_dev()) for a in good]
+    p = V.Plan(dev, ctx, measure=True)
+    info = p.info()
+    assert info["selection"] == "unmeasured" and all(c["ms"] == 0.0 for c in info["candidates"])
+    costs = [c["cost"] for c in info["candidates"]]
+    kept = [c for c in info["candidates"] if c["batched"] == info["batched"]][0]
+    assert kept["cost"] == min(costs)
+    with pytest.raises(V.VortexGpuError, match="out of bounds"):
+        ctx.sync()
+    ctx.sync()  # reported once
+    res = p.launch(sync=True)
+    assert res[0].numpy().tobytes() == canon(good[0])[0].tobytes()
+    p.close()
+    # with nothing pending, the same create measures both candidates
+    p = V.Plan(dev, ctx, measure=True)
+    assert p.info()["selection"] in ("faster", "tie_fewer_nodes")
+    assert all(c["ms"] > 0 for c in p.info()["candidates"])
+    p.close()
+
+
 def test_alp_f32_cascade(ctx):
     rng = np.random.default_rng(4)
     vals = (np.round(rng.uniform(-500, 500, 50_000) * 10) / 10).astype(np.float32)
@@ -896,7 +928,8 @@ def sys_path_bench():
 
 class plan_mode:
     """VXG_PLAN_BATCH for the plans created inside (capi.hip reads it at every vxg_plan_create):
-    "0" unbatched, "1" batched, "mixed", None = the default (both recorded, the faster kept)."""
+    "0" unbatched, "1" batched, "mixed", None = the default (plain create: one candidate by the
+    400 MB output rule; measure=True: both recorded, vxg_plan_select keeps one)."""
 
     def __init__(self, mode):
         self.mode = mode
@@ -1052,6 +1085,52 @@ def test_plan_string_dict_job_lookup(ctx, sizes):
     (rviews, rbufs), _ = canon(sarr)
     assert res.numpy()[0].tobytes() == rviews.tobytes()
     assert [b.tobytes() for b in res.buffers()] == [b.tobytes() for b in rbufs]
+    plan.close()
+
+
+@pytest.mark.parametrize("mode", ["0", "1"])
+@pytest.mark.parametrize("n_words,wlen", [(300, 20), (1000, 20)], ids=["bytes_gt_2k", "views_bytes_gt_16k"])
+def test_plan_string_dict_large_dictionary(ctx, mode, n_words, wlen):
+    """K1g builds a Dict(VarBin) column's views from LDS only when the dictionary
+    bytes fit (<= 2 KiB beside the views in 16 KiB); larger dictionaries take the global-memory
+    branch (views read their bytes from HBM).  300 distinct 20-byte words (6 KB of bytes) and
+    1000 (views + bytes > 16 KiB), unbatched (one K1g per column) and batched: every view and
+    byte equals the oracle."""
+    import torch
+    rng = np.random.default_rng(89 + n_words)
+    words = [(b"w%05d-" % i + bytes(rng.integers(97, 123, wlen - 7, dtype=np.uint8))) for i in range(n_words)]
+    strs = [[words[i] for i in rng.integers(0, n_words, n)] for n in (70_000, 65_536, 1234)]
+    sarr = A.chunked([E.encode_dict_strings(s) for s in strs])
+    with plan_mode(mode):
+        plan = V.Plan([sarr.to(torch.device("cuda", 0))], ctx)
+    res = plan.launch(sync=True)[0]
+    (rviews, rbufs), _ = canon(sarr)
+    assert res.numpy()[0].tobytes() == rviews.tobytes()
+    assert [b.tobytes() for b in res.buffers()] == [b.tobytes() for b in rbufs]
+    plan.close()
+
+
+@pytest.mark.parametrize("mode", ["0", "1"])
+@pytest.mark.parametrize("n_words", [5, 300])
+def test_plan_string_dict_bad_offsets(ctx, mode, n_words):
+    """A Dict(VarBin) dictionary whose offsets run past its bytes is reported by the plan's
+    replay as 'VarBin offsets out of range' (LDS and global-memory K1g branches)."""
+    import torch
+    rng = np.random.default_rng(90)
+    words = [b"word-%04d-abcdefghij" % i for i in range(n_words)]
+    chunks = []
+    for n in (40_000, 5_000):
+        d = E.encode_dict_strings([words[i] for i in rng.integers(0, n_words, n)])
+        vb = d.children[0]
+        offs = np.ascontiguousarray(vb.children[0].buffers[0]).view(A.NP_OF_PTYPE[vb.children[0].ptype]).copy()
+        offs[len(offs) // 2] = offs[-1] + 5000  # past the end of the bytes
+        vb.children[0] = A.primitive(offs)
+        chunks.append(d)
+    with plan_mode(mode):
+        plan = V.Plan([A.chunked(chunks).to(torch.device("cuda", 0))], ctx)
+    with pytest.raises(V.VortexGpuError, match="VarBin offsets out of range"):
+        plan.launch(sync=True)
+    ctx.sync()
     plan.close()
 
 
@@ -1329,7 +1408,8 @@ def test_plan_modes_non_c5_mix(ctx, mode):
     u64 W=10, u64 values)], 6 chunks), a C4-like FSST column, bool columns (RunEndBool, ByteBool,
     a primitive with a RunEndBool validity) and one large chunked u32 column -- recorded unbatched,
     batched, mixed (arrays <= VXG_PLAN_BATCH_MAX_BYTES batched) and by default (both recorded, the
-    faster kept): every replay byte-identical to the oracle in every mode."""
+    faster kept unless within 3 %, then the smaller graph, measure=True): every replay
+    byte-identical to the oracle in every mode."""
     import torch
     sys_path_bench()
     import bench
@@ -1355,7 +1435,7 @@ def test_plan_modes_non_c5_mix(ctx, mode):
     os.environ.update(env)
     try:
         with plan_mode(mode):
-            plan = V.Plan([a.to(torch_dev()) for a in arrs], ctx)
+            plan = V.Plan([a.to(torch_dev()) for a in arrs], ctx, measure=mode is None)
     finally:
         for k, v in old.items():
             if v is None:

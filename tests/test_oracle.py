@@ -547,3 +547,147 @@ def test_kat_dict_nullable():
     k = KATS["dict_repeated_values"]
     arr = E.encode_dict_strings([s.encode() for s in k["strings"]])
     assert canon(arr.children[1])[0].tolist() == k["expect_codes"]
+
+
+# ---------------------------------------------------------------- round-5 KATs: slices, nulls, take
+def _delta_kat(n: int):
+    """DeltaArray::try_from_vec((0u32..n).collect()): the deltas stay a PrimitiveArray."""
+    return E.encode_delta(np.arange(n, dtype=np.uint32), bitpack_deltas=False)
+
+
+def _apply_slices(arr, slices):
+    """The first slice is SliceFn::slice (the KAT calls it directly), later ones compute::slice."""
+    from oracle_tree import slice_any, slice_checked
+    for j, s in enumerate(slices):
+        arr = (slice_any if j == 0 else slice_checked)(arr, *s)
+    return arr
+
+
+@pytest.mark.parametrize("case", [c["test"] for c in KATS["delta_slices"]["cases"]])
+def test_kat_delta_slices(case):
+    k = next(c for c in KATS["delta_slices"]["cases"] if c["test"] == case)
+    arr = _apply_slices(_delta_kat(k["n"]), k["slices"])
+    lo, hi = k["expect"]
+    assert arr.len == hi - lo
+    assert canon(arr)[0].tolist() == list(range(lo, hi))
+
+
+def test_kat_delta_slice_metadata():
+    """delta/compute.rs:36-73 on the jagged 2000-row array: slice(1034, 1274) keeps the one
+    remainder base and the 976 remainder deltas, offset 10 (delta/mod.rs:89-157 checks pass)."""
+    from oracle_tree import slice_any
+    sl = slice_any(_delta_kat(2000), 1034, 1274)
+    assert (sl.children[0].len, sl.children[1].len, sl.meta["offset"], sl.meta["deltas_len"]) == (1, 976, 10, 976)
+
+
+def _ree(b, ends_ptype="u64"):
+    """RunEndArray: ree_array() = RunEndArray::encode(values) (u64 ends, runend/compress.rs:15-93);
+    otherwise RunEndArray::try_new(ends, values, validity) from the literals."""
+    if "values" in b:
+        ends, rv = E.runend_encode(np.array(b["values"], np.int32))
+        ends = ends.astype(A.NP_OF_PTYPE[ends_ptype])
+    else:
+        ends = np.array(b["ends"], A.NP_OF_PTYPE[ends_ptype])
+        rv = np.array(b["run_values"], np.int32)
+    vv = b.get("values_validity")
+    validity = b.get("validity")
+    if validity is not None and vv is None:
+        vv = "ALL_VALID"
+    return A.run_end(A.primitive(ends), A.primitive(rv, validity=vv), validity=validity)
+
+
+def _runend_expect(arr, k):
+    """-> (values, validity) the KAT case expects, from the oracle; None entries = null rows."""
+    vals, valid = canon(arr)
+    if "take" in k:
+        idx = np.array(k["take"], np.int64)
+        if (idx >= arr.len).any():
+            raise IndexError("OutOfBounds")
+        vals = vals[idx]
+        valid = None if valid is None else valid[idx]
+    return [None if (valid is not None and not ok) else int(v)
+            for v, ok in zip(vals, valid if valid is not None else [True] * len(vals))], valid
+
+
+def test_kat_runend_nullable():
+    k = KATS["runend_decode_nullable"]
+    arr = _ree(dict(ends=k["ends"], run_values=k["run_values"], values_validity=k["values_validity"],
+                    validity=k["validity"]), k["ends_ptype"])
+    vals, valid = canon(arr)
+    assert vals.tolist() == k["expect_decoded"] and valid.tolist() == k["expect_validity"]
+
+
+@pytest.mark.parametrize("case", [c["test"] for c in KATS["runend_compute"]["cases"]])
+def test_kat_runend_compute(case):
+    k = next(c for c in KATS["runend_compute"]["cases"] if c["test"] == case)
+    arr = _ree(k["build"], k.get("ends_ptype", "u64"))
+    arr = _apply_slices(arr, k.get("slices", []))
+    if "expect_error" in k:
+        with pytest.raises(IndexError):
+            _runend_expect(arr, k)
+        return
+    got, valid = _runend_expect(arr, k)
+    if "expect_validity" in k:  # maybe_null_slice values (nulls included) + the validity
+        assert canon(arr)[0].tolist() == k["expect"] and valid.tolist() == k["expect_validity"]
+    else:
+        assert got == k["expect"]
+
+
+def test_kat_ree_array_encoding():
+    """runend/compute.rs:125-131: RunEndArray::encode of [1,1,1,4,4,4,2,2,5,5,5,5]."""
+    ends, rv = E.runend_encode(np.array([1, 1, 1, 4, 4, 4, 2, 2, 5, 5, 5, 5], np.int32))
+    assert ends.tolist() == [3, 6, 8, 12] and rv.tolist() == [1, 4, 2, 5]
+
+
+def _sparse_kat(k):
+    idx = A.primitive(np.array(k["indices"], np.uint64))
+    if "values_bits" in k:
+        vals = A.primitive(_f(k["values_bits"], k["ptype"]), validity="ALL_VALID")
+        return A.sparse(idx, vals, k["len"])  # fill null
+    return A.sparse(idx, A.primitive(np.array(k["values"], A.NP_OF_PTYPE[k["ptype"]])), k["len"], fill=k["fill"])
+
+
+@pytest.mark.parametrize("case", [c["test"] for c in KATS["sparse_slices"]["cases"]])
+def test_kat_sparse_slices(case):
+    k0 = KATS["sparse_slices"]
+    k = next(c for c in k0["cases"] if c["test"] == case)
+    from oracle_tree import slice_checked
+    arr = _sparse_kat(k0)
+    for s in k["slices"]:
+        arr = slice_checked(arr, *s)
+    assert arr.len == k["expect_len"]
+    assert canon(arr.children[1])[0].tolist() == k["expect_values"]
+    got, valid = canon(arr)
+    assert valid is None
+    for i, v in k["expect_at"]:
+        assert int(got[i]) == v
+    assert int(np.count_nonzero(got)) == len(k["expect_values"])
+
+
+@pytest.mark.parametrize("case", [c["test"] for c in KATS["sparse_take"]["cases"]])
+def test_kat_sparse_take(case):
+    from oracle_tree import sparse_take
+    k0 = KATS["sparse_take"]
+    k = next(c for c in k0["cases"] if c["test"] == case)
+    taken = sparse_take(_sparse_kat(k0), k["take"])
+    assert canon(taken.children[0])[0].tolist() == k["expect_indices"]
+    tv = canon(taken.children[1])[0]
+    assert [struct.pack("<d", x).hex() for x in tv] == k["expect_values_bits"]
+    assert taken.len == k.get("expect_len", len(k["take"]))
+
+
+def test_kat_sparse_bool():
+    k = KATS["sparse_bool"]
+    arr = A.sparse_bool(A.primitive(np.array(k["indices"], np.uint64)), A.bool_array(k["values"]), k["len"],
+                        fill=k["fill"])
+    vals, valid = canon(arr)
+    assert vals.tolist() == k["expect"] and valid.tolist() == k["expect_validity"]
+
+
+def test_kat_chunked_pack_sliced_varbin():
+    from oracle_tree import slice_checked
+    k = KATS["chunked_pack_sliced_varbin"]
+    base = E.encode_varbinview([s.encode() for s in k["strings"]])
+    chunks = [slice_checked(base, *s) for s in k["slices"]]
+    (views, bufs), _ = canon(A.chunked(chunks))
+    assert [view_bytes(views, bufs, i).decode() for i in range(views.shape[0])] == k["expect"]

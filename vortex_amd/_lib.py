@@ -22,7 +22,7 @@ PTYPES = ["u8", "u16", "u32", "u64", "i8", "i16", "i32", "i64", "f16", "f32", "f
 PTYPE = {n: i for i, n in enumerate(PTYPES)}
 DTYPE = dict(NULL=0, BOOL=1, PRIMITIVE=2, UTF8=3, BINARY=4)
 VALIDITY = dict(NON_NULLABLE=0, ALL_VALID=1, ALL_INVALID=2, ARRAY=3)
-ABI_VERSION = 6  # VXG_ABI_VERSION
+ABI_VERSION = 7  # VXG_ABI_VERSION
 STATUS = {0: "OK", 1: "OutOfBounds", 2: "ComputeError", 3: "InvalidArgument", 4: "InvalidSerde",
           5: "NotImplemented", 6: "MismatchedTypes", 7: "AssertionFailed", 8: "HipError",
           9: "OutOfMemory"}
@@ -144,7 +144,11 @@ PLAN_MEASURE = 1  # VXG_PLAN_MEASURE
 class VxgPlanInfo(C.Structure):
     _fields_ = [("batched", C.c_uint32), ("branches", C.c_uint32), ("direct_nodes", C.c_uint32),
                 ("n_candidates", C.c_uint32), ("candidate_batched", C.c_uint32 * 2),
-                ("candidate_ms", C.c_float * 2), ("create_ms", C.c_float), ("reserved", C.c_uint32)]
+                ("candidate_ms", C.c_float * 2), ("create_ms", C.c_float), ("selection", C.c_uint32),
+                ("candidate_cost", C.c_uint32 * 2), ("reserved", C.c_uint32)]
+
+
+PLAN_SELECTION = {0: "single", 1: "faster", 2: "tie_fewer_nodes", 3: "unmeasured"}
 
 
 class VxgIntStats(C.Structure):
@@ -182,6 +186,7 @@ GPU_SIGNATURES = {
     "vxg_plan_create": (ST, [VP, C.POINTER(VxgArray), C.POINTER(VxgCanonical), U32, C.POINTER(VP)]),
     "vxg_plan_create_ex": (ST, [VP, C.POINTER(VxgArray), C.POINTER(VxgCanonical), U32, U32, C.POINTER(VP)]),
     "vxg_plan_get_info": (ST, [VP, C.c_void_p]),
+    "vxg_plan_select": (U32, [C.POINTER(C.c_float), C.POINTER(U32), U32, C.POINTER(U32)]),
     "vxg_plan_launch": (ST, [VP, VP]),
     "vxg_plan_destroy": (ST, [VP]),
     "vxg_canonical_layout": (ST, [VP, C.POINTER(VxgArray), C.POINTER(U64), C.POINTER(U64),

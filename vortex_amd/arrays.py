@@ -240,10 +240,20 @@ def delta(bases: Array, deltas: Array, offset: int = 0, length: Optional[int] = 
 
 def run_end(ends: Array, values: Array, length: Optional[int] = None, offset: int = 0,
             validity=None) -> Array:
-    """RunEndArray (runend/array.rs:47-106)."""
+    """RunEndArray (runend/array.rs:38-93): length defaults to the last end (try_new); a
+    non-zero offset must be below the first end (with_offset_and_length :63-68)."""
     if ends.ptype[0] not in "ui":
         _bail("InvalidArgument", "Run ends must be integers")
-    length = length if length is not None else None
+    if ends.encoding == ENC["PRIMITIVE"] and ends.len:
+        ev = np.asarray(ends.buffers[0]).view(NP_OF_PTYPE[ends.ptype])
+        if length is None:
+            length = int(ev[ends.len - 1])
+        if offset != 0 and int(ev[0]) <= offset:
+            _bail("InvalidArgument", f"First run end {int(ev[0])} must be bigger than offset {offset}")
+    elif length is None and ends.len == 0:
+        length = 0
+    if length is None:
+        _bail("InvalidArgument", "length needed for compressed ends")
     nullable = validity is not None
     vk, vchild = _validity_kind(nullable, validity)
     return Array(ENC["RUN_END"], length, DTYPE["PRIMITIVE"], values.ptype, nullable, vk,
@@ -774,8 +784,11 @@ class Plan:
         _lib.check(self.ctx.lib.vxg_plan_get_info(self.handle, C.byref(i)))
         cands = [{"batched": bool(i.candidate_batched[c]), "ms": round(float(i.candidate_ms[c]), 4)}
                  for c in range(i.n_candidates)]
+        for c in range(i.n_candidates):
+            cands[c]["cost"] = int(i.candidate_cost[c])
         return {"batched": bool(i.batched), "branches": int(i.branches), "direct_nodes": int(i.direct_nodes),
-                "candidates": cands, "create_ms": round(float(i.create_ms), 3)}
+                "candidates": cands, "selection": _lib.PLAN_SELECTION.get(int(i.selection), str(i.selection)),
+                "create_ms": round(float(i.create_ms), 3)}
 
     def launch(self, sync: bool = False):
         _lib.check(self.ctx.lib.vxg_plan_launch(self.handle, self.ctx.stream_ptr()))

@@ -2273,7 +2273,41 @@ static vxg_status time_plans(const std::vector<vxg_plan*>& cands, int reps, std:
     return st;
 }
 
+// Graph nodes + dependency edges: what a replay pays beyond its kernels (each cross-branch edge
+// is a queue synchronisation; a direct chain replays with no graph at all).
+static uint32_t graph_cost(hipGraph_t g) {
+    size_t nn = 0, ne = 0;
+    if (!g || hipGraphGetNodes(g, nullptr, &nn) != hipSuccess) return 0;
+    if (hipGraphGetEdges(g, nullptr, nullptr, &ne) != hipSuccess) ne = 0;
+    return uint32_t(nn + ne);
+}
+
 extern "C" {
+
+uint32_t vxg_plan_select(const float* ms, const uint32_t* cost, uint32_t n, uint32_t* selection) {
+    uint32_t sel = VXG_PLAN_SEL_SINGLE, best = 0;
+    if (n > 1 && !ms) {  // unmeasured: the smallest graph
+        sel = VXG_PLAN_SEL_UNMEASURED;
+        for (uint32_t c = 1; c < n; c++)
+            if (cost && cost[c] < cost[best]) best = c;
+    } else if (n > 1) {
+        uint32_t fastest = 0;
+        for (uint32_t c = 1; c < n; c++)
+            if (ms[c] < ms[fastest]) fastest = c;
+        best = fastest;
+        sel = VXG_PLAN_SEL_FASTER;
+        // candidates within 3 % of the fastest are equal: the smallest graph among them, the
+        // lowest index on equal cost
+        for (uint32_t c = 0; c < n; c++) {
+            if (c == fastest || !(ms[c] <= ms[fastest] * 1.03f)) continue;
+            sel = VXG_PLAN_SEL_TIE_COST;
+            if (!cost) continue;
+            if (cost[c] < cost[best] || (cost[c] == cost[best] && c < best)) best = c;
+        }
+    }
+    if (selection) *selection = sel;
+    return best;
+}
 
 vxg_status vxg_plan_create(vxg_ctx* ctx, const vxg_array* arrays, vxg_canonical* outs, uint32_t n, vxg_plan** plan) {
     return vxg_plan_create_ex(ctx, arrays, outs, n, 0, plan);
@@ -2336,19 +2370,28 @@ vxg_status vxg_plan_create_ex(vxg_ctx* ctx, const vxg_array* arrays, vxg_canonic
         plans.push_back(p);
     }
     size_t best = 0;
+    uint32_t selection = VXG_PLAN_SEL_SINGLE;
     std::vector<float> ms(plans.size(), 0.f);
-    if (st == VXG_OK && measure && !plans.empty()) {
+    std::vector<uint32_t> cost(plans.size(), 0);
+    for (size_t c = 0; c < plans.size(); c++) cost[c] = graph_cost(plans[c]->graph);
+    if (st == VXG_OK && measure && plans.size() > 1) {
         // the candidates read the inputs now: every upload the caller enqueued (any stream) first
         st = hip_check(hipDeviceSynchronize(), "plan create: device synchronize");
-        if (st == VXG_OK) st = time_plans(plans, 3, &ms);
-        for (size_t c = 1; c < ms.size(); c++)
-            if (ms[c] < ms[best]) best = c;
-        if (st == VXG_OK) {  // errors the measured runs found belong to create, not the next sync
-            uint32_t err = 0;
-            st = hip_check(hipMemcpy(&err, ctx->c.err_word, 4, hipMemcpyDeviceToHost), "error word readback");
-            if (st == VXG_OK && err) {
-                st = hip_check(hipMemset(ctx->c.err_word, 0, 4), "error word reset");
-                if (st == VXG_OK) st = status_of_err_word(err);
+        uint32_t pending = 0;  // an error of the caller's earlier work: theirs to sync, not ours
+        if (st == VXG_OK)
+            st = hip_check(hipMemcpy(&pending, ctx->c.err_word, 4, hipMemcpyDeviceToHost), "error word readback");
+        if (st == VXG_OK && pending) {
+            best = vxg_plan_select(nullptr, cost.data(), uint32_t(plans.size()), &selection);
+        } else if (st == VXG_OK) {
+            st = time_plans(plans, 3, &ms);
+            if (st == VXG_OK) best = vxg_plan_select(ms.data(), cost.data(), uint32_t(plans.size()), &selection);
+            if (st == VXG_OK) {  // errors the measured runs found belong to create, not the next sync
+                uint32_t err = 0;
+                st = hip_check(hipMemcpy(&err, ctx->c.err_word, 4, hipMemcpyDeviceToHost), "error word readback");
+                if (st == VXG_OK && err) {
+                    st = hip_check(hipMemset(ctx->c.err_word, 0, 4), "error word reset");
+                    if (st == VXG_OK) st = status_of_err_word(err);
+                }
             }
         }
         if (std::getenv("VXG_PLAN_DEBUG"))
@@ -2367,6 +2410,8 @@ vxg_status vxg_plan_create_ex(vxg_ctx* ctx, const vxg_array* arrays, vxg_canonic
             in.candidate_batched[c] = plans[c]->batched;
             in.candidate_ms[c] = ms[c];
         }
+        in.selection = selection;
+        for (size_t c = 0; c < plans.size() && c < 2; c++) in.candidate_cost[c] = cost[c];
         in.create_ms = std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
     for (size_t c = 0; c < plans.size(); c++)

@@ -894,13 +894,14 @@ static size_t fsst_pad_lds() {
     return v;
 }
 
+// Called by every vxg_open after its device is selected: the mask is parsed once per process,
+// copied to each context's device (g_fsst_abl is per device).
 hipError_t fsst_diag_init() {
-    static const hipError_t st = [] {
+    static const uint32_t m = [] {
         const char* e = std::getenv("VXG_FSST_ABL");
-        const uint32_t m = e ? uint32_t(std::strtoul(e, nullptr, 10)) : 0u;
-        return m ? hipMemcpyToSymbol(HIP_SYMBOL(g_fsst_abl), &m, sizeof m) : hipSuccess;
+        return e ? uint32_t(std::strtoul(e, nullptr, 10)) : 0u;
     }();
-    return st;
+    return m ? hipMemcpyToSymbol(HIP_SYMBOL(g_fsst_abl), &m, sizeof m) : hipSuccess;
 }
 
 vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint32_t* err, hipStream_t s,
