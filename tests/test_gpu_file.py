@@ -110,7 +110,12 @@ def test_c5_full_size_plan(ctx, lineitem_file_bytes):
     plan.launch()
     res = plan.launch(sync=True)
     assert bench.c5_verify(res, range(n)) == f.row_count
-    ref = [(r.kind, [bytes(t.cpu().numpy()) for t in (r.values, r.views, r.data) if t is not None]) for r in res]
+    def content(r):  # the canonical's bytes: values, or views + each data buffer's used bytes
+        if r.kind == "primitive":
+            return [bytes(r.values.cpu().numpy())]
+        return [bytes(r.views.cpu().numpy())] + [b.tobytes() for b in r.buffers()]
+
+    ref = [content(r) for r in res]
     # oracle on a sample of chunks: each column's chunk arrays as written, canonicalized on the CPU
     from oracle_tree import view_bytes
     sample = (0, 45, n - 1)
@@ -133,8 +138,8 @@ def test_c5_full_size_plan(ctx, lineitem_file_bytes):
             p = A.Plan(dc.nodes, ctx)
         out = p.launch(sync=True)
         assert p.info()["batched"] == (mode == "1")
-        for (kind, bufs), r in zip(ref, out):
-            assert [bytes(t.cpu().numpy()) for t in (r.values, r.views, r.data) if t is not None] == bufs
+        for (name, _), want, r in zip(LI.COLUMNS, ref, out):
+            assert content(r) == want, (mode, name)
         p.close()
     f.close()
     assert time.perf_counter() - t0 < 120

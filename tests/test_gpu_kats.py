@@ -15,6 +15,7 @@ import pytest
 import vortex_amd.arrays as A
 import vortex_amd.encode as E
 from oracle_tree import canon, slice_any, view_bytes
+from vortex_amd._lib import VortexGpuError
 
 pytestmark = pytest.mark.gpu
 
@@ -188,7 +189,7 @@ def test_kat_runend_compute_on_gpu(ctx, case):
         return
     idx = np.array(k["take"], np.int64)
     if "expect_error" in k:
-        with pytest.raises(A.VortexError, match="OutOfBounds|out of bounds"):
+        with pytest.raises(VortexGpuError, match="OutOfBounds|out of bounds"):
             A.take(arr.to(_dev()), idx, ctx)
         return
     res = A.take(arr.to(_dev()), idx, ctx)
