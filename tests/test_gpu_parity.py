@@ -582,6 +582,33 @@ def _fsst_handmade(strings, symbols):
                   A.primitive(np.array(lens, np.int32)))
 
 
+def _fsst_onebyte(strings, alphabet):
+    """_fsst_handmade for a table of one-byte symbols (byte alphabet[i] = code i, any other byte
+    escaped), vectorised."""
+    lens = np.array([0 if s is None else len(s) for s in strings], np.int64)
+    heap = np.frombuffer(b"".join(s or b"" for s in strings), np.uint8)
+    lut = np.full(256, 255, np.int32)
+    lut[np.frombuffer(alphabet, np.uint8)] = np.arange(len(alphabet))
+    code = lut[heap]
+    esc = code == 255
+    width = 1 + esc.astype(np.int64)
+    pos = np.zeros(heap.size + 1, np.int64)
+    np.cumsum(width, out=pos[1:])
+    codes = np.zeros(int(pos[-1]), np.uint8)
+    codes[pos[:-1]] = code.astype(np.uint8)
+    codes[pos[:-1][esc] + 1] = heap[esc]
+    sb = np.zeros(len(strings) + 1, np.int64)
+    np.cumsum(lens, out=sb[1:])
+    coffs = pos[sb]
+    valid = np.array([s is not None for s in strings])
+    syms = [bytes([c]) for c in alphabet]
+    sym_u64 = np.array([int.from_bytes(y.ljust(8, b"\0"), "little") for y in syms], np.uint64)
+    code_vb = A.varbin(A.primitive(coffs.astype(np.int32)), A.primitive(codes), utf8=False,
+                       validity=None if valid.all() else valid)
+    return A.fsst(A.primitive(sym_u64), A.primitive(np.ones(len(syms), np.uint8)), code_vb,
+                  A.primitive(lens.astype(np.int32)))
+
+
 def _comment_strings(rng, n, vocab=40):
     words = [bytes(rng.integers(97, 123, rng.integers(2, 10)).astype(np.uint8)) for _ in range(vocab)]
     out = []
@@ -721,6 +748,66 @@ def test_fsst_long_strings_direct_path(ctx):
     rng = np.random.default_rng(1)
     strings = [bytes(rng.integers(97, 123, int(rng.integers(100, 600))).astype(np.uint8)) for _ in range(700)]
     assert_string_parity(E.encode_fsst(strings), ctx, strings)
+
+
+@pytest.mark.parametrize("escapes", [False, True])
+def test_fsst_wave_tile_geometry(ctx, escapes):
+    """The one-launch decode's geometry (K7w: 64-string wave tiles, 1024-string ranges, 64-range
+    look-back superblocks): one-byte symbols make tile t's code span 64 x its string length, so
+    staged tiles cover every code-window size (1-4 dwords per lane), tiles over the 1 KiB code
+    window or the 3 KiB image take the direct path next to staged ones inside one range (the
+    carried partial chunk is flushed first), lengths that shift the image alignment by every
+    residue, escapes in some tiles, a range that starts with a direct tile, and a partial last
+    tile -- over 2.3 superblocks of ranges."""
+    rng = np.random.default_rng(41 + escapes)
+    alphabet = b"abcdefghij "
+    pattern = [3, 5, 9, 13, 15, 17, 2, 40, 1, 7, 0, 11, 60, 4, 6, 8]  # one length per tile of a range
+    strings = []
+    for r in range(150):  # ranges: 150 x 1024 strings (3 superblocks, the last partial)
+        for t, L in enumerate(pattern[r % 3:] + pattern[:r % 3]):
+            for i in range(64):
+                Li = max(L + int(rng.integers(-1, 2)) * (i % 5 == 0), 0)
+                s = bytes(rng.choice(np.frombuffer(alphabet, np.uint8), Li))
+                if escapes and t % 3 == 1 and i % 29 == 3 and Li:
+                    s = s[:-1] + b"\xf7"  # not a symbol: escaped
+                strings.append(None if (i % 61 == 17) else s)
+    strings += [b"tail-strings"] * 45  # partial last tile and range
+    arr = _fsst_onebyte(strings, alphabet)
+    if escapes:
+        assert (arr.children[2].children[1].buffers[0] == 255).any()
+    assert_string_parity(arr, ctx, strings)
+
+
+def test_fsst_plan_replays_and_one_shots(ctx):
+    """K7w's look-back state carries over launches by tags: a plan replayed many times, two plans
+    over the same array alternated, one-shot canonicalize calls in between and a second plan
+    recorded after the first one's replays -- every output equal to the oracle's."""
+    import torch
+    rng = np.random.default_rng(77)
+    strings = _comment_strings(rng, 200_000, vocab=60)
+    arr = E.encode_fsst(strings)
+    dev = arr.to(torch_dev())
+    (rv, rh), _ = canon(arr)
+    p1 = V.Plan([dev], ctx)
+    p2 = V.Plan([A.chunked([arr, arr]).to(torch_dev())], ctx)
+    for k in range(6):
+        res = p1.launch(sync=True)[0]
+        assert res.numpy()[0].tobytes() == rv.tobytes(), k
+        assert res.buffers()[0].tobytes() == rh.tobytes(), k
+        if k % 2:
+            r2 = p2.launch(sync=True)[0]
+            v2 = r2.numpy()[0]
+            assert [b.tobytes() for b in r2.buffers()] == [rh.tobytes()] * 2
+            assert v2[: len(strings)].tobytes() == rv.tobytes()
+        if k % 3 == 2:
+            one = A.canonicalize(dev, ctx)
+            assert one.numpy()[0].tobytes() == rv.tobytes()
+    p1.close()
+    p3 = V.Plan([dev], ctx)
+    for _ in range(3):
+        assert p3.launch(sync=True)[0].numpy()[0].tobytes() == rv.tobytes()
+    p3.close()
+    p2.close()
 
 
 # ------------------------------------------------------------------ direct C-ABI entry points
