@@ -751,14 +751,12 @@ def test_fsst_long_strings_direct_path(ctx):
 
 
 @pytest.mark.parametrize("escapes", [False, True])
-def test_fsst_wave_tile_geometry(ctx, escapes):
-    """The one-launch decode's geometry (K7w: 64-string wave tiles, 1024-string ranges, 64-range
-    look-back superblocks): one-byte symbols make tile t's code span 64 x its string length, so
-    staged tiles cover every code-window size (1-4 dwords per lane), tiles over the 1 KiB code
-    window or the 3 KiB image take the direct path next to staged ones inside one range (the
-    carried partial chunk is flushed first), lengths that shift the image alignment by every
-    residue, escapes in some tiles, a range that starts with a direct tile, and a partial last
-    tile -- over 2.3 superblocks of ranges."""
+def test_fsst_tile_geometry(ctx, escapes):
+    """One-byte symbols make a tile's code span equal its decoded bytes: lengths that change
+    every 64 strings give 256-string tiles of every code-segment size (1-6 dwords per thread),
+    heap offsets of every alignment, escapes in some tiles and a partial last tile -- over 600
+    tiles, i.e. several pre-pass scan blocks (a tile's heap offset is its block's prefix plus the
+    tile records before it)."""
     rng = np.random.default_rng(41 + escapes)
     alphabet = b"abcdefghij "
     pattern = [3, 5, 9, 13, 15, 17, 2, 40, 1, 7, 0, 11, 60, 4, 6, 8]  # one length per tile of a range
@@ -779,9 +777,10 @@ def test_fsst_wave_tile_geometry(ctx, escapes):
 
 
 def test_fsst_plan_replays_and_one_shots(ctx):
-    """K7w's look-back state carries over launches by tags: a plan replayed many times, two plans
-    over the same array alternated, one-shot canonicalize calls in between and a second plan
-    recorded after the first one's replays -- every output equal to the oracle's."""
+    """The decode's scratch (pre-pass tile records, block totals) is rewritten by every launch: a
+    plan replayed many times, two plans over the same array alternated, one-shot canonicalize
+    calls in between and a second plan recorded after the first one's replays -- every output
+    equal to the oracle's."""
     import torch
     rng = np.random.default_rng(77)
     strings = _comment_strings(rng, 200_000, vocab=60)

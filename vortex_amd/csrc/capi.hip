@@ -1869,7 +1869,6 @@ static vxg_status status_of_err_word(uint32_t err) {
     if (err & kErrFsst) return set_error(VXG_ERR_INVALID_ARGUMENT, "FSST codes do not decode to uncompressed_lengths");
     if (err & kErrRoaring) return set_error(VXG_ERR_INVALID_SERDE, "RoaringBool buffer is not a croaring Native bitmap");
     if (err & kErrVarBin) return set_error(VXG_ERR_INVALID_ARGUMENT, "VarBin offsets out of range of the bytes");
-    if (err & kErrLookback) return set_error(VXG_ERR_ASSERTION_FAILED, "FSST decode: look-back state inconsistent");
     return set_error(VXG_ERR_ASSERTION_FAILED, "unknown device error bit");
 }
 

@@ -164,20 +164,6 @@ __device__ __forceinline__ int64_t wave_total64(int64_t v) {
     return int64_t(uint64_t(A) + (uint64_t(B) << 16) + (uint64_t(C) << 32));
 }
 
-// Exact wave-wide exclusive scan and total of one int64 per lane (mod 2^64), as wave_total64: three
-// 32-bit DPP scans of the 16 + 16 + 32-bit parts.
-__device__ __forceinline__ void wave_excl_scan64(int64_t v, int64_t& excl, int64_t& total) {
-    const uint64_t u = uint64_t(v);
-    const int a = wave_incl_scan(int(uint32_t(u) & 0xFFFFu));
-    const int b = wave_incl_scan(int(uint32_t(u) >> 16));
-    const int c = wave_incl_scan(int(uint32_t(u >> 32)));
-    const uint64_t incl = uint64_t(uint32_t(a)) + (uint64_t(uint32_t(b)) << 16) + (uint64_t(uint32_t(c)) << 32);
-    excl = int64_t(incl - u);
-    total = int64_t(uint64_t(uint32_t(__builtin_amdgcn_readlane(a, 63))) +
-                    (uint64_t(uint32_t(__builtin_amdgcn_readlane(b, 63))) << 16) +
-                    (uint64_t(uint32_t(__builtin_amdgcn_readlane(c, 63))) << 32));
-}
-
 // Exclusive block scan of one int32 per thread (kTile/64 waves); `ws` must not be reused
 // before the next barrier.
 __device__ __forceinline__ int block_excl_scan32(int v, int* ws, int& total) {
@@ -850,525 +836,10 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) v
     tile_run<OffAcc, LenAcc>(ch, in, L, err);
 }
 
-// ===================================================================================
-// K7w: the one-launch decode (no pre-pass).  Wave-tiled: a wave decodes a RANGE of 1024
-// consecutive strings as 16 tiles of 64 (lane = string), one tile's loads in flight while the
-// previous tile decodes, with no workgroup barrier inside the range.  Four ranges form a JOB (one
-// per wave of a 256-thread workgroup, which shares the chunk's symbol table in LDS); workgroups
-// take jobs w, w + G, ... of a grid G no larger than the chip holds at once.
-//
-// Output offsets without a pre-pass: each range publishes the sum of its lengths (its
-// aggregate) as soon as it has read them, and learns its heap offset from its predecessors'
-// aggregates (decoupled look-back, two levels so it never walks far): the ranges before it in
-// its 64-range superblock, plus one published total per earlier superblock (written by each
-// superblock's last range).  Every wait points at a lower range, and every lower range belongs to
-// a workgroup that is already resident (the grid fits the chip), so the chain always drains.
-// Entries are 8-byte {tag:22, value:42} granules written with one agent-scope (sc1) store and
-// polled with sc1 loads (MI355X_MICROARCH.md, inter-workgroup hand-off by data-tagged granules).
-// Tags instead of a reset: a range reads its own entry's old tag t and publishes t + 1; every
-// entry is written once per launch, so all entries share one tag between launches (the state
-// starts zeroed: a plan's is zeroed once at record time, a one-shot call's by a memset).  A wait
-// that outlasts kLbTimeout raises kErrLookback instead of hanging.
-//
-// A tile's codes are staged raw (16-byte aligned window; bytes outside the tile set to 0xFF, the
-// escape slot whose symbol is empty) and decoded code-parallel as in K7 (pass 1 lengths + wave
-// scan, pass 2 ORs into a zeroed LDS image); the image keeps the heap's 16-byte alignment and the
-// partial last chunk of a tile is carried into the next tile's image, so only a range's first and
-// last partial chunks are written bytewise.  Every store is an unconditional buffer store (lanes
-// out of range dropped by the resource bounds), so each tile issues a fixed number of memory
-// instructions and the next tile's loads are waited for without waiting for this tile's stores.
-// ===================================================================================
-namespace {
-#ifndef KW_STORE_POLICY
-#define KW_STORE_POLICY 2  // buffer store cache policy of the heap / view stores: 2 = nt, 0 = plain
-#endif
-constexpr int kWT = 64;                      // strings per wave tile
-constexpr int kRT = 32;                      // tiles per range at most (a launch picks rt <= kRT)
-constexpr int kJR = 4;                       // ranges per job (waves per workgroup)
-constexpr int kSB = 64;                      // ranges per look-back superblock
-constexpr int kWCode = 1024;                 // staged code window per tile (alignment shift included)
-constexpr int kWImg = 3072;                  // decoded bytes per tile
-constexpr int kImg = 16 + kWImg + 64;        // image: carry chunk + tile + slack (ORs / view reads past the end)
-constexpr int kImgChunks = kImg / 16;
-constexpr int kLbShift = 42;
-constexpr uint64_t kLbVal = (1ull << kLbShift) - 1;
-constexpr uint32_t kLbTagMask = (1u << 22) - 1;
-constexpr uint64_t kLbTimeout = 50'000'000;  // s_memrealtime ticks (100 MHz): 0.5 s
-static_assert(kWCode % 256 == 0 && kWCode / 256 <= 4, "at most 4 code dwords per lane");
-static_assert(4 * 64 * 16 >= kImg, "four 64-lane rounds of 16-byte chunks cover the image");
-
-struct alignas(16) WaveLds {
-    uint8_t codes[kWCode + 32];
-    uint32_t img[kImg / 4];
-    uint8_t lens8[kRT * kWT];      // the range's lengths, saturated at 255 (255: read the column)
-    uint8_t vbits[kRT * kWT / 8];  // the range's validity bits
-    int64_t ttot[kRT];             // each tile's sum of lengths
-    int64_t tout[kRT];             // heap offset of each direct-path tile (decoded after the range)
-};
-
-__device__ __forceinline__ uint64_t lb_ld(const uint64_t* p) {
-    return __hip_atomic_load((gptr<const uint64_t>)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void lb_st(uint64_t* p, uint64_t v) {
-    __hip_atomic_store((gptr<uint64_t>)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t lb_pack(uint32_t tag, int64_t v) {
-    return (uint64_t(tag) << kLbShift) | (uint64_t(v) & kLbVal);
-}
-
-// Sum of the values of p[0, cnt) once every entry carries `tag` (64 entries per poll round).
-__device__ __forceinline__ int64_t lb_sum(const uint64_t* p, uint32_t cnt, uint32_t tag, uint32_t* err) {
-    const uint32_t lane = threadIdx.x & 63u;
-    int64_t acc = 0;
-    for (uint32_t b = 0; b < cnt; b += 64) {
-        const uint32_t i = b + lane;
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        uint64_t x;
-        while (true) {
-            x = i < cnt ? lb_ld(p + i) : (uint64_t(tag) << kLbShift);
-            if (__ballot(uint32_t(x >> kLbShift) != tag) == 0) break;
-            if (__builtin_amdgcn_s_memrealtime() - t0 > kLbTimeout) {
-                if (lane == 0) __hip_atomic_fetch_or(err, kErrLookback, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                x = uint64_t(tag) << kLbShift;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(2);
-        }
-        acc += int64_t(x & kLbVal);
-    }
-    return wave_total64(acc);
-}
-
-// A wave tile's load issued one tile ahead: chunk `lane` of the tile's 16-byte aligned code
-// window (lengths and validity come from the range's LDS copy).
-struct WTile {
-    uint4 cx;
-};
-
-__device__ __forceinline__ uint32_t bcast32(uint32_t v, uint32_t l) { return __builtin_amdgcn_readlane(v, l); }
-__device__ __forceinline__ int64_t bcast64(int64_t v, uint32_t l) {
-    return int64_t(uint64_t(bcast32(uint32_t(uint64_t(v)), l)) | (uint64_t(bcast32(uint32_t(uint64_t(v) >> 32), l)) << 32));
-}
-
-__device__ __forceinline__ void wtile_issue(const FsstChunk& ch, int64_t cf, int64_t cl, WTile& w, uint32_t lane) {
-    const int cshift = int((reinterpret_cast<uintptr_t>(ch.codes) + uintptr_t(cf)) & 15);
-    const int64_t span = cl - cf;
-    const int win = span >= 0 && cshift + span <= kWCode ? int(cshift + span) : 0;
-    const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t*>(ch.codes + (cf - cshift)), short(0), (win + 15) & ~15, 0x00020000);
-    w.cx = as_uint4(__builtin_amdgcn_raw_buffer_load_b128(crs, 16 * lane, 0, 0));
-}
-
-// Sum of the lengths of strings [r0, r0 + 64 ntiles) (clamped at n): ntiles per lane, 4 in flight;
-// each length is also kept in lens8 (saturated at 255).
-template <class LenAcc>
-__device__ __forceinline__ int64_t range_sum(const LenAcc& lens, uint64_t r0, uint64_t n, uint32_t ntiles, uint8_t* lens8,
-                                             int64_t* ttot) {
-    const uint32_t lane = threadIdx.x & 63u;
-    int64_t acc = 0;
-    for (uint32_t b = 0; b < ntiles; b += 4) {
-        TileLen<LenAcc> t[4];
-        bool v[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const uint64_t first = r0 + 64ull * uint64_t(b + k) < n ? r0 + 64ull * uint64_t(b + k) : r0;
-            v[k] = b + k < ntiles && r0 + 64ull * uint64_t(b + k) + lane < n;
-            t[k].issue(lens, first, first + lane < n ? lane : uint32_t(n - 1 - first));
-        }
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const int64_t x = v[k] ? t[k].value(lens) : 0;
-            acc += x;
-            if (b + k < ntiles) lens8[64 * (b + k) + lane] = uint8_t(uint64_t(x) < 255 ? x : 255);
-            const int64_t tt = wave_total64(x);
-            if (b + k < ntiles && lane == 0) ttot[b + k] = tt;
-        }
-    }
-    return acc;
-}
-
-// Pass 1 / scan / pass 2 of one staged tile: the tile's codes are codes[lo, hi) of the window
-// (bytes outside it are 0xFF), lane t takes window bytes [4 ND t, 4 ND (t + 1)); decoded bytes go to
-// image byte `base` on.  Returns false (nothing written) if the codes do not decode to `ttot`.
-template <int ND>
-__device__ __forceinline__ bool wave_segments(const uint8_t* __restrict__ codes, int lo, int hi,
-                                              const uint64_t* __restrict__ s_sym, const uint8_t* __restrict__ s_len,
-                                              uint32_t* __restrict__ img, int base, int ttot, int lane) {
-    const int s0 = lane * 4 * ND;
-    const bool act = s0 < hi;
-    const uint32_t* __restrict__ c32 = reinterpret_cast<const uint32_t*>(codes);
-    uint32_t pk[ND];
-    uint32_t sum8 = 0, any = 0;
-#pragma unroll
-    for (int d = 0; d < ND; d++) {
-        const uint32_t x = c32[(s0 >> 2) + d];
-        uint32_t k = 0;
-#pragma unroll
-        for (int j = 0; j < 4; j++) k |= uint32_t(s_len[(x >> (8 * j)) & 0xFFu]) << (8 * j + 3);
-        // bytes of the dword outside [lo, hi) have no length
-        const int p = s0 + 4 * d;
-        const int lb = min(max(lo - p, 0), 4), hb = min(max(hi - p, 0), 4);
-        const uint32_t keep = uint32_t((0xFFFFFFFFull << (8 * lb)) & ((1ull << (8 * hb)) - 1));
-        pk[d] = act ? (k & keep) : 0u;
-        any |= pk[d];
-        sum8 = __builtin_amdgcn_sad_u8(pk[d], 0u, sum8);
-    }
-    const bool fast = __ballot((any & 0x80808080u) != 0) == 0;  // no escape in the tile
-    if (!fast) {
-        sum8 = 0;
-        if (act) {
-            bool skp = false;  // is the current byte the literal of an escape?
-            if (s0 > lo && codes[s0 - 1] == 255) {
-                int r = 0;
-                for (int p = s0 - 1; p >= lo && codes[p] == 255; --p) ++r;
-                skp = r & 1;
-            }
-#pragma unroll
-            for (int d = 0; d < ND; d++) {
-                const uint32_t x = c32[(s0 >> 2) + d];
-                uint32_t k = 0;
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const int p = s0 + 4 * d + j;
-                    const uint32_t c = (x >> (8 * j)) & 0xFFu;
-                    const bool emit = p >= lo && p < hi && !skp;
-                    skp = emit && c == 255;
-                    const uint32_t L = emit ? (c == 255 ? 1u : uint32_t(s_len[c])) : 0u;
-                    k |= L << (8 * j + 3);
-                }
-                pk[d] = k;
-                sum8 = __builtin_amdgcn_sad_u8(k, 0u, sum8);
-            }
-        }
-    }
-    const int v = int(sum8 >> 3);
-    const int incl = wave_incl_scan(v);
-    const int total = __builtin_amdgcn_readlane(incl, 63);
-    if (total != ttot) return false;
-    if (!act) return true;
-    uint32_t o8 = uint32_t(base + incl - v) << 3;  // bit position in the image
-    auto put = [&](uint64_t m, uint32_t L8) {
-        const uint32_t sh = o8 & 24u, w = o8 >> 5;
-        const uint64_t lo64 = m << sh;
-        const uint32_t hi32 = uint32_t((m >> 32) << sh >> 32);
-        __hip_atomic_fetch_or(&img[w], uint32_t(lo64), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        __hip_atomic_fetch_or(&img[w + 1], uint32_t(lo64 >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        __hip_atomic_fetch_or(&img[w + 2], hi32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        o8 += L8;
-    };
-    if (fast) {
-        uint32_t xn = c32[s0 >> 2];
-#pragma unroll
-        for (int d = 0; d < ND; d++) {
-            const uint32_t x = xn;
-            uint64_t sy[4];
-#pragma unroll
-            for (int j = 0; j < 4; j++) sy[j] = s_sym[(x >> (8 * j)) & 0xFFu];
-            if (d + 1 < ND) xn = c32[(s0 >> 2) + d + 1];
-#pragma unroll
-            for (int j = 0; j < 4; j++) put(sy[j], (pk[d] >> (8 * j)) & 0xFFu);
-        }
-    } else {
-#pragma unroll
-        for (int d = 0; d < ND; d++) {
-            const uint32_t x = c32[(s0 >> 2) + d];
-            const uint32_t after = codes[s0 + 4 * d + 4];  // literal of an escape in byte 3
-            uint64_t sy[4];
-#pragma unroll
-            for (int j = 0; j < 4; j++) sy[j] = s_sym[(x >> (8 * j)) & 0xFFu];
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const uint32_t c = (x >> (8 * j)) & 0xFFu;
-                const uint32_t L8 = (pk[d] >> (8 * j)) & 0xFFu;
-                const uint64_t lit = j < 3 ? ((x >> (8 * j + 8)) & 0xFFu) : after;
-                put(L8 ? (c == 255 ? lit : sy[j]) : 0ull, L8);
-            }
-        }
-    }
-    return true;
-}
-
-// Bytes of v (16) where byte j is kept if lo <= j < hi, else 0xFF.
-__device__ __forceinline__ uint4 fill_outside(uint4 v, int lo, int hi) {
-    auto f = [&](uint32_t w, int b) {
-        const int l = min(max(lo - b, 0), 4), h = min(max(hi - b, 0), 4);
-        const uint32_t keep = uint32_t((0xFFFFFFFFull << (8 * l)) & ((1ull << (8 * h)) - 1));
-        return (w & keep) | ~keep;
-    };
-    return make_uint4(f(v.x, 0), f(v.y, 4), f(v.z, 8), f(v.w, 12));
-}
-
-// The direct path of a tile (too large to stage, or lengths of 255 and up), run after the
-// range's staged tiles (out of line: its registers do not weigh on the staged loop): every string
-// is decoded straight into HBM at its offset (its codes [offs[i], offs[i+1]) must decode to exactly
-// lengths[i] bytes) and its view built from HBM.  The staged tile before it wrote its own partial
-// last chunk bytewise, the one after it starts bytewise, so the bytes of the tile are its own.
-template <class OffAcc>
-__device__ __noinline__ void direct_tile(const uint8_t* codes, uint8_t* heap, uint8_t* views, IntCol offs, IntCol lens,
-                                         uint64_t n, uint32_t bidx, uint64_t first, uint32_t t, int64_t out,
-                                         const uint8_t* __restrict__ vbits, const uint64_t* __restrict__ s_sym,
-                                         const uint8_t* __restrict__ s_len, uint32_t* __restrict__ err) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t i = first + lane;
-    const bool live = i < n;
-    const int64_t my_len = live ? intcol_get(lens, i) : 0;
-    int64_t my_rel = 0, tot = 0;
-    wave_excl_scan64(my_len, my_rel, tot);
-    const bool valid = live && ((vbits[(64 * t + lane) >> 3] >> (lane & 7)) & 1u);
-    const OffAcc code_offs(offs);
-    const int64_t c0 = live ? code_offs(i) : 0, c1 = live ? code_offs(i + 1) : 0;
-    int64_t o = out + my_rel;
-    const int64_t o_start = o, o_end = o + my_len;
-    for (int64_t kk = c0; kk < c1; kk++) {
-        const uint8_t c = gload(codes + kk);
-        if (c == 255) {
-            ++kk;
-            if (o < o_end) gstore(heap + o, gload(codes + kk));
-            o++;
-        } else {
-            const uint64_t sym = s_sym[c];
-            const int Ln = s_len[c];
-            for (int b = 0; b < Ln; b++)
-                if (o + b < o_end) gstore(heap + o + b, uint8_t(sym >> (8 * b)));
-            o += Ln;
-        }
-    }
-    if (o != o_end) __hip_atomic_fetch_or(err, kErrFsst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t vlen = valid ? uint32_t(my_len) : 0u;
-    const uint8_t* hp = heap + o_start;
-    const uint4 vw = valid ? build_view(vlen, uint32_t(o_start), bidx,
-                                        [&](int b) { return uint32_t(b) < vlen ? gload(hp + b) : uint8_t(0); })
-                           : make_uint4(0, 0, 0, 0);
-    if (live) nt_store(reinterpret_cast<uint4*>(views) + i, vw);
-}
-
-// One wave's range r (chunk-local) of chunk ch.
-template <class OffAcc, class LenAcc>
-__device__ __forceinline__ void decode_range(const FsstChunk& ch, uint32_t r, uint32_t rt, uint32_t n_ranges, uint32_t n_slots,
-                                             WaveLds& L, const uint64_t* __restrict__ s_sym,
-                                             const uint8_t* __restrict__ s_len, uint32_t* __restrict__ err) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t n = ch.n;
-    const uint64_t r0 = uint64_t(r) * rt * kWT;
-    const uint32_t ntiles = uint32_t(min<uint64_t>(rt, (n - r0 + kWT - 1) / kWT));
-    const OffAcc offs(ch.offs);
-    const LenAcc lens(ch.lens);
-    uint64_t* const agg = ch.lb;
-    uint64_t* const sup = ch.lb + n_slots;
-    // (1) the own entry's old tag, the tile boundaries' code offsets (lane t: offs of string
-    // r0 + 64 t, t <= ntiles) and the range's lengths, all in flight together
-    const uint64_t old = lb_ld(agg + r);
-    const int64_t offv = offs(min<uint64_t>(r0 + 64ull * min(lane, ntiles), n));
-    const int64_t my_agg = wave_total64(range_sum(lens, r0, n, ntiles, L.lens8, L.ttot));
-    {  // the range's validity bits (bytes r0/8 ...; r0 is a multiple of 64)
-        const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<uint8_t*>(ch.validity), short(0), ch.validity ? int((n + 7) >> 3) : 0, 0x00020000);
-        for (uint32_t q0 = 0; q0 < 8 * ntiles; q0 += 64) {
-            const uint32_t vb = __builtin_amdgcn_raw_buffer_load_b8(vrs, uint32_t(r0 >> 3) + q0 + lane, 0, 0);
-            if (q0 + lane < 8 * ntiles) L.vbits[q0 + lane] = uint8_t(ch.validity ? vb : 0xFFu);
-        }
-    }
-    const uint32_t tag = (uint32_t(old >> kLbShift) + 1u) & kLbTagMask;
-    if (lane == 0) lb_st(agg + r, lb_pack(tag, my_agg));
-    // which tiles take the direct path: a length of 255 or more (saturated in lens8), a code
-    // window over kWCode, or more decoded bytes than the image holds
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    uint32_t dmask = 0;
-    for (uint32_t t = 0; t < ntiles; t++) {
-        const bool any_bad = __ballot(L.lens8[64 * t + lane] == 255) != 0;
-        const int64_t cf = bcast64(offv, t), span = bcast64(offv, t + 1) - cf;
-        const int cshift = int((reinterpret_cast<uintptr_t>(ch.codes) + uintptr_t(cf)) & 15);
-        const bool ok = !any_bad && span >= 0 && cshift + span <= kWCode && L.ttot[t] <= kWImg;
-        dmask |= ok ? 0u : (1u << t);
-    }
-    // (2) tile 0's codes, then the heap offset of the range from the predecessors
-    WTile w0;
-    wtile_issue(ch, bcast64(offv, 0), bcast64(offv, 1), w0, lane);
-    const uint32_t k = r / kSB, rb = k * kSB;
-    const int64_t in_sb = lb_sum(agg + rb, r - rb, tag, err);
-    if (r == min(rb + kSB - 1, n_ranges - 1) && lane == 0) lb_st(sup + k, lb_pack(tag, in_sb + my_agg));
-    int64_t out = lb_sum(sup, k, tag, err) + in_sb;  // heap offset of the tile's first byte
-    uint8_t* const heap = ch.heap;
-    uint8_t* const img8 = reinterpret_cast<uint8_t*>(L.img);
-    uint4* const img16 = reinterpret_cast<uint4*>(L.img);
-    int hl = int(out & 15);  // image bytes below hl belong to another range (head): written bytewise
-    uint32_t errbits = 0;    // device errors of the range's staged tiles (wave-uniform)
-    // Tile t's code window into L.codes: the raw 16-byte chunks, bytes outside [cshift, hi) ->
-    // 0xFF (escape slot: empty symbol, and pass 1 masks their lengths), plus one all-0xFF chunk
-    // past them for the lane whose segment straddles the end.  Tiles that will not be staged
-    // write nothing.
-    auto stage = [&](uint32_t t, const WTile& w, uint32_t lane) {
-        const int64_t cf = bcast64(offv, t), span = bcast64(offv, t + 1) - cf;
-        const int cshift = int((reinterpret_cast<uintptr_t>(ch.codes) + uintptr_t(cf)) & 15);
-        if (span < 0 || cshift + span > kWCode) return;
-        const int hi = cshift + int(span), nch = (hi + 15) >> 4;
-        if (int(lane) <= nch)
-            *reinterpret_cast<uint4*>(L.codes + 16 * lane) =
-                int(lane) < nch ? fill_outside(w.cx, cshift - 16 * int(lane), hi - 16 * int(lane))
-                                : make_uint4(~0u, ~0u, ~0u, ~0u);
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    };
-    if (!(dmask & 1u)) stage(0, w0, lane);
-    // Tile t: its codes are in L.codes (staged by the previous step); the next tile's code chunk is
-    // requested first and staged last, after this tile's stores -- so the wait for it counts those
-    // stores instead of waiting for them, and no in-flight register crosses an iteration.
-    for (uint32_t t = 0; t < ntiles; t++) {
-        // the lane index made opaque per tile: address arithmetic derived from it is recomputed
-        // inside the loop instead of being hoisted (the hoisted copies did not fit the VGPR
-        // budget and were spilled)
-        uint32_t lane = threadIdx.x & 63u;
-        asm volatile("" : "+v"(lane));
-        const uint64_t first = r0 + 64ull * t;
-        const int64_t cf = bcast64(offv, t), cl = bcast64(offv, t + 1);
-        const uint32_t tn = t + 1 < ntiles ? t + 1 : t;  // (the last tile re-requests its own: a fixed count)
-        WTile nx;
-        wtile_issue(ch, bcast64(offv, tn), bcast64(offv, tn + 1), nx, lane);
-        const bool more = t + 1 < ntiles;
-        const bool staged = !((dmask >> t) & 1u);
-        const bool next_direct = more && ((dmask >> (t + 1)) & 1u);
-        const bool live = first + lane < n;
-        const int64_t my_len = live ? int64_t(L.lens8[64 * t + lane]) : 0;  // (< 255 on staged tiles)
-        const int lenv = int(my_len);
-        const int incl = wave_incl_scan(lenv);
-        const int ttot = __builtin_amdgcn_readlane(incl, 63);
-        const int my_rel = incl - lenv;
-        const int cshift = int((reinterpret_cast<uintptr_t>(ch.codes) + uintptr_t(cf)) & 15);
-        const int64_t span = cl - cf;
-        const int hs = int(out & 15);
-        const bool last = !more || next_direct;  // the partial last chunk is written bytewise
-        const bool valid = live && ((L.vbits[(64 * t + lane) >> 3] >> (lane & 7)) & 1u);
-        // views of the tile: 16 * live rows from views[first]
-        const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(
-            ch.views + 16 * first, short(0), int(16 * min<uint64_t>(64, n - first)), 0x00020000);
-        if (staged) {
-            const int hi = cshift + int(span);
-            bool ok;
-            switch ((hi + 255) >> 8) {
-            case 0:
-            case 1: ok = wave_segments<1>(L.codes, cshift, hi, s_sym, s_len, L.img, hs, ttot, int(lane)); break;
-            case 2: ok = wave_segments<2>(L.codes, cshift, hi, s_sym, s_len, L.img, hs, ttot, int(lane)); break;
-            case 3: ok = wave_segments<3>(L.codes, cshift, hi, s_sym, s_len, L.img, hs, ttot, int(lane)); break;
-            default: ok = wave_segments<4>(L.codes, cshift, hi, s_sym, s_len, L.img, hs, ttot, int(lane)); break;
-            }
-            errbits |= ok ? 0u : kErrFsst;  // reported once per range
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            // views from the image
-            const uint4 vw = valid ? lds_view(L.img, hs + my_rel, uint32_t(my_len), uint32_t(out + my_rel), ch.bidx)
-                                   : make_uint4(0, 0, 0, 0);
-            __builtin_amdgcn_raw_buffer_store_b128(
-                (unsigned int __attribute__((ext_vector_type(4)))){vw.x, vw.y, vw.z, vw.w}, vrs, 16 * lane, 0, KW_STORE_POLICY);
-            // copy-out: full 16-byte chunks [q0, qb) of the image (chunk 0 holds the carry) as
-            // four unconditional rounds; chunk 0 of a range's head and the range's last partial
-            // chunk bytewise; the partial chunk qb carried into the next tile's chunk 0
-            const int end = hs + ttot, qb = end >> 4;
-            const int q0 = hl > 0 ? 1 : 0;
-            const __amdgpu_buffer_rsrc_t hrs = __builtin_amdgcn_make_buffer_rsrc(heap + (out - hs), short(0), 16 * qb,
-                                                                                 0x00020000);
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                const int q = 64 * i + int(lane);
-                const uint4 x = img16[q < kImgChunks ? q : kImgChunks - 1];
-                __builtin_amdgcn_raw_buffer_store_b128((unsigned int __attribute__((ext_vector_type(4)))){x.x, x.y, x.z, x.w},
-                                                       hrs, q >= q0 ? 16 * q : 0x7FFFFFF0, 0, KW_STORE_POLICY);
-            }
-            // bytewise: lanes 0-15 the head chunk's bytes [hl, 16) once chunk 0 is complete;
-            // lanes 16-31 the range's last partial chunk [max(16 qb, hl), end)
-            {
-                const int a = lane < 16 ? int(lane) : 16 * qb + int(lane) - 16;
-                const bool wr = lane < 16 ? (hl > 0 && qb >= 1 && a >= hl)
-                                          : (lane < 32 && last && a < end && a >= hl && a >= 16 * qb);
-                const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(heap + (out - hs), short(0),
-                                                                                     end, 0x00020000);
-                __builtin_amdgcn_raw_buffer_store_b8(img8[a < kImg ? a : 0], brs, wr ? a : 0x7FFFFFF0, 0, 0);
-            }
-            // image back to zero except the carry: chunks [1, qb] zeroed, chunk qb moved to 0
-            const uint4 tail = img16[qb];
-            for (int q = 1 + int(lane); q <= qb; q += 64) img16[q] = make_uint4(0, 0, 0, 0);
-            if (lane == 0) img16[0] = last ? make_uint4(0, 0, 0, 0) : tail;
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-            hl = qb == 0 ? hl : 0;
-            out += ttot;
-        } else {  // decoded after the loop, from this offset
-            if (lane == 0) L.tout[t] = out;
-            out += L.ttot[t];
-            hl = int(out & 15);
-        }
-        if (more && !next_direct) stage(t + 1, nx, lane);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    for (uint32_t m = dmask; m; m &= m - 1) {
-        const uint32_t t = uint32_t(__builtin_ctz(m));
-        direct_tile<OffAcc>(ch.codes, ch.heap, ch.views, ch.offs, ch.lens, n, ch.bidx, r0 + 64ull * t, t, L.tout[t],
-                            L.vbits, s_sym, s_len, err);
-    }
-    if (errbits && lane == 0) __hip_atomic_fetch_or(err, errbits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-}  // namespace
-
-#ifndef KW_WAVES
-#define KW_WAVES 5
-#endif
-template <class OffAcc, class LenAcc, bool EXT>
-__global__ __launch_bounds__(kWT * kJR) __attribute__((amdgpu_waves_per_eu(KW_WAVES, 8))) void fsst_decode_w(
-    FsstTable tab, uint64_t n_jobs, uint32_t rt, const uint32_t* __restrict__ job_chunk, uint32_t* __restrict__ err) {
-    __shared__ uint64_t s_sym[256];
-    __shared__ uint8_t s_len[256];
-    __shared__ WaveLds wl[kJR];
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63u;
-    WaveLds& L = wl[wave];
-    for (int q = int(lane); q < kImgChunks; q += 64) reinterpret_cast<uint4*>(L.img)[q] = make_uint4(0, 0, 0, 0);
-    uint32_t have = ~0u;
-    for (uint64_t j = blockIdx.x; j < n_jobs; j += gridDim.x) {
-        uint32_t ci;
-        if constexpr (EXT) {
-            ci = __builtin_amdgcn_readfirstlane(job_chunk[j]);
-        } else {
-            uint32_t lo = 0, hi = tab.n;
-            while (hi - lo > 1) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (tab.c[mid].first_job <= j) lo = mid; else hi = mid;
-            }
-            ci = lo;
-        }
-        const FsstChunk& ch = EXT ? tab.ext[ci] : tab.c[ci];
-        if (ci != have) {  // workgroup-uniform
-            uint64_t sym_v;
-            uint32_t sl;
-            __syncthreads();  // every wave is done with the previous table
-            symbol_load(ch, sym_v, sl);
-            DecLds D{};
-            D.s_sym = s_sym;
-            D.s_len = s_len;
-            symbol_store(ch, D, sym_v, sl, err);
-            __syncthreads();
-            have = ci;
-        }
-        const uint32_t n_ranges = uint32_t((ch.n + uint64_t(rt) * kWT - 1) / (uint64_t(rt) * kWT));
-        const uint32_t n_slots = (n_ranges + kJR - 1) / kJR * kJR;
-        const uint32_t r = uint32_t(j - ch.first_job) * kJR + wave;
-        if (r < n_ranges) decode_range<OffAcc, LenAcc>(ch, r, rt, n_ranges, n_slots, L, s_sym, s_len, err);
-    }
-}
-
-// Ranges of a chunk of n strings at rt tiles per range, rounded up to whole jobs.
-static uint64_t fsst_range_slots(uint64_t n, uint32_t rt) {
-    const uint64_t ranges = (n + uint64_t(rt) * kWT - 1) / (uint64_t(rt) * kWT);
-    return (ranges + kJR - 1) / kJR * kJR;
-}
-// Look-back entries of one chunk: a slot per range + one per superblock (rt = 1: the most).
-static uint64_t fsst_lb_entries(uint64_t n, uint32_t rt = 1) {
-    const uint64_t slots = fsst_range_slots(n, rt);
-    return slots + (slots + kSB - 1) / kSB;
-}
-
 uint64_t fsst_scratch_bytes(uint64_t n) {
-    // two-kernel form: tile prefixes + scan-block totals + tile code ends; one-launch form: the
-    // look-back state
+    // tile prefixes + scan-block totals + tile code ends
     const uint64_t n_tiles = (n + kTS - 1) / kTS;
-    const uint64_t two = (2 * n_tiles + (n_tiles + kScanTiles - 1) / kScanTiles + 2) * sizeof(int64_t);
-    const uint64_t one = (fsst_lb_entries(n) + 2) * sizeof(uint64_t);
-    return two > one ? two : one;
+    return (2 * n_tiles + (n_tiles + kScanTiles - 1) / kScanTiles + 2) * sizeof(int64_t);
 }
 
 uint64_t fsst_batch_scratch_bytes(const FsstChunk* chunks, size_t n_chunks) {
@@ -1433,140 +904,6 @@ hipError_t fsst_diag_init() {
     return m ? hipMemcpyToSymbol(HIP_SYMBOL(g_fsst_abl), &m, sizeof m) : hipSuccess;
 }
 
-// VXG_FSST_V1=1 (read once): the two-kernel form (pre-pass + per-tile decode) instead of K7w (A/B).
-static bool fsst_v1() {
-    static const bool v = [] {
-        const char* e = std::getenv("VXG_FSST_V1");
-        return e && e[0] == '1';
-    }();
-    return v;
-}
-
-// Workgroups of `fn` the device holds at once (the persistent grid's bound).
-template <class F>
-static uint64_t resident_groups(F fn) {
-    int dev = 0, cus = 0, per = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        return 256;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reinterpret_cast<const void*>(fn), kWT * kJR, 0) != hipSuccess ||
-        per < 1)
-        per = 1;
-    return uint64_t(cus) * uint64_t(per);
-}
-
-// Resident workgroups of the one-launch decode (every instance has the same resources).
-static uint64_t fsst_w_capacity() {
-    static const uint64_t c = resident_groups(&fsst_decode_w<PlainCol<4>, PlainCol<4>, false>);
-    return c;
-}
-// VXG_FSST_RT: tiles per range forced (1..16, diagnostics; read once).
-static uint32_t fsst_rt_env() {
-    static const uint32_t v = [] {
-        const char* e = std::getenv("VXG_FSST_RT");
-        const long x = e ? std::strtol(e, nullptr, 10) : 0;
-        return uint32_t(x >= 1 && x <= kRT ? x : 0);
-    }();
-    return v;
-}
-
-#define FSST_TRY(expr)                  \
-    do {                                \
-        const vxg_status st_ = (expr);  \
-        if (st_ != VXG_OK) return st_;  \
-    } while (0)
-
-static vxg_status launch_fsst_w(std::vector<FsstChunk>& chunks, void* scratch, uint32_t* err, hipStream_t s, DevTables* dt) {
-    std::stable_sort(chunks.begin(), chunks.end(), [](const FsstChunk& a, const FsstChunk& b) {
-        return std::make_pair(acc_kind(a.offs), acc_kind(a.lens)) < std::make_pair(acc_kind(b.offs), acc_kind(b.lens));
-    });
-    uint64_t* lb_all = static_cast<uint64_t*>(scratch);  // one-shot: zeroed below
-    size_t i = 0;
-    while (i < chunks.size()) {
-        FsstTable tab{};
-        size_t j = i, live = 0;
-        const auto key = std::make_pair(acc_kind(chunks[i].offs), acc_kind(chunks[i].lens));
-        while (j < chunks.size() && (dt || j - i < size_t(kFsstArgChunks)) &&
-               std::make_pair(acc_kind(chunks[j].offs), acc_kind(chunks[j].lens)) == key)
-            live += chunks[j++].n != 0;
-        FsstChunk* cs = tab.c;
-        if (live > size_t(kFsstArgChunks)) {
-            FsstChunk* host;
-            FSST_TRY(dt->table(live, &host, &tab.ext));
-            cs = host;
-        }
-        // tiles per range: the shortest ranges whose jobs all fit the chip at once (one job per
-        // resident workgroup, no second round), at most kRT; small tables -- a sharded scan's few
-        // chunks -- take short ranges
-        uint64_t tiles = 0;
-        for (size_t k = i; k < j; k++) tiles += (chunks[k].n + kWT - 1) / kWT;
-        const uint64_t cap = fsst_w_capacity();
-        uint32_t rt = uint32_t(std::min<uint64_t>(kRT, std::max<uint64_t>(1, (tiles + cap * kJR - 1) / (cap * kJR))));
-        auto jobs_at = [&](uint32_t r) {
-            uint64_t q = 0;
-            for (size_t k = i; k < j; k++) q += fsst_range_slots(chunks[k].n, r) / kJR;
-            return q;
-        };
-        while (rt < uint32_t(kRT) && jobs_at(rt) > cap) rt++;
-        if (const uint32_t e = fsst_rt_env()) rt = e;
-        uint64_t jobs = 0, entries = 0;
-        for (size_t k = i; k < j; k++) {
-            if (chunks[k].n == 0) continue;
-            FsstChunk& c = cs[tab.n++];
-            c = chunks[k];
-            c.first_job = jobs;
-            jobs += fsst_range_slots(c.n, rt) / kJR;
-            entries += fsst_lb_entries(c.n, rt);
-        }
-        if (tab.n) {
-            // look-back state: a plan's lives with the plan (zeroed once, tags carry it across
-            // replays); a one-shot launch's is zeroed here
-            uint64_t* lb;
-            if (dt) {
-                uint64_t* host_lb;
-                const uint64_t* dev_lb;
-                FSST_TRY(dt->table(entries, &host_lb, &dev_lb));
-                lb = const_cast<uint64_t*>(dev_lb);
-            } else {
-                lb = lb_all;
-                lb_all += entries;
-                FSST_TRY(hip_check(hipMemsetAsync(lb, 0, entries * sizeof(uint64_t), s), "fsst look-back reset"));
-            }
-            for (uint32_t k = 0; k < tab.n; k++) {
-                cs[k].lb = lb;
-                lb += fsst_lb_entries(cs[k].n, rt);
-            }
-            const uint32_t* job_chunk = nullptr;
-            if (tab.ext) {
-                uint32_t* host_map;
-                FSST_TRY(dt->table(jobs, &host_map, &job_chunk));
-                for (uint32_t k = 0; k < tab.n; k++) {
-                    const uint64_t nj = fsst_range_slots(cs[k].n, rt) / kJR;
-                    for (uint64_t q = 0; q < nj; q++) host_map[cs[k].first_job + q] = k;
-                }
-            }
-            bool ok = true;
-            with_acc(key.first, [&](auto* oa) {
-                ok = with_acc(key.second, [&](auto* la) {
-                    using OA = std::remove_pointer_t<decltype(oa)>;
-                    using LA = std::remove_pointer_t<decltype(la)>;
-                    auto go = [&](auto ext) {
-                        constexpr bool X = decltype(ext)::value;
-                        auto* fn = &fsst_decode_w<OA, LA, X>;
-                        const uint64_t grid = std::min<uint64_t>(jobs, resident_groups(fn));
-                        hipLaunchKernelGGL(fn, dim3(unsigned(grid)), dim3(kWT * kJR), 0, s, tab, jobs, rt, job_chunk, err);
-                    };
-                    if (tab.ext) go(std::true_type{});
-                    else go(std::false_type{});
-                });
-            });
-            if (!ok) return set_error(VXG_ERR_MISMATCHED_TYPES, "FSST accessor");
-            FSST_TRY(hip_check(hipGetLastError(), "fsst decode"));
-        }
-        i = j;
-    }
-    return VXG_OK;
-}
-
 vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint32_t* err, hipStream_t s,
                              DevTables* dt) {
     for (const FsstChunk& c : chunks) {
@@ -1577,7 +914,6 @@ vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint
             return set_error(VXG_ERR_MISMATCHED_TYPES, "FSST offsets/lengths must be 1/2/4/8-byte integers "
                                                         "(packed: 32/64-bit)");
     }
-    if (!fsst_v1()) return launch_fsst_w(chunks, scratch, err, s, dt);
     std::stable_sort(chunks.begin(), chunks.end(),
                      [](const FsstChunk& a, const FsstChunk& b) { return fsst_key(a) < fsst_key(b); });
     int64_t* tiles_all = static_cast<int64_t*>(scratch);

@@ -103,7 +103,7 @@ extern const double kIF10d[24];
 
 // Device error word bits (set by kernels, read by vxg_check via vxg_stream_sync).
 enum : uint32_t { kErrTakeOOB = 1u, kErrPatchOOB = 2u, kErrRunEnd = 4u, kErrFsst = 8u, kErrRoaring = 16u, kErrVarBin = 32u,
-                  kErrPatchOrder = 64u, kErrLookback = 128u };
+                  kErrPatchOrder = 64u };
 
 struct Ctx {
     int device = 0;
@@ -403,24 +403,23 @@ struct FsstChunk {
     IntCol lens;              // uncompressed lengths (n)
     uint64_t n;
     uint64_t heap_len;        // decoded bytes (sum of the lengths) if known, else 0: picks the LDS budget
-    uint64_t first_tile;      // launch-local (two-kernel form): first decode workgroup /
+    uint64_t first_tile;      // launch-local: first decode workgroup (a tile of 256 strings) /
     uint64_t first_scan;      //               first pre-pass workgroup
-    uint64_t first_job;       // launch-local (one-launch form): first job (4 ranges of 1024 strings)
-    uint64_t* lb;             // one-launch form: the chunk's look-back state (ranges, then superblocks)
     uint32_t n_symbols;
     uint32_t bidx;            // buffer_index of non-inlined views
 };
-constexpr int kFsstArgChunks = 22;
+constexpr int kFsstArgChunks = 24;
 struct FsstTable {
     FsstChunk c[kFsstArgChunks];
     uint32_t n;
     const FsstChunk* ext;  // device table of n entries (plans), or null
 };
-// Scratch for a set of chunks (tile prefixes + scan-block totals).
+// Scratch for a set of chunks (tile prefixes + scan-block totals + tile code ends).
 uint64_t fsst_scratch_bytes(uint64_t n);
 uint64_t fsst_batch_scratch_bytes(const FsstChunk* chunks, size_t n_chunks);
 // Decode every chunk: grouped by accessor kinds, kFsstArgChunks per launch pair (pre-pass +
-// decode).  `scratch` >= fsst_batch_scratch_bytes.
+// decode; a recorded plan's group over a device table is one pair).  `scratch` >=
+// fsst_batch_scratch_bytes.
 // The FSST decode's diagnostics mask (VXG_FSST_ABL, read once per process) into its __constant__;
 // called by vxg_open.
 hipError_t fsst_diag_init();
