@@ -1065,6 +1065,56 @@ def test_plan_graph_replay_matches_direct(ctx):
     plan.close()
 
 
+@pytest.mark.parametrize("fuse", ["1", "0"])
+def test_plan_fused_fsst_k1g(ctx, fuse):
+    """A batched plan decodes one FSST accessor group's tiles inside its K1g launch
+    (fsst_k1g_kernel, the tiles spread between the K1g workgroups): lineitem columns (Dict(VarBin)
+    strings, RunEnd, numeric cascades -- K1g jobs) beside chunked FSST columns with FastLanes-
+    packed offsets/lengths (the fused group), plain i32 offsets/lengths (a second group: its own
+    launch), nulls and ragged chunk sizes, and a FSST-only plan (a K1g launch with no K1g jobs).
+    VXG_PLAN_FUSE=0 records the unfused form; both equal the oracle on every replay."""
+    import os
+    import torch
+    sys_path_bench()
+    from tools import lineitem as L
+    rows, cr = 5 * 4096 + 11, 4096
+    cols, plain_vals = L.lineitem_columns(range(L.n_chunks(rows, cr)), rows=rows, chunk_rows=cr)
+    rng = np.random.default_rng(505)
+    strs = _comment_strings(rng, 60_000, vocab=80)
+    strs = [None if i % 23 == 5 else x for i, x in enumerate(strs)]
+    cuts = [0, 6, 9_000, 9_257, 40_000, 60_000]  # every chunk holds a null (one nullable dtype)
+    packed = A.chunked([E.encode_fsst(strs[a:b]) for a, b in zip(cuts, cuts[1:])])
+    plain = A.chunked([E.encode_fsst(strs[a:b], compress_children=False) for a, b in zip(cuts[:3], cuts[1:4])])
+    arrs = [cols[name] for name, _ in L.COLUMNS] + [packed, plain]
+    kinds = [kind for _, kind in L.COLUMNS] + ["utf8", "utf8"]
+    old = os.environ.get("VXG_PLAN_FUSE")
+    os.environ["VXG_PLAN_FUSE"] = fuse
+    try:
+        with plan_mode("1"):
+            plans = [V.Plan([a.to(torch_dev()) for a in arrs], ctx), V.Plan([packed.to(torch_dev())], ctx)]
+    finally:
+        if old is None:
+            os.environ.pop("VXG_PLAN_FUSE", None)
+        else:
+            os.environ["VXG_PLAN_FUSE"] = old
+    assert all(p.info()["batched"] for p in plans)
+    want = [canon(a) if k == "utf8" else np.concatenate(plain_vals[n]) for a, k, n in
+            zip(arrs, kinds, [name for name, _ in L.COLUMNS] + ["", ""])]
+    for _ in range(3):
+        for plan, idx in zip(plans, ([*range(len(arrs))], [len(arrs) - 2])):
+            res = plan.launch(sync=True)
+            for r, i in zip(res, idx):
+                if kinds[i] == "utf8":
+                    (rviews, rbufs), rvalid = want[i]
+                    assert r.numpy()[0].tobytes() == rviews.tobytes(), i
+                    assert [b.tobytes() for b in r.buffers()] == [b.tobytes() for b in rbufs], i
+                    assert np.array_equal(r.validity_mask(), rvalid), i
+                else:
+                    assert r.numpy().tobytes() == want[i].tobytes(), i
+    for p in plans:
+        p.close()
+
+
 @pytest.mark.parametrize("rows,cr", [(3 * 8192 + 99, 8192), (100 * 1024 + 77, 1024)])
 def test_plan_lineitem_columns(ctx, rows, cr):
     """vxg_plan over the lineitem columns (RunEnd, Dict strings, FSST chunks: planner

@@ -189,7 +189,7 @@ static int k1_out_width(const K1Job& j) {
 vxg_status launch_k1_jobs(std::vector<K1Job>& jobs, uint32_t* err, hipStream_t s, DevTables* dt = nullptr,
                           bool generic_small = false,
                           const std::vector<std::pair<int, RunEndChunk>>* gen_runs = nullptr,
-                          const PatchCol* patch = nullptr) {
+                          const PatchCol* patch = nullptr, const FsstFused* fuse = nullptr) {
     std::stable_sort(jobs.begin(), jobs.end(), [](const K1Job& a, const K1Job& b) {
         return std::make_tuple(a.T, a.W, int(a.epi), a.vw, a.vb) < std::make_tuple(b.T, b.W, int(b.epi), b.vw, b.vb);
     });
@@ -236,7 +236,8 @@ vxg_status launch_k1_jobs(std::vector<K1Job>& jobs, uint32_t* err, hipStream_t s
         i = j;
     }
     const size_t n_runs = gen_runs ? gen_runs->size() : 0;
-    if (!gen.empty() || n_runs) {
+    if (!gen.empty() || n_runs || (fuse && fuse->valid)) {
+        if (!dt) return set_error(VXG_ERR_INVALID_ARGUMENT, "internal: K1g launch outside a plan");
         if (gen.size() + n_runs > 0xFFFFFFFFull) return set_error(VXG_ERR_INVALID_ARGUMENT, "too many chunks");
         GenChunk* host;
         const GenChunk* ext;
@@ -285,7 +286,7 @@ vxg_status launch_k1_jobs(std::vector<K1Job>& jobs, uint32_t* err, hipStream_t s
         for (size_t k = 0; k < cnt.size(); k++)
             cnt[k] = (k + 1 < cnt.size() ? host[k + 1].d.first_group : groups) - host[k].d.first_group;
         VXG_TRY_S(launch_k1_generic(ext, uint32_t(gen.size() + n_runs), groups, dict_lds, packed_bytes, dict_bytes,
-                                    runs_bytes, err, s, common_groups(cnt.data(), cnt.size())));
+                                    runs_bytes, err, s, common_groups(cnt.data(), cnt.size()), fuse));
     }
     return VXG_OK;
 }
@@ -394,8 +395,16 @@ struct PlanBatch {
     std::vector<VarBinChunk> dicts;
     std::vector<K1Job> jobs;
     std::vector<Run> runs;
-    bool empty() const { return dicts.empty() && jobs.empty() && runs.empty(); }
+    std::vector<FsstChunk> fssts;  // FSST chunks of chunked columns
+    bool empty() const { return dicts.empty() && jobs.empty() && runs.empty() && fssts.empty(); }
 };
+
+// VXG_PLAN_FUSE=0 (read at every flush): a batched plan's FSST decode keeps its own launch
+// instead of running inside the K1g launch (A/B).
+static bool plan_fuse_enabled() {
+    const char* e = std::getenv("VXG_PLAN_FUSE");
+    return !(e && e[0] == '0');
+}
 
 vxg_status launch_varbin_dicts(const std::vector<VarBinChunk>& dicts, uint32_t* err, hipStream_t s, DevTables* dt) {
     const size_t per = dt && dicts.size() > size_t(kVarBinArgChunks) ? dicts.size() : size_t(kVarBinArgChunks);
@@ -421,6 +430,16 @@ vxg_status launch_varbin_dicts(const std::vector<VarBinChunk>& dicts, uint32_t* 
 }
 
 vxg_status flush_plan_batch(PlanBatch& b, uint32_t* err, hipStream_t s, DevTables* dt) {
+    // FSST chunks: pre-passes first; one accessor group's decode tiles then run inside the K1g
+    // launch (fsst_k1g_kernel), beside the K1 jobs, the other groups' decodes here
+    FsstFused ff;
+    if (!b.fssts.empty()) {
+        void* scratch = nullptr;
+        VXG_TRY_S(hip_check(hipMalloc(&scratch, (fsst_batch_scratch_bytes(b.fssts.data(), b.fssts.size()) + 15) & ~15ull),
+                            "hipMalloc (plan FSST scratch)"));
+        dt->allocs.push_back(scratch);
+        VXG_TRY_S(launch_fsst_batch(b.fssts, scratch, err, s, dt, plan_fuse_enabled() ? &ff : nullptr));
+    }
     VXG_TRY_S(launch_varbin_dicts(b.dicts, err, s, dt));
     // short-run expansions that read their children in place join the K1g launch; the others
     // follow the K1 decodes that produce their children
@@ -431,7 +450,7 @@ vxg_status flush_plan_batch(PlanBatch& b, uint32_t* err, hipStream_t s, DevTable
         if (r.indep && r.c.len <= kRunEndShortRun * r.c.n_runs && gen_runs_kind(r.w) >= 0) gen_runs.emplace_back(r.w, r.c);
         else rest.push_back(r);
     }
-    VXG_TRY_S(launch_k1_jobs(b.jobs, err, s, dt, true, &gen_runs));
+    VXG_TRY_S(launch_k1_jobs(b.jobs, err, s, dt, true, &gen_runs, nullptr, &ff));
     std::vector<int> widths;
     for (const auto& r : rest) widths.push_back(r.w);
     std::sort(widths.begin(), widths.end());
@@ -895,7 +914,7 @@ vxg_status Planner::decode_chunked_primitive(const vxg_array& a, void* dst) {
         } else {
             const void* p;
             VXG_TRY(view_primitive(c, &p));
-            VXG_TRY(hip_check(hipMemcpyAsync(slice, p, c.len * w, hipMemcpyDeviceToDevice, s_), "chunk copy"));
+            VXG_TRY(launch_copy_bytes(slice, p, c.len * w, s_));
         }
         off += c.len;
     }
@@ -961,7 +980,7 @@ vxg_status Planner::decode_into(const vxg_array& a, void* dst) {
         const void* p;
         VXG_TRY(view_primitive(a, &p));
         if (p != dst && a.len)
-            VXG_TRY(hip_check(hipMemcpyAsync(dst, p, a.len * w, hipMemcpyDeviceToDevice, s_), "primitive copy"));
+            VXG_TRY(launch_copy_bytes(dst, p, a.len * w, s_));
         return VXG_OK;
     }
     case VXG_ENC_FL_BITPACKED:
@@ -1118,7 +1137,7 @@ vxg_status Planner::validity_into(const vxg_array& a, void** bitmap) {
     }
     const uint64_t bytes = ((a.len + 31) / 32) * 4;
     if (!*bitmap) VXG_TRY(hip_check(hipMalloc(bitmap, bytes ? bytes : 4), "validity alloc"));
-    VXG_TRY(hip_check(hipMemsetAsync(*bitmap, 0, bytes ? bytes : 4, s_), "validity memset"));
+    VXG_TRY(launch_copy_bytes(*bitmap, nullptr, bytes ? bytes : 4, s_));
     if (kind == 1) return VXG_OK;
     if (kind == 2) {
         const vxg_buffer* b = buf(*node, 0);
@@ -1321,7 +1340,7 @@ vxg_status Planner::filter(const vxg_array& a, const vxg_array& pred, vxg_canoni
     const uint64_t n = a.len, tiles = filter_tiles(n);
     void* mask;
     VXG_TRY(temp(((n + 63) / 64) * 8, &mask));
-    VXG_TRY(hip_check(hipMemsetAsync(mask, 0, ((n + 63) / 64) * 8, s_), "filter mask memset"));
+    VXG_TRY(launch_copy_bytes(mask, nullptr, ((n + 63) / 64) * 8, s_));
     VXG_TRY(bools_into(pred, mask, 0));
     void* toff;
     VXG_TRY(temp((tiles + 1) * 8, &toff));
@@ -1361,7 +1380,7 @@ vxg_status Planner::filter(const vxg_array& a, const vxg_array& pred, vxg_canoni
     const uint64_t vbits = ((k + 31) / 32) * 4;
     if (src.validity) {  // validity.filter(predicate)
         if (!out.validity) VXG_TRY(hip_check(hipMalloc(&out.validity, vbits ? vbits : 4), "filter validity alloc"));
-        VXG_TRY(hip_check(hipMemsetAsync(out.validity, 0, vbits ? vbits : 4, s_), "filter validity memset"));
+        VXG_TRY(launch_copy_bytes(out.validity, nullptr, vbits ? vbits : 4, s_));
         VXG_TRY(launch_filter_bits(m, n, to, static_cast<const uint8_t*>(src.validity), out.validity, s_));
     } else {
         out.validity = nullptr;
@@ -1375,7 +1394,7 @@ vxg_status Planner::filter(const vxg_array& a, const vxg_array& pred, vxg_canoni
     if (a.dtype == VXG_DTYPE_BOOL) {
         out.values_bytes = vbits;
         if (!out.values) VXG_TRY(hip_check(hipMalloc(&out.values, vbits ? vbits : 4), "filter bool alloc"));
-        VXG_TRY(hip_check(hipMemsetAsync(out.values, 0, vbits ? vbits : 4, s_), "filter bool memset"));
+        VXG_TRY(launch_copy_bytes(out.values, nullptr, vbits ? vbits : 4, s_));
         return launch_filter_bits(m, n, to, static_cast<const uint8_t*>(src.values), out.values, s_);
     }
     // strings: compact the views, then rebuild one heap of the selected rows
@@ -1458,7 +1477,7 @@ vxg_status Planner::bools_into(const vxg_array& a, void* bits, uint64_t off) {
         void* vb;
         const uint64_t vbytes = ((val->len + 31) / 32) * 4;
         VXG_TRY(temp(vbytes, &vb));
-        VXG_TRY(hip_check(hipMemsetAsync(vb, 0, vbytes, s_), "sparse bools memset"));
+        VXG_TRY(launch_copy_bytes(vb, nullptr, vbytes, s_));
         VXG_TRY(bools_into(*val, vb, 0));
         const void* pi;
         VXG_TRY(view_primitive(*idx, &pi));
@@ -1581,7 +1600,7 @@ vxg_status Planner::strings_into(const vxg_array& a, uint8_t* views, uint8_t* da
         VXG_TRY(view_primitive(*bytes, &pb));
         uint8_t* heap = data + bufs[0].offset;
         if (bufs[0].len)
-            VXG_TRY(hip_check(hipMemcpyAsync(heap, pb, bufs[0].len, hipMemcpyDeviceToDevice, s_), "heap copy"));
+            VXG_TRY(launch_copy_bytes(heap, pb, bufs[0].len, s_));
         return launch_varbin_views(heap, bufs[0].len, width(*offs), po, a.len, validity, bidx, views, ctx_->c.err_word, s_);
     }
     case VXG_ENC_VARBINVIEW: {
@@ -1595,8 +1614,7 @@ vxg_status Planner::strings_into(const vxg_array& a, uint8_t* views, uint8_t* da
             const void* pb;
             VXG_TRY(view_primitive(a.children[1 + b], &pb));
             if (bufs[b].len)
-                VXG_TRY(hip_check(hipMemcpyAsync(data + bufs[b].offset, pb, bufs[b].len, hipMemcpyDeviceToDevice, s_),
-                                  "view buffer copy"));
+                VXG_TRY(launch_copy_bytes(data + bufs[b].offset, pb, bufs[b].len, s_));
         }
         return VXG_OK;
     }
@@ -1757,7 +1775,9 @@ vxg_status Planner::strings_into(const vxg_array& a, uint8_t* views, uint8_t* da
             b += k;
         }
         if (row != a.len) return set_error(VXG_ERR_INVALID_ARGUMENT, "Chunked len != sum of chunk lens");
-        if (!fssts.empty()) {
+        if (!fssts.empty() && defer(a)) {  // a plan's root: decoded at the batch's flush
+            batch_->fssts.insert(batch_->fssts.end(), fssts.begin(), fssts.end());
+        } else if (!fssts.empty()) {
             void* scratch;
             VXG_TRY(temp(fsst_batch_scratch_bytes(fssts.data(), fssts.size()), &scratch));
             VXG_TRY(launch_fsst_batch(fssts, scratch, ctx_->c.err_word, s_, plan_));
@@ -1841,7 +1861,7 @@ vxg_status Planner::canonical(const vxg_array& a, vxg_canonical& out) {
         if (!out.values)
             VXG_TRY(hip_check(hipMalloc(&out.values, out.values_bytes ? out.values_bytes : 4), "bool values alloc"));
         if (out.values_bytes)
-            VXG_TRY(hip_check(hipMemsetAsync(out.values, 0, out.values_bytes, s_), "bool values memset"));
+            VXG_TRY(launch_copy_bytes(out.values, nullptr, out.values_bytes, s_));
         VXG_TRY(bools_into(a, out.values, 0));
         return validity_into(a, &out.validity);
     }
@@ -2225,6 +2245,11 @@ static vxg_status record_plan(vxg_ctx* ctx, const vxg_array* arrays, vxg_canonic
         const hipError_t e = hipStreamEndCapture(cs, &g);
         if (st == VXG_OK) st = hip_check(e, "hipStreamEndCapture");
         pl->graph = g;
+        if (st == VXG_OK && std::getenv("VXG_PLAN_DOT")) {  // diagnostics: PREFIX_<n>.dot per recorded graph
+            static int cnt = 0;
+            const std::string path = std::string(std::getenv("VXG_PLAN_DOT")) + "_" + std::to_string(cnt++) + ".dot";
+            (void)hipGraphDebugDotPrint(g, path.c_str(), 0);
+        }
         if (st == VXG_OK)
             st = hip_check(hipGraphInstantiate(&pl->exec, g, nullptr, nullptr, 0), "hipGraphInstantiate");
         if (st == VXG_OK) st = pl->store.upload();  // device chunk tables, once for all replays

@@ -30,6 +30,7 @@
 
 #include "fl_unpack_impl.hpp"
 #include "intcol.hpp"
+#include "k1g_impl.hpp"
 
 namespace vxg {
 
@@ -787,26 +788,60 @@ __device__ __forceinline__ void tile_run(const FsstChunk& ch, const TileIn<LenAc
     }
 }
 
+// The decode's LDS carved from one buffer (the plan launch that runs decode tiles beside K1g
+// jobs has only dynamic LDS): image, codes, symbols, scan scratch -- kDecLdsBytes in all.
+constexpr uint32_t kDecHeapBytes = kHeapLds + 96;  // + slack: view reads past a string, and ORs
+                                                   // of the (<= 3) dwords past the tile
+constexpr uint32_t kDecCodesBytes = kCodeLds + 48; // + slack: the straddling segment's dwords
+                                                   // past the tile (masked in pass 1)
+constexpr uint32_t kDecLdsBytes = kDecHeapBytes + kDecCodesBytes + 8 * 256 + 8 * (kTile / 64) + 8 +
+                                  4 * 4 * (kTile / 64) + 256;
+static_assert(kDecHeapBytes % 16 == 0 && kDecCodesBytes % 16 == 0, "16-byte aligned stages");
+__device__ __forceinline__ DecLds dec_lds(uint8_t* p) {
+    DecLds L;
+    L.s_heap32 = reinterpret_cast<uint32_t*>(p);
+    p += kDecHeapBytes;
+    L.s_codes = p;
+    p += kDecCodesBytes;
+    L.s_sym = reinterpret_cast<uint64_t*>(p);
+    p += 8 * 256;
+    L.ws64 = reinterpret_cast<int64_t*>(p);
+    p += 8 * (kTile / 64);
+    L.s_block_prefix = reinterpret_cast<int64_t*>(p);
+    p += 8;
+    L.ws_a = reinterpret_cast<int*>(p);
+    L.ws_b = L.ws_a + kTile / 64;
+    L.ws_bad = reinterpret_cast<unsigned*>(L.ws_b + kTile / 64);
+    L.ws_esc = L.ws_bad + kTile / 64;
+    L.s_len = reinterpret_cast<uint8_t*>(L.ws_esc + kTile / 64);
+    return L;
+}
+
 // One tile per workgroup: the tile's loads (tile_issue) are all in flight before the symbol
 // table and the scan-block prefix are loaded.  (Two consecutive tiles per workgroup with both
 // tiles' loads issued in the prologue was measured 10 % slower on C4 -- 6 instead of 8 waves per
 // SIMD; profiles/r04_fsst_decode.md.)
+template <class OffAcc, class LenAcc>
+__device__ __forceinline__ void fsst_decode_tile(const FsstChunk& ch, uint64_t g, const int64_t* __restrict__ tile_prefix_all,
+                                                 const int64_t* __restrict__ block_totals_all,
+                                                 const int64_t* __restrict__ tile_code_all, uint32_t* __restrict__ err,
+                                                 const DecLds& L) {
+    TileIn<LenAcc> in;
+    tile_issue<OffAcc, LenAcc>(ch, g, tile_prefix_all, tile_code_all, in);
+    uint64_t sym_v;
+    uint32_t sl;
+    symbol_load(ch, sym_v, sl);
+    block_prefix(ch, in.tile, block_totals_all, L);
+    symbol_store(ch, L, sym_v, sl, err);
+    tile_run<OffAcc, LenAcc>(ch, in, L, err);
+}
+
 template <class OffAcc, class LenAcc, bool EXT>
 __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) void fsst_decode(
     FsstTable tab, const int64_t* __restrict__ tile_prefix_all, const int64_t* __restrict__ block_totals_all,
     const int64_t* __restrict__ tile_code_all, uint32_t* __restrict__ err, const uint32_t* __restrict__ wg_chunk) {
-    __shared__ uint64_t s_sym[256];
-    __shared__ uint8_t s_len[256];
-    __shared__ int ws_a[kTile / 64], ws_b[kTile / 64];
-    __shared__ unsigned ws_bad[kTile / 64], ws_esc[kTile / 64];
-    __shared__ int64_t ws64[kTile / 64];
-    __shared__ int64_t s_block_prefix;
-    // + slack: the straddling segment's dwords past the tile (masked in pass 1)
-    __shared__ __attribute__((aligned(16))) uint8_t s_codes[kCodeLds + 48];
-    // + slack: view reads past a string, and ORs of the (<= 3) dwords past the tile
-    __shared__ __attribute__((aligned(16))) uint32_t s_heap32[(kHeapLds + 96) / 4];
-    const DecLds L{s_sym, s_len, ws_a, ws_b, ws_bad, ws_esc, ws64, &s_block_prefix, s_codes, s_heap32};
-
+    __shared__ __attribute__((aligned(16))) uint8_t s_lds[kDecLdsBytes];
+    const DecLds L = dec_lds(s_lds);
     // the tile's chunk: a recorded plan's device table through the plan's per-tile map (one
     // scalar load; the chunk's entry is then shared by its ~255 tiles' workgroups in the scalar
     // cache -- a per-tile copy of the entry, which saves that dependent load but always misses,
@@ -825,15 +860,35 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) v
         }
         ci = lo;
     }
-    const FsstChunk& ch = EXT ? tab.ext[ci] : tab.c[ci];
-    TileIn<LenAcc> in;
-    tile_issue<OffAcc, LenAcc>(ch, g, tile_prefix_all, tile_code_all, in);
-    uint64_t sym_v;
-    uint32_t sl;
-    symbol_load(ch, sym_v, sl);
-    block_prefix(ch, in.tile, block_totals_all, L);
-    symbol_store(ch, L, sym_v, sl, err);
-    tile_run<OffAcc, LenAcc>(ch, in, L, err);
+    fsst_decode_tile<OffAcc, LenAcc>(EXT ? tab.ext[ci] : tab.c[ci], g, tile_prefix_all, block_totals_all, tile_code_all,
+                                     err, L);
+}
+
+// The plan launch of a batched plan (FsstFused): one recorded group's decode tiles and the
+// plan's K1g jobs (k1g_impl.hpp) in ONE grid, so that the decode's latency-bound tiles (two
+// dependent memory round trips and two barriers per 256 strings) run beside the K1g jobs' store
+// streams instead of alone.  The decode tiles are spread evenly over the first `mix` workgroups
+// of the grid (the rest are K1g jobs): workgroup b < mix is tile floor(b T / mix) when that
+// floor steps at b.  Every workgroup has the decode's LDS (8 per CU, the wave limit anyway).
+template <class OffAcc, class LenAcc>
+__global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) void fsst_k1g_kernel(
+    FsstFusedArgs fa, const GenChunk* __restrict__ gtab, uint32_t gn, uint32_t dict_off, bool dict_lds,
+    uint32_t* __restrict__ err, uint64_t gpe) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const uint64_t b = blockIdx.x, T = fa.tiles, M = fa.mix;
+    uint64_t gg;  // K1g workgroup
+    if (b < M) {
+        const uint64_t d0 = b * T / M, d1 = (b + 1) * T / M;
+        if (d1 > d0) {
+            fsst_decode_tile<OffAcc, LenAcc>(fa.ext[fa.wg_chunk[d0]], d0, fa.tp, fa.bt, fa.tc, err, dec_lds(lds));
+            return;
+        }
+        gg = b - d1;
+    } else {
+        gg = b - T;
+    }
+    const GenChunk& gc = gtab[ext_chunk_index_gpe(gtab, gn, gg, gpe, [](const GenChunk& d) { return d.d.first_group; })];
+    gen_dispatch(int(gc.kind), gc, gg, lds, dict_off, dict_lds, err);
 }
 
 uint64_t fsst_scratch_bytes(uint64_t n) {
@@ -904,8 +959,44 @@ hipError_t fsst_diag_init() {
     return m ? hipMemcpyToSymbol(HIP_SYMBOL(g_fsst_abl), &m, sizeof m) : hipSuccess;
 }
 
+// Accessor pairs the fused plan launch is instantiated for (the file reader's FastLanes-packed
+// u32 offsets and lengths; plain u32 for arrays built in memory): each is one more copy of K1g's
+// 43 job bodies.
+static bool fused_acc(int oa, int la) { return (oa == 32 && la == 32) || (oa == 4 && la == 4); }
+
+// Percentage of the K1g workgroups interleaved with the decode tiles (VXG_FUSED_MIX, 0-100,
+// read once; default 100: the tiles spread over the whole grid).
+static uint64_t fused_mix_pct() {
+    static const uint64_t v = [] {
+        const char* e = std::getenv("VXG_FUSED_MIX");
+        const long x = e ? std::strtol(e, nullptr, 10) : 100;
+        return uint64_t(x >= 0 && x <= 100 ? x : 100);
+    }();
+    return v;
+}
+
+vxg_status launch_fsst_k1g(const FsstFused& fuse, const GenChunk* ext, uint32_t n, uint64_t groups, uint32_t dict_off,
+                           bool dict_lds, size_t shm, uint32_t* err, hipStream_t s, uint64_t gpe) {
+    if (!fuse.valid || !fused_acc(fuse.oa, fuse.la)) return set_error(VXG_ERR_INVALID_ARGUMENT, "internal: fused FSST group");
+    if (n == 0) groups = 0;
+    FsstFusedArgs a = fuse.a;
+    a.mix = a.tiles + groups * fused_mix_pct() / 100;
+    const uint64_t grid = a.tiles + groups;
+    if (grid == 0) return VXG_OK;
+    if (grid > 0xFFFFFFFFull) return set_error(VXG_ERR_INVALID_ARGUMENT, "array too long for one launch");
+    shm = std::max<size_t>(shm, kDecLdsBytes + fsst_pad_lds());
+    if (fuse.oa == 32)
+        hipLaunchKernelGGL((fsst_k1g_kernel<PackedCol<32>, PackedCol<32>>), dim3(unsigned(grid)), dim3(kTile), shm, s, a,
+                           ext, n, dict_off, dict_lds, err, gpe);
+    else
+        hipLaunchKernelGGL((fsst_k1g_kernel<PlainCol<4>, PlainCol<4>>), dim3(unsigned(grid)), dim3(kTile), shm, s, a, ext,
+                           n, dict_off, dict_lds, err, gpe);
+    return hip_check(hipGetLastError(), "fsst_k1g_kernel launch");
+}
+
 vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint32_t* err, hipStream_t s,
-                             DevTables* dt) {
+                             DevTables* dt, FsstFused* fuse) {
+    if (fuse) fuse->valid = false;
     for (const FsstChunk& c : chunks) {
         if (c.n_symbols > 255) return set_error(VXG_ERR_INVALID_ARGUMENT, "FSST symbol table > 255 entries");
         if ((c.n + kTS - 1) / kTS > 0xFFFFFFFFull) return set_error(VXG_ERR_INVALID_ARGUMENT, "FSST array too long");
@@ -926,8 +1017,11 @@ vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint
         size_t j = i, live = 0;
         while (j < chunks.size() && (dt || j - i < size_t(kFsstArgChunks)) && fsst_key(chunks[j]) == fsst_key(chunks[i]))
             live += chunks[j++].n != 0;
+        // the first group the fused launch covers (a device table: the fused kernel reads no kernarg table)
+        const bool fusing = fuse && dt && !fuse->valid && live &&
+                            fused_acc(std::get<0>(fsst_key(chunks[i])), std::get<1>(fsst_key(chunks[i])));
         FsstChunk* cs = tab.c;
-        if (live > size_t(kFsstArgChunks)) {
+        if (live > size_t(kFsstArgChunks) || fusing) {
             FsstChunk* host;
             const vxg_status st = dt->table(live, &host, &tab.ext);
             if (st != VXG_OK) return st;
@@ -963,6 +1057,24 @@ vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint
             if (std::get<2>(key) >= 0)
                 launch_tile_scan_fl32(std::get<2>(key), dim3(unsigned(scans)), s, tab, tp, bt, tc,
                                       std::make_integer_sequence<int, 33>{});
+            if (fusing) {  // its pre-pass now, its decode inside the K1g launch
+                if (std::get<2>(key) < 0) {
+                    bool ok = with_acc(std::get<1>(key), [&](auto* la) {
+                        using LA = std::remove_pointer_t<decltype(la)>;
+                        hipLaunchKernelGGL((fsst_tile_scan<LA, true>), dim3(unsigned(scans)), dim3(kTile), 0, s, tab, tp,
+                                           bt, tc);
+                    });
+                    if (!ok) return set_error(VXG_ERR_MISMATCHED_TYPES, "FSST accessor");
+                }
+                fuse->valid = true;
+                fuse->oa = std::get<0>(key);
+                fuse->la = std::get<1>(key);
+                fuse->a = FsstFusedArgs{tab.ext, tp, bt, tc, wg_chunk, tiles, tiles};
+                const vxg_status st = hip_check(hipGetLastError(), "fsst pre-pass");
+                if (st != VXG_OK) return st;
+                i = j;
+                continue;
+            }
             bool ok = true;
             with_acc(std::get<0>(key), [&](auto* oa) {
                 ok = with_acc(std::get<1>(key), [&](auto* la) {

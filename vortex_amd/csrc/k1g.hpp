@@ -59,8 +59,14 @@ uint32_t gen_runs_lds_bytes(int value_width);
 // job's dictionary fits the LDS stage (16 KiB, 16-byte aligned); packed_bytes / dict_bytes /
 // runs_bytes = the largest packed stage (bpw * 128 * W), dictionary stage (staged dictionaries,
 // VarBin views) and RunEnd expansion LDS of the launch's jobs.
+// With `fuse` valid, the launch also decodes that FSST group's tiles (fsst.hip fsst_k1g_kernel;
+// n = 0 is allowed then).
 vxg_status launch_k1_generic(const GenChunk* ext, uint32_t n, uint64_t groups, bool dict_lds, uint32_t packed_bytes,
                              uint32_t dict_bytes, uint32_t runs_bytes, uint32_t* err, hipStream_t s,
-                             uint64_t gpe = 0);
+                             uint64_t gpe = 0, const FsstFused* fuse = nullptr);
+// The fused launch (fsst.hip): K1g jobs `ext` (n entries, `groups` workgroups, LDS `shm` with the
+// dictionary stage at dict_off) beside `fuse`'s decode tiles.
+vxg_status launch_fsst_k1g(const FsstFused& fuse, const GenChunk* ext, uint32_t n, uint64_t groups, uint32_t dict_off,
+                           bool dict_lds, size_t shm, uint32_t* err, hipStream_t s, uint64_t gpe);
 
 }  // namespace vxg

@@ -742,6 +742,42 @@ vxg_status launch_fill(int value_width, const uint8_t* scalar16, uint64_t n, voi
     return hip_check(hipGetLastError(), "fill_kernel");
 }
 
+// ------------------------------------------------------------------ K10 byte copy / zero
+// dst[0, n) = src[0, n) (src null: zeros).  The planner's device-to-device copies and zero fills
+// are kernels rather than hipMemcpyAsync / hipMemsetAsync: inside a recorded plan those become
+// graph memcpy/memset nodes, and a memset node at the root of a replayed graph was measured to
+// leave stale bits that the following kernels' atomic ORs then kept (profiles/r05_plan_memset.md);
+// kernel nodes also keep a plan eligible for direct replay.  16-byte body when dst and src share
+// their alignment mod 16, bytes otherwise.
+__global__ __launch_bounds__(kBlock) void copy_bytes_kernel(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
+                                                            uint64_t n, uint64_t head, uint64_t body) {
+    const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+    const uint64_t t0 = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    for (uint64_t q = t0; q < body; q += stride) {  // 16-byte chunks after the head
+        const uint4 v = src ? gload(reinterpret_cast<const uint4*>(src + head) + q) : make_uint4(0, 0, 0, 0);
+        gstore(reinterpret_cast<uint4*>(dst + head) + q, v);
+    }
+    const uint64_t tail0 = head + 16 * body, edge = head + (n - tail0);  // head bytes + tail bytes
+    for (uint64_t k = t0; k < edge; k += stride) {
+        const uint64_t i = k < head ? k : tail0 + (k - head);
+        gstore(dst + i, src ? gload(src + i) : uint8_t(0));
+    }
+}
+
+vxg_status launch_copy_bytes(void* dst, const void* src, uint64_t n, hipStream_t s) {
+    if (n == 0) return VXG_OK;
+    const uintptr_t d = reinterpret_cast<uintptr_t>(dst), a = reinterpret_cast<uintptr_t>(src);
+    uint64_t head = n, body = 0;
+    if (!src || ((d ^ a) & 15) == 0) {
+        head = std::min<uint64_t>(n, (16 - (d & 15)) & 15);
+        body = (n - head) / 16;
+    }
+    const uint64_t work = std::max<uint64_t>(body, 32);
+    hipLaunchKernelGGL(copy_bytes_kernel, dim3(grid_for(work)), dim3(kBlock), 0, s, static_cast<uint8_t*>(dst),
+                       static_cast<const uint8_t*>(src), n, head, body);
+    return hip_check(hipGetLastError(), "copy_bytes_kernel");
+}
+
 // ------------------------------------------------------------------ VarBin -> views
 // arrow-array 53.2 make_view: len<=12 inline (zero padded), else {len, prefix, 0, offset};
 // null rows -> all-zero view (GenericByteViewBuilder::append_null).

@@ -389,6 +389,8 @@ struct VarBinTable {
 };
 vxg_status launch_varbin_chunks(const VarBinTable& t, uint64_t groups, hipStream_t s);
 
+// dst[0, n) = src[0, n), or zeros when src is null (kernels.hip K10).
+vxg_status launch_copy_bytes(void* dst, const void* src, uint64_t n, hipStream_t s);
 vxg_status launch_fill(int value_width, const uint8_t* scalar16, uint64_t n, void* out,
                        hipStream_t s);
 // One FSST -> VarBinView decode (a whole array or one chunk of a ChunkedArray).
@@ -417,14 +419,31 @@ struct FsstTable {
 // Scratch for a set of chunks (tile prefixes + scan-block totals + tile code ends).
 uint64_t fsst_scratch_bytes(uint64_t n);
 uint64_t fsst_batch_scratch_bytes(const FsstChunk* chunks, size_t n_chunks);
+// A batched plan's FSST group whose decode tiles run inside the plan's K1g launch
+// (fsst_k1g_kernel, launch_fsst_k1g in k1g.hpp): its device table, pre-pass records and tile map.
+struct FsstFusedArgs {
+    const FsstChunk* ext;
+    const int64_t* tp;          // tile prefixes
+    const int64_t* bt;          // scan-block totals
+    const int64_t* tc;          // tile code ends
+    const uint32_t* wg_chunk;   // chunk of every decode tile
+    uint64_t tiles;             // decode tiles
+    uint64_t mix;               // first workgroups of the grid the tiles are spread over (set at launch)
+};
+struct FsstFused {
+    bool valid = false;
+    int oa = 0, la = 0;         // offsets / lengths accessor kinds
+    FsstFusedArgs a{};
+};
 // Decode every chunk: grouped by accessor kinds, kFsstArgChunks per launch pair (pre-pass +
 // decode; a recorded plan's group over a device table is one pair).  `scratch` >=
-// fsst_batch_scratch_bytes.
+// fsst_batch_scratch_bytes.  With `fuse` (recording a batched plan), one group whose accessors
+// the fused kernel covers gets only its pre-pass launched and is described in *fuse instead.
 // The FSST decode's diagnostics mask (VXG_FSST_ABL, read once per process) into its __constant__;
 // called by vxg_open.
 hipError_t fsst_diag_init();
 vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint32_t* err, hipStream_t s,
-                             DevTables* dt = nullptr);
+                             DevTables* dt = nullptr, FsstFused* fuse = nullptr);
 // Views carry `bidx` as the buffer_index of non-inlined rows.
 vxg_status launch_varbin_views(const uint8_t* heap, uint64_t heap_len, int offs_width, const void* offsets, uint64_t n,
                                const uint8_t* validity, uint32_t bidx, uint8_t* views, uint32_t* err, hipStream_t s);
