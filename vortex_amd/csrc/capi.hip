@@ -165,13 +165,14 @@ bool same_kernel(const K1Job& a, const K1Job& b) {
 }
 
 // Output bytes below which a plan batch's kernel group goes to the one K1g launch instead of its
-// own K1 launch (VXG_K1G_MAX_BYTES overrides; 0 disables K1g).  Measured on the simulated 8-GPU
-// C5 shard: 0.120 ms/step with per-kernel launches, 0.094 with K1g below 16 MiB, 0.085 below
-// 64 MiB (tools/gpu_ab_c5.sh).
+// own K1 launch (VXG_K1G_MAX_BYTES overrides; 0 disables K1g).  Round 5, C5 (same box, ms per
+// step): 1 GPU 0.289 with 64 MiB (every numeric column in K1g: unbatched kept) vs 0.272 with
+// 16 MiB (batched kept); 2-GPU shard 0.163 vs 0.145; 4-GPU shard 0.0715 vs 0.0784 (its 18 MB
+// date-column group then leaves K1g); 8-GPU shard equal.  20 MiB sits between.
 static uint64_t k1g_max_bytes() {
     static const uint64_t v = [] {
         const char* e = std::getenv("VXG_K1G_MAX_BYTES");
-        return e ? uint64_t(std::strtoull(e, nullptr, 10)) : uint64_t(64) << 20;
+        return e ? uint64_t(std::strtoull(e, nullptr, 10)) : uint64_t(20) << 20;
     }();
     return v;
 }
@@ -2123,11 +2124,12 @@ struct vxg_plan {
 };
 
 // Direct replay of short kernel chains (VXG_PLAN_DIRECT=0 disables; at most
-// VXG_PLAN_DIRECT_MAX nodes, default 8).
+// VXG_PLAN_DIRECT_MAX nodes, default 16: C5's 1-GPU batched chain is 9 kernels, 0.2745 ms per
+// step as a graph vs 0.2719 direct).
 static size_t plan_direct_max() {
     static const size_t v = [] {
         const char* e = std::getenv("VXG_PLAN_DIRECT_MAX");
-        return e ? size_t(std::strtoull(e, nullptr, 10)) : size_t(8);
+        return e ? size_t(std::strtoull(e, nullptr, 10)) : size_t(16);
     }();
     return v;
 }
