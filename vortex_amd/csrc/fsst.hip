@@ -272,51 +272,59 @@ __global__ __launch_bounds__(kTile) void fsst_tile_scan(FsstTable tab, int64_t* 
     scan_tile_sums(s_ts, ws, n_tiles, sb, tile_prefix, block_totals, tile_code_all + c.first_tile, code_end);
 }
 
-// Patch-free FoR(BitPacked u32/i32) lengths with offset 0 (the reference cascade): decode
-// whole FastLanes blocks K1-style (8 threads per block, W x 16-byte loads, SWAR rows).  Row R
-// of a block holds strings (R % 8) * 128 + ..., i.e. tile (R % 8) * 128 / kTS of the block, so
-// each thread accumulates kTPB tile partial sums, reduced across its 8 threads.
+// Patch-free FoR(BitPacked u32/i32) lengths with offset 0 (the reference cascade): one thread
+// per (FastLanes block, 32-bit lane) -- 1024 threads = the scan block's 32 blocks -- reads its
+// lane's W words (the 32 lanes of a block: 128 contiguous bytes per word) and extracts the
+// lane's 32 rows with immediate shifts.  Row R of a block holds strings (R % 8) * 128 + ..., i.e.
+// tile (R % 8) * 128 / kTS of the block, so each thread keeps kTPB tile partial sums, reduced
+// across the block's 32 lanes.  (Round 4 used 8 threads per block with 16-byte slices: 183
+// workgroups of 4 waves for C4, ~1,000 VALU per wave on one serial chain per SIMD; round 5
+// spreads the same work over 4x the waves.)
 // A: int64 (any lengths) or uint32 (every length of the column < 2^23 and non-negative, so
 // 256 of them sum below 2^31: the common case, half the adds and no 64-bit selects).
+constexpr int kScanThreads = 32 * 32;  // 32 blocks x 32 lanes
+static_assert(kScanTiles == 32 * kTPB, "a scan block is 32 FastLanes blocks of lengths");
+
 template <int W, class A, int... Rs>
-__device__ __forceinline__ void fl32_tile_rows(const Vec16<32>* p, int t, uint64_t blk0, uint64_t n, uint32_t shift,
+__device__ __forceinline__ void fl32_lane_rows(const uint32_t* p, int lane, uint32_t left, uint32_t for_shift,
                                                uint32_t reference, bool sgn, A* acc,
                                                std::integer_sequence<int, Rs...>) {
-    const uint32_t left = blk0 + 1024 <= n ? 1024u : uint32_t(n - blk0);  // valid elements of the block
     auto row = [&](auto rc) {
         constexpr int R = decltype(rc)::value;
-        const Vec16<32> v = extract_row<32, W, R>(p);
-        const int idx0 = fl_index(R, 4 * t);
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const uint32_t u = uint32_t(v.elem(j) << shift) + reference;
-            A x;
-            if constexpr (sizeof(A) == 8) x = sgn ? A(int32_t(u)) : A(u);
-            else x = u;
-            acc[(R % 8) * 128 / kTS] += uint32_t(idx0 + j) < left ? x : A(0);
+        uint32_t v = 0;
+        if constexpr (W > 0) {
+            constexpr int start = R * W, word = start / 32, sh = start % 32;
+            constexpr uint32_t m = W >= 32 ? 0xFFFFFFFFu : ((1u << W) - 1u);
+            if constexpr (sh + W <= 32) v = (p[word] >> sh) & m;
+            else v = __builtin_amdgcn_alignbit(p[word + 1], p[word], uint32_t(sh)) & m;
         }
+        const uint32_t u = uint32_t(v << for_shift) + reference;
+        A x;
+        if constexpr (sizeof(A) == 8) x = sgn ? A(int32_t(u)) : A(u);
+        else x = u;
+        acc[(R % 8) * 128 / kTS] += uint32_t(fl_index(R, lane)) < left ? x : A(0);
     };
     (row(std::integral_constant<int, Rs>{}), ...);
 }
 
 template <int W, bool EXT>
-__global__ __launch_bounds__(kTile) void fsst_tile_scan_fl32(FsstTable tab, int64_t* __restrict__ tile_prefix_all,
-                                                             int64_t* __restrict__ block_totals_all,
-                                                             int64_t* __restrict__ tile_code_all) {
+__global__ __launch_bounds__(kScanThreads) void fsst_tile_scan_fl32(FsstTable tab, int64_t* __restrict__ tile_prefix_all,
+                                                                    int64_t* __restrict__ block_totals_all,
+                                                                    int64_t* __restrict__ tile_code_all) {
     __shared__ int64_t s_ts[kScanTiles];
-    __shared__ int64_t ws[kTile / 64];
-    const int tid = threadIdx.x, t = tid & 7;
+    __shared__ int64_t ws[2];
+    const int tid = threadIdx.x, lane = tid & 31, lane64 = tid & 63, wave = tid >> 6;
     const FsstChunk& c = fsst_chunk_of<true, EXT>(tab, blockIdx.x);
     const uint8_t* __restrict__ packed = static_cast<const uint8_t*>(c.lens.p);
-    const uint32_t shift = c.lens.shift, reference = uint32_t(c.lens.reference);
+    const uint32_t for_shift = c.lens.shift, reference = uint32_t(c.lens.reference);
     const bool sgn = c.lens.sgn;
     const uint64_t n = c.n, n_tiles = (n + kTS - 1) / kTS, sb = blockIdx.x - c.first_scan;
     int64_t* const tile_prefix = tile_prefix_all + c.first_tile;
     int64_t* const block_totals = block_totals_all + c.first_scan;
-    const uint64_t blk = sb * 32 + (tid >> 3);
+    const uint64_t blk = sb * 32 + (tid >> 5);
     const int64_t code_end = tile_code_end(c, sb);
     // every value of the column below 2^23 (uniform): 32-bit sums are exact
-    const uint64_t vmax = ((W >= 32 ? 0xFFFFFFFFull : ((1ull << W) - 1)) << shift) + reference;
+    const uint64_t vmax = ((W >= 32 ? 0xFFFFFFFFull : ((1ull << W) - 1)) << for_shift) + reference;
     const bool small = vmax < (1ull << 23) && !(sgn && int32_t(reference) < 0);
     auto run = [&](auto* tag) {
         using A = std::remove_pointer_t<decltype(tag)>;
@@ -324,27 +332,44 @@ __global__ __launch_bounds__(kTile) void fsst_tile_scan_fl32(FsstTable tab, int6
 #pragma unroll
         for (int k = 0; k < kTPB; k++) acc[k] = 0;
         if (blk * 1024 < n) {
-            Vec16<32> p[W > 0 ? W : 1];
+            uint32_t p[W > 0 ? W : 1];
             if constexpr (W > 0) {
+                const uint32_t* __restrict__ base = reinterpret_cast<const uint32_t*>(packed + blk * (128 * W)) + lane;
 #pragma unroll
-                for (int w = 0; w < W; w++) p[w] = load16_global<32>(packed + blk * (128 * W) + 128 * w + 16 * t);
+                for (int w = 0; w < W; w++) p[w] = gload(base + 32 * w);
             }
-            fl32_tile_rows<W>(p, t, blk * 1024, n, shift, reference, sgn, acc, std::make_integer_sequence<int, 32>{});
+            const uint32_t left = blk * 1024 + 1024 <= n ? 1024u : uint32_t(n - blk * 1024);
+            fl32_lane_rows<W>(p, lane, left, for_shift, reference, sgn, acc, std::make_integer_sequence<int, 32>{});
         }
 #pragma unroll
         for (int k = 0; k < kTPB; k++) {
 #pragma unroll
-            for (int d = 1; d < 8; d <<= 1) acc[k] += __shfl_xor(acc[k], d, 64);
+            for (int d = 1; d < 32; d <<= 1) acc[k] += __shfl_xor(acc[k], d, 64);
         }
-        if (t == 0) {
+        if (lane == 0) {
 #pragma unroll
-            for (int k = 0; k < kTPB; k++) s_ts[(tid >> 3) * kTPB + k] = int64_t(acc[k]);
+            for (int k = 0; k < kTPB; k++) s_ts[(tid >> 5) * kTPB + k] = int64_t(acc[k]);
         }
     };
     if (small) run(static_cast<uint32_t*>(nullptr));
     else run(static_cast<int64_t*>(nullptr));
     __syncthreads();
-    scan_tile_sums(s_ts, ws, n_tiles, sb, tile_prefix, block_totals, tile_code_all + c.first_tile, code_end);
+    // exclusive scan of the 128 tile sums by waves 0-1
+    const int64_t v = tid < kScanTiles ? s_ts[tid] : 0;
+    int64_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int64_t y = __shfl_up(x, d, 64);
+        if (lane64 >= d) x += y;
+    }
+    if (lane64 == 63 && wave < 2) ws[wave] = x;
+    __syncthreads();
+    const uint64_t tt = sb * kScanTiles + tid;
+    if (tid < kScanTiles && tt < n_tiles) {
+        tile_prefix[tt] = x - v + (wave == 1 ? ws[0] : 0);
+        tile_code_all[c.first_tile + tt] = code_end;
+    }
+    if (tid == 0) block_totals[sb] = ws[0] + ws[1];
 }
 
 // Length of string first + k of a tile (k clamped by the caller), in two steps so the load can
@@ -919,7 +944,7 @@ void launch_tile_scan_fl32(int W, dim3 grid, hipStream_t s, const FsstTable& t, 
     using Fn = void (*)(FsstTable, int64_t*, int64_t*, int64_t*);
     static constexpr Fn table[] = {&fsst_tile_scan_fl32<Ws, false>...};
     static constexpr Fn table_ext[] = {&fsst_tile_scan_fl32<Ws, true>...};
-    hipLaunchKernelGGL((t.ext ? table_ext : table)[W], grid, dim3(kTile), 0, s, t, tiles, blocks, codes);
+    hipLaunchKernelGGL((t.ext ? table_ext : table)[W], grid, dim3(kScanThreads), 0, s, t, tiles, blocks, codes);
 }
 
 // accessor = plain width 1/2/4/8 or packed T = 32/64
