@@ -1014,8 +1014,8 @@ def sys_path_bench():
 
 class plan_mode:
     """VXG_PLAN_BATCH for the plans created inside (capi.hip reads it at every vxg_plan_create):
-    "0" unbatched, "1" batched, "mixed", None = the default (plain create: one candidate by the
-    400 MB output rule; measure=True: both recorded, vxg_plan_select keeps one)."""
+    "0" unbatched, "1" batched, "mixed", None = the default (plain create: the batched
+    candidate; measure=True: both recorded, vxg_plan_select keeps one)."""
 
     def __init__(self, mode):
         self.mode = mode

@@ -2063,12 +2063,11 @@ static uint32_t plan_branches_env() {
     return nb;
 }
 
-// Plan batching (PlanBatch + K1g).  Whether it pays depends on the table: C5 per GPU at 8 / 4 GPUs
-// (140 / 275 MB) measured 0.060 / 0.095 ms batched vs 0.120 / 0.131 unbatched, but 0.200 vs
-// 0.180 at 2 GPUs (550 MB), and mixing batched and unbatched arrays was slower than either
-// (tools/gpu_thresh.sh).  So the default is measured, not a byte threshold: vxg_plan_create
-// records the plan both ways (unbatched on 2 graph branches, batched on 1) and keeps the one
-// whose replays are faster (3 interleaved timed replays each after one warm-up).  The knob
+// Plan batching (PlanBatch + K1g).  Whether it pays depends on the table (round 4: C5 per GPU at
+// 8 / 4 GPUs measured 0.060 / 0.095 ms batched vs 0.120 / 0.131 unbatched, but 0.200 vs 0.180 at
+// 2 GPUs; mixing batched and unbatched arrays was slower than either).  So VXG_PLAN_MEASURE
+// records the plan both ways (unbatched on 2 graph branches, batched on 1) and keeps one by
+// vxg_plan_select (3 interleaved timed replays each after one warm-up).  The knob
 // VXG_PLAN_BATCH (read at every create) is a diagnostic: "0" unbatched, "1" batched, "mixed"
 // (arrays whose output is <= VXG_PLAN_BATCH_MAX_BYTES batched, the others not), unset = measured.
 // "s" batches only the string-dictionary columns (one K1g launch for all of them on a branch
@@ -2099,10 +2098,11 @@ static uint64_t env_bytes(const char* name, uint64_t dflt) {
     return e ? uint64_t(std::strtoull(e, nullptr, 10)) : dflt;
 }
 static uint64_t plan_batch_max_bytes() { return env_bytes("VXG_PLAN_BATCH_MAX_BYTES", uint64_t(64) << 20); }
-// vxg_plan_create without VXG_PLAN_MEASURE records one candidate: batched when the plan's
-// canonical output is at most this (C5 shards at 4 / 8 GPUs, 275 / 140 MB: batched 0.095 / 0.060
-// vs unbatched 0.131 / 0.120 ms; at 2 GPUs, 550 MB, unbatched 0.180 vs 0.200).
-constexpr uint64_t kPlanBatchDefaultBytes = 400ull << 20;
+// vxg_plan_create without VXG_PLAN_MEASURE records one candidate: batched.  (Round 4 kept
+// unbatched plans above 400 MB of output: then every small-enough numeric column went to K1g's
+// runtime-width body.  With K1g limited to groups below 20 MiB and the FSST decode inside the
+// K1g launch, batched measured faster at every C5 size in round 5: 1 GPU 0.272 vs 0.289 ms,
+// 2-GPU shard 0.145 vs 0.173, 4 0.072 vs 0.125, 8 0.042 vs 0.104.)
 
 static uint64_t canonical_out_bytes(const vxg_array& a) {
     const bool str = a.dtype == VXG_DTYPE_UTF8 || a.dtype == VXG_DTYPE_BINARY;
@@ -2347,7 +2347,6 @@ vxg_status vxg_plan_create_ex(vxg_ctx* ctx, const vxg_array* arrays, vxg_canonic
     if (!plan || (n && (!arrays || !outs))) return set_error(VXG_ERR_INVALID_ARGUMENT, "null plan/arrays/outs");
     if (flags & ~uint32_t(VXG_PLAN_MEASURE)) return set_error(VXG_ERR_INVALID_ARGUMENT, "unknown plan flags");
     *plan = nullptr;
-    uint64_t total_out = 0;
     for (uint32_t i = 0; i < n; i++) {  // nothing may allocate or synchronise while recording
         const vxg_array& a = arrays[i];
         const vxg_canonical& o = outs[i];
@@ -2356,7 +2355,6 @@ vxg_status vxg_plan_create_ex(vxg_ctx* ctx, const vxg_array* arrays, vxg_canonic
             return set_error(VXG_ERR_INVALID_ARGUMENT, "a plan needs caller-allocated outputs");
         if (a.nullable && !o.validity)
             return set_error(VXG_ERR_INVALID_ARGUMENT, "a plan needs caller-allocated validity for nullable arrays");
-        total_out += canonical_out_bytes(a);
     }
     // candidates: (batched mask, branches); 2 branches unbatched (C5 at 1 GPU 322.6 us/replay vs
     // 362 with 1 and 348 with 3), 1 batched (each cross-branch edge costs a replay several
@@ -2381,10 +2379,8 @@ vxg_status vxg_plan_create_ex(vxg_ctx* ctx, const vxg_array* arrays, vxg_canonic
         if (measure) {
             cand.emplace_back(none, env_br ? env_br : 2u);
             if (n) cand.emplace_back(all, env_br ? env_br : 1u);
-        } else if (n && total_out <= kPlanBatchDefaultBytes) {
-            cand.emplace_back(all, env_br ? env_br : 1u);
         } else {
-            cand.emplace_back(none, env_br ? env_br : 2u);
+            cand.emplace_back(all, env_br ? env_br : 1u);
         }
         break;
     }

@@ -566,9 +566,13 @@ __device__ __forceinline__ uint64_t patch_lower_bound(const PatchCol& pc, uint64
 }
 
 template <int T, int W, Epi EPI, int VW, bool LDSD>
-__device__ __forceinline__ void unpack_chunk_w(const ChunkDev& c, uint64_t g, uint32_t* err, const PatchCol& pc) {
+__device__ __forceinline__ void unpack_chunk_w(const ChunkDev& c, uint64_t g, uint32_t* err, const PatchCol& pc,
+                                               uint32_t bpw_rt) {
     using O = typename EpiOut<T, EPI, VW>::type;
-    constexpr int BPW = kw_bpw(W, LDSD);
+    constexpr int BPW_MAX = kw_bpw(W, LDSD);
+    // blocks per workgroup: the width's maximum (~32 KiB of packed words), or fewer for a launch
+    // too small to fill the chip with it (launch_w)
+    const int BPW = bpw_rt ? int(bpw_rt) : BPW_MAX;
     extern __shared__ __attribute__((aligned(16))) uint8_t k1w_lds[];
     uint8_t* const s_pk = k1w_lds;
     EpiParams ep;
@@ -593,7 +597,7 @@ __device__ __forceinline__ void unpack_chunk_w(const ChunkDev& c, uint64_t g, ui
     // loaded unconditionally).  When the window brackets the range, each thread holds at most one
     // of the workgroup's patches and stores it after the decode; otherwise the range is found by
     // patch_lower_bound.  Scratch: the LDS slack row, whose bytes kw_extract always masks off.
-    uint32_t* const s_pscr = reinterpret_cast<uint32_t*>(k1w_lds + kw_packed_lds<W, LDSD>() - 128);
+    uint32_t* const s_pscr = reinterpret_cast<uint32_t*>(k1w_lds + (W > 0 ? BPW * 128 * W : 0));
     const bool patched = pc.n != 0;
     uint64_t olo = 0, ohi = 0, pbase = 0, pw0 = 0, pw1 = 0;
     uint32_t psh = 0;
@@ -631,8 +635,8 @@ __device__ __forceinline__ void unpack_chunk_w(const ChunkDev& c, uint64_t g, ui
 #if VXG_K1W_BURST
         // A/B variant (VXG_K1W_BURST=1 build): a full workgroup issues all PQ of its thread's
         // loads before any LDS write (PQ * 4 VGPRs; the default loop keeps one load in flight)
-        constexpr int NQ = BPW * 8 * W, PQ = (NQ + 255) / 256;
-        if (nb == BPW) {
+        constexpr int NQ = BPW_MAX * 8 * W, PQ = (NQ + 255) / 256;
+        if (nb == BPW_MAX) {
             u32x4 v[PQ];
 #pragma unroll
             for (int p = 0; p < PQ; p++) {
@@ -656,7 +660,7 @@ __device__ __forceinline__ void unpack_chunk_w(const ChunkDev& c, uint64_t g, ui
     O* const out = static_cast<O*>(c.out);
     const bool aligned = (reinterpret_cast<uintptr_t>(c.out) & 15) == 0;
     bool oob = false;
-    constexpr int PER = BPW / 4;
+    const int PER = BPW / 4;
     for (int j = 0; j < PER; j++) {
         const int b = wave * PER + j;
         if (b >= nb) break;  // wave-uniform
@@ -720,14 +724,14 @@ __global__ __launch_bounds__(256) void fl_unpack_w_kernel(ChunkTable tab) {
     if constexpr (EXT) {
         const ChunkDev& c =
             tab.ext[ext_chunk_index(tab.ext, tab.n, g, [](const ChunkDev& d) { return d.first_group; })];
-        unpack_chunk_w<T, W, EPI, VW, LDSD>(c, g, tab.err, PatchCol{});
+        unpack_chunk_w<T, W, EPI, VW, LDSD>(c, g, tab.err, PatchCol{}, tab.bpw);
     } else {
         uint32_t lo = 0, hi = tab.n;
         while (hi - lo > 1) {
             const uint32_t mid = (lo + hi) >> 1;
             if (tab.c[mid].first_group <= g) lo = mid; else hi = mid;
         }
-        unpack_chunk_w<T, W, EPI, VW, LDSD>(tab.c[lo], g, tab.err, tab.patch);
+        unpack_chunk_w<T, W, EPI, VW, LDSD>(tab.c[lo], g, tab.err, tab.patch, tab.bpw);
     }
 }
 
@@ -752,10 +756,33 @@ __global__ __launch_bounds__(256) void fl_unpack_kernel(ChunkTable tab) {
 }
 
 
+// Workgroups a K1w launch should have at least: with the width's maximum blocks per workgroup
+// a C5 column (6 M values, 5,861 blocks) was 183 workgroups for 256 CUs, one 4-wave workgroup
+// per CU.  VXG_K1W_MIN_GROUPS overrides (read once; 0 keeps the maximum).
+inline uint64_t k1w_min_groups() {
+    static const uint64_t v = [] {
+        const char* e = std::getenv("VXG_K1W_MIN_GROUPS");
+        return e ? uint64_t(std::strtoull(e, nullptr, 10)) : uint64_t(1024);
+    }();
+    return v;
+}
+
 template <int T, int W, Epi EPI, int VW, bool LDSD, bool EXT>
 vxg_status launch_w(ChunkTable tab, hipStream_t s) {
-    constexpr int BPW = kw_bpw(W, LDSD);
+    constexpr int BPW_MAX = kw_bpw(W, LDSD);
     ChunkDev* cs = tab.ext ? tab.host : tab.c;
+    uint64_t blocks = 0;
+    for (uint32_t k = 0; k < tab.n; k++) blocks += cs[k].n_blocks;
+    // fewer blocks per workgroup (a multiple of 4, >= 4) when the maximum leaves the launch
+    // under k1w_min_groups() workgroups; the dictionary stage (LDSD) keeps its fixed offset
+    int BPW = BPW_MAX;
+    const uint64_t want = k1w_min_groups();
+    if (want && blocks < want * uint64_t(BPW_MAX)) {
+        const uint64_t b = blocks / want;
+        BPW = int(b < 4 ? 4 : (b / 4) * 4);
+        if (BPW > BPW_MAX) BPW = BPW_MAX;
+    }
+    tab.bpw = uint32_t(BPW);
     uint64_t groups = 0, dict_bytes = 0;
     for (uint32_t k = 0; k < tab.n; k++) {
         cs[k].first_group = groups;
@@ -765,7 +792,8 @@ vxg_status launch_w(ChunkTable tab, hipStream_t s) {
     }
     if (groups == 0) return VXG_OK;
     if (groups > 0xFFFFFFFFull) return set_error(VXG_ERR_INVALID_ARGUMENT, "array too long for one launch");
-    const size_t shm = size_t(kw_packed_lds<W, LDSD>()) + (LDSD ? size_t(dict_bytes) : 0);
+    const size_t shm = LDSD ? size_t(kw_packed_lds<W, LDSD>()) + size_t(dict_bytes)
+                            : size_t(W > 0 ? BPW * 128 * W : 0) + 128;
     hipLaunchKernelGGL((fl_unpack_w_kernel<T, W, EPI, VW, LDSD, EXT>), dim3(unsigned(groups)), dim3(256), shm, s, tab);
     if constexpr (!EXT) {
         if (tab.patch.n) g_k1w_wrote_patches = true;  // only this kernel reads tab.patch

@@ -276,6 +276,7 @@ struct ChunkTable {
     const ChunkDev* ext;
     ChunkDev* host;
     PatchCol patch;      // kernel-argument tables with n == 1 only (launch_fl_unpack, K1w)
+    uint32_t bpw;        // K1w: blocks per workgroup of this launch (0 = the width's maximum)
 };
 
 // Set (host side) by a kernel-argument K1w launch that was handed tab.patch, the only K1 path
