@@ -97,7 +97,7 @@ thread_local bool g_k1w_wrote_patches = false;
 bool k1_takes_wave(int T, int W, Epi epi, uint64_t groups32) {
     const char* e = std::getenv("VXG_K1_WAVE");
     const int mode = !e ? 1 : (e[0] == '0' ? 0 : (e[0] == 'f' ? 2 : 1));
-    const bool split = (T == 32 || T == 64) && W > 0 && groups32 < kSplitBelowGroups;
+    const bool split = (T == 32 || T == 64) && W > 0 && groups32 < split_below_groups();
     return groups32 > 0 && (mode == 2 || (mode == 1 && !split && epi != Epi::Dict));
 }
 

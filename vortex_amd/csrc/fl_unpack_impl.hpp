@@ -830,7 +830,7 @@ template <int T, int W, Epi EPI, int VW>
 vxg_status launch_one(const ChunkTable& tab, uint64_t groups32, hipStream_t s) {
     if (groups32 == 0) return VXG_OK;
     constexpr bool kSplit = (T == 32 || T == 64) && W > 0;
-    const bool split = kSplit && groups32 < kSplitBelowGroups;
+    const bool split = kSplit && groups32 < split_below_groups();
     bool lds = false;
     if constexpr (EPI == Epi::Dict) {
         const ChunkDev* cs = tab.ext ? tab.host : tab.c;

@@ -284,8 +284,16 @@ struct ChunkTable {
 // scatter when it stays false (no other path may silently drop them).
 extern thread_local bool g_k1w_wrote_patches;
 
-// A launch with fewer 32-block workgroups than this uses the row split (S = 4).
-constexpr uint64_t kSplitBelowGroups = 512;
+// A launch with fewer 32-block workgroups than this uses the row split (S = 4): default 1024
+// (round 5: the C3 8-GPU shard's 32-chunk kernel-argument launch is exactly 512 workgroups of 32
+// blocks, one per two CUs' worth of waves); VXG_SPLIT_BELOW overrides (read once).
+inline uint64_t split_below_groups() {
+    static const uint64_t v = [] {
+        const char* e = std::getenv("VXG_SPLIT_BELOW");
+        return e ? uint64_t(std::strtoull(e, nullptr, 10)) : uint64_t(1024);
+    }();
+    return v;
+}
 // Whether launch_fl_unpack takes K1w for a kernel-argument table of `groups32` 32-block workgroups.
 bool k1_takes_wave(int T, int W, Epi epi, uint64_t groups32);
 
