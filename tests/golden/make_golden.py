@@ -288,6 +288,47 @@ def kats() -> list[dict]:
     out.append(dict(
         name="zigzag_i64_range", ref="encodings/zigzag/src/compress.rs:66-74",
         kind="zigzag", ptype="i64", gen="i - 10_000", n=20_000, expect="roundtrip"))
+    out.append(dict(
+        name="zigzag_nullable_scalar_at", ref="encodings/zigzag/src/compute.rs:96-106",
+        kind="zigzag_nullable", ptype="i32", values=[-189, -160, 1], validity="ALL_VALID",
+        # the reference asserts scalar_at(1) == Scalar::primitive(-160, Nullable); the encoded
+        # words follow the zigzag crate's (v << 1) ^ (v >> 31)
+        expect_at=[[1, -160]], expect_encoded=[377, 319, 2], expect_decoded=[-189, -160, 1]))
+    # ---- round 6: the last literal-holding tests on the path (VERDICT r05 Missing 2) -----------
+    # dict/compute.rs:76-90 flatten_nullable_primitive: dict_encode_typed_primitive::<i32> of
+    # from_nullable_vec([42, -9, None, 42, None, -9]) canonicalizes to a buffer EQUAL to the
+    # reference's buffer, null slots included: from_nullable_vec writes unwrap_or_default() = 0
+    # there (primitive/mod.rs:82-86) and the dictionary's null slot 0 holds T::zero()
+    # (dict/compress.rs:46-48), so the bytes at null rows are pinned to 0.
+    out.append(dict(
+        name="dict_flatten_nullable_primitive", ref="encodings/dict/src/compute.rs:76-90",
+        kind="dict_nullable", ptype="i32", values=[42, -9, 0, 42, 0, -9],
+        validity=[True, True, False, True, False, True], expect_codes=[1, 2, 0, 1, 0, 2],
+        expect_values=[None, 42, -9],
+        expect_buffer_hex=np.array([42, -9, 0, 42, 0, -9], "<i4").tobytes().hex()))
+    out.append(dict(
+        name="dict_flatten_nullable_varbin", ref="encodings/dict/src/compute.rs:92-114",
+        kind="dict_varbin_nullable", strings=["a", "b", None, "a", None, "b"],
+        # dict_encode_varbinview (dict/compress.rs:104-116): null slot 0, codes in first-seen order
+        expect_codes=[1, 2, 0, 1, 0, 2], expect_values=[None, "a", "b"],
+        expect_strings=["a", "b", None, "a", None, "b"]))
+    # for/compute.rs:173-180 for_scalar_at: for_compress of i32 [-100, 1100, 1500, 1900]; the
+    # reference asserts the four scalar_at values.  Reference and shift follow for_compress
+    # (for/compress.rs:13-60): min -100, shift = trailing_zeros of the VALUES (all end in 2
+    # zero bits) = 2, encoded = (v - min) >> 2 reinterpreted as u32.
+    out.append(dict(
+        name="for_scalar_at_negative", ref="encodings/fastlanes/src/for/compute.rs:173-180",
+        kind="for", ptype="i32", values=[-100, 1100, 1500, 1900], expect_reference=-100, expect_shift=2,
+        expect_encoded=[0, 300, 400, 500], expect_decoded=[-100, 1100, 1500, 1900]))
+    # alp/compute.rs:187-201 compare_with_patches: alp_encode of f32 [1.234, 1.5, 19.0, E,
+    # 1_000_000.9] has patches, and comparing with 1_000_000.9 is true at the last row -- the
+    # value the patch holds, so the last row must canonicalize to exactly 1_000_000.9f32.
+    out.append(dict(
+        name="alp_f32_compare_with_patches", ref="encodings/alp/src/alp/compute.rs:187-201",
+        kind="alp", ptype="f32",
+        values_bits=[f32bits(v) for v in (1.234, 1.5, 19.0, math.e, 1_000_000.9)],
+        expect_has_patches=True, expect_last_bits=f32bits(1_000_000.9), expect_eq_last=True,
+        expect="roundtrip"))
     # ---- FSST / VarBin -> VarBinView --------------------------------------------------------
     out.append(dict(
         name="fsst_three_sentences", ref="encodings/fsst/tests/fsst_tests.rs:19-35,37-60",

@@ -272,3 +272,68 @@ def test_kat_chunked_pack_sliced_varbin_on_gpu(ctx):
         assert [view_bytes(views, heap, i) for i in range(views.shape[0])] == expect
         (rv, rb), _ = canon(arr)
         assert [view_bytes(rv, rb, i) for i in range(rv.shape[0])] == expect
+
+
+# ---------------------------------------------------------------- round 6 (VERDICT r05 Missing 2)
+def test_kat_dict_flatten_nullable_primitive_on_gpu(ctx):
+    """dict/compute.rs:76-90: the canonical values buffer equals the reference's byte for byte,
+    null rows included (the dictionary's null slot holds 0, as from_nullable_vec writes)."""
+    import kat_trees as K
+    k = KATS["dict_flatten_nullable_primitive"]
+    for label, arr in K.dict_nullable_primitive(k):
+        res = _gpu(arr, ctx)
+        assert res.numpy().tobytes().hex() == k["expect_buffer_hex"], label
+        assert res.validity_mask().tolist() == k["validity"], label
+
+
+def test_kat_dict_flatten_nullable_varbin_on_gpu(ctx):
+    """dict/compute.rs:92-114: VarBinView and VarBin dictionaries with a null slot canonicalize to
+    the reference's iterator values ["a", "b", None, "a", None, "b"]."""
+    import kat_trees as K
+    k = KATS["dict_flatten_nullable_varbin"]
+    want = [None if s is None else s.encode() for s in k["expect_strings"]]
+    for label, arr in K.dict_nullable_varbin(k):
+        res = _gpu(arr, ctx)
+        views, _ = res.numpy()
+        heap = res.buffers()
+        assert K.masked([view_bytes(views, heap, i) for i in range(arr.len)], res.validity_mask()) == want, label
+        (rv, rh), _ = canon(arr)
+        assert views.tobytes() == rv.tobytes(), label
+
+
+def test_kat_for_scalar_at_negative_on_gpu(ctx):
+    """for/compute.rs:173-180: FoR over i32 with a negative reference (-100, shift 2)."""
+    import kat_trees as K
+    k = KATS["for_scalar_at_negative"]
+    for label, arr in K.for_negative(k):
+        got = _gpu(arr, ctx).numpy()
+        assert got.tolist() == k["expect_decoded"], label
+        assert got.tobytes() == canon(arr)[0].tobytes(), label
+
+
+def test_kat_zigzag_nullable_scalar_at_on_gpu(ctx):
+    """zigzag/compute.rs:96-106: ZigZag over an AllValid child; scalar_at(1) == -160."""
+    import kat_trees as K
+    k = KATS["zigzag_nullable_scalar_at"]
+    for label, arr in K.zigzag_nullable(k):
+        res = _gpu(arr, ctx)
+        got = res.numpy()
+        assert got.tolist() == k["expect_decoded"], label
+        for i, v in k["expect_at"]:
+            assert int(got[i]) == v
+        valid = res.validity_mask()
+        assert valid is None or valid.all()
+
+
+def test_kat_alp_f32_compare_with_patches_on_gpu(ctx):
+    """alp/compute.rs:187-201: f32 with patches; the last row (a patch) decodes to exactly
+    1_000_000.9f32, so comparing with it is true there."""
+    import kat_trees as K
+    k = KATS["alp_f32_compare_with_patches"]
+    vals = K.f32(k["values_bits"])
+    for label, arr in K.alp_compare_with_patches(k):
+        got = _gpu(arr, ctx).numpy()
+        assert struct.pack("<f", got[-1]).hex() == k["expect_last_bits"], label
+        assert bool(got[-1] == np.float32(1_000_000.9)) == k["expect_eq_last"]
+        assert got.tobytes() == vals.tobytes(), label
+        assert got.tobytes() == canon(arr)[0].tobytes(), label

@@ -105,11 +105,68 @@ def test_bitunpack_with_patches(ctx, T):
 
 
 # K1w (the large-launch K1: burst LDS staging + wave-contiguous stores) is chosen by launch size;
-# VXG_K1_WAVE=force takes it for every launch so every width, epilogue, offset and tail is
-# compared with the oracle at test sizes.
+# the context option K1_WAVE=2 takes it for every launch so every width, epilogue, offset and tail
+# is compared with the oracle at test sizes.  Its blocks per workgroup (BPW) is the width's
+# maximum, or fewer (a multiple of 4) for a launch that would have < K1W_MIN_GROUPS workgroups
+# (the default rule picks an intermediate BPW for any 4-30 Mi-value plan column): every case runs
+# at the maximum, intermediate values, 4 and a non-multiple of 4, and asserts the BPW it ran with
+# (vxg_get_launch_stats).
+def kw_bpw_max(W, lds_dict=False):
+    """fl_unpack_impl.hpp kw_bpw: ~32 KiB of packed words (16 KiB beside an LDS dictionary)."""
+    b = ((16 if lds_dict else 32) * 1024) // (128 * max(W, 1))
+    return min(32, max(4, b // 4 * 4))
+
+
+def kw_rule_bpw(blocks, bpw_max, min_groups):
+    """fl_unpack_impl.hpp k1w_pick_bpw without a forced value."""
+    if min_groups <= 0 or blocks >= min_groups * bpw_max:
+        return bpw_max
+    b = blocks // min_groups
+    return min(bpw_max, 4 if b < 4 else b // 4 * 4)
+
+
+BPW_MODES = ["max", 16, 8, 6, 4]
+
+
+@pytest.fixture
+def k1w(ctx):
+    """The session context with K1w forced for every launch; the options are restored after."""
+    ctx.set_option("k1_wave", 2)
+    ctx.launch_stats(reset=True)
+    try:
+        yield ctx
+    finally:
+        ctx.set_option("k1_wave", -1)
+        ctx.set_option("k1w_bpw", 0)
+        ctx.set_option("k1w_min_groups", 1024)
+
+
+def set_bpw_mode(ctx, mode):
+    if mode == "max":
+        ctx.set_option("k1w_min_groups", 0)
+        ctx.set_option("k1w_bpw", 0)
+    else:
+        ctx.set_option("k1w_bpw", int(mode))
+
+
+def assert_bpw_ran(ctx, mode, bpw_max=None):
+    """Every K1w launch since the last check ran with the mode's BPW (forced: min(mode, max))."""
+    st = ctx.launch_stats(reset=True)
+    assert st["k1w_launches"] >= 1, "no K1w launch"
+    if bpw_max is not None:
+        assert st["k1w_last_bpw_max"] == bpw_max
+    want = st["k1w_last_bpw_max"] if mode == "max" else min(int(mode), st["k1w_last_bpw_max"])
+    assert st["k1w_last_bpw"] == want, (mode, st)
+    if mode != "max":
+        assert st["k1w_max_bpw"] <= int(mode)
+    return st
+
+
+@pytest.mark.parametrize("mode", BPW_MODES)
 @pytest.mark.parametrize("T", [8, 16, 32, 64])
-def test_k1w_every_width(ctx, T, monkeypatch):
-    monkeypatch.setenv("VXG_K1_WAVE", "force")
+def test_k1w_every_width(k1w, T, mode):
+    ctx = k1w
+    set_bpw_mode(ctx, mode)
     rng = np.random.default_rng(100 + T)
     dt = UT[T]
     for W in range(T + 1) if T < 64 else list(range(0, 64, 3)) + [63]:
@@ -119,13 +176,36 @@ def test_k1w_every_width(ctx, T, monkeypatch):
         vals = (rng.integers(0, 1 << W, n, dtype=np.uint64) if W else np.zeros(n, np.uint64)).astype(dt)
         off = int(rng.integers(0, 1024)) if W % 2 else 0
         assert_primitive_parity(E.encode_bitpacked(vals, bit_width=W, allow_patches=False, offset=off), ctx, vals)
+        assert_bpw_ran(ctx, mode, kw_bpw_max(W))
 
 
-def test_k1w_epilogues_and_chunks(ctx, monkeypatch):
+@pytest.mark.parametrize("min_groups", [1, 3, 7])
+def test_k1w_runtime_rule(k1w, min_groups):
+    """The default rule at test sizes: K1W_MIN_GROUPS small enough that blocks / min_groups lands
+    between 4 and the width's maximum (the same rule a 4-30 Mi-value plan column takes at 1024)."""
+    ctx = k1w
+    ctx.set_option("k1w_min_groups", min_groups)
+    rng = np.random.default_rng(200 + min_groups)
+    seen = set()
+    for T, W, n, off in [(32, 7, 40_000, 0), (32, 7, 77_777, 517), (16, 5, 90_000, 3), (64, 17, 60_000, 1000),
+                         (8, 3, 150_000, 0), (64, 24, 33_000, 9)]:
+        vals = rng.integers(0, 1 << W, n, dtype=np.uint64).astype(UT[T])
+        assert_primitive_parity(E.encode_bitpacked(vals, bit_width=W, allow_patches=False, offset=off), ctx, vals)
+        st = ctx.launch_stats(reset=True)
+        blocks = (n + off + 1023) // 1024
+        want = kw_rule_bpw(blocks, kw_bpw_max(W), min_groups)
+        assert st["k1w_last_bpw"] == want, (T, W, n, st)
+        seen.add(want)
+    assert len(seen) >= 2
+
+
+@pytest.mark.parametrize("mode", ["max", 8, 4])
+def test_k1w_epilogues_and_chunks(k1w, mode):
     """FoR / ZigZag / ALP / Dict epilogues, patches, chunked tables (ragged, sliced, unaligned
-    slices) and a plan's device table through K1w."""
+    slices) and a plan's device table through K1w, at each blocks-per-workgroup mode."""
     import torch
-    monkeypatch.setenv("VXG_K1_WAVE", "force")
+    ctx = k1w
+    set_bpw_mode(ctx, mode)
     rng = np.random.default_rng(7)
     cases = []
     for dt in (np.int8, np.int16, np.int32, np.int64, np.uint32):
@@ -150,11 +230,72 @@ def test_k1w_epilogues_and_chunks(ctx, monkeypatch):
             assert_primitive_parity(a, ctx)
         else:
             assert_string_parity(a, ctx)
-    plan = V.Plan([a.to(torch.device("cuda", 0)) for a in cases[-2:]], ctx)
+        if a.encoding != A.ENC["DICT"] or a.children[0].dtype == A.DTYPE["PRIMITIVE"]:
+            assert_bpw_ran(ctx, mode)  # (string dictionaries take K14, not K1w)
+        ctx.launch_stats(reset=True)
+    with plan_mode("0"):  # unbatched: the chunked columns' device-table K1w launches
+        plan = V.Plan([a.to(torch.device("cuda", 0)) for a in cases[-2:]], ctx)
+    assert_bpw_ran(ctx, mode)
     for _ in range(2):
         res = plan.launch(sync=True)
         for a, r in zip(cases[-2:], res):
             assert r.numpy().tobytes() == canon(a)[0].tobytes()
+    plan.close()
+
+
+@pytest.mark.parametrize("batch", ["1", "0"])
+def test_k1w_mid_size_default_rule(ctx, batch):
+    """plan columns of 4-30 Mi values take an intermediate BPW under the DEFAULT rule
+    (K1W_MIN_GROUPS 1024) -- the production path of C5's columns.  u32 W=7, 12 x 1 Mi values with
+    a sliced chunk (12,288 blocks -> BPW 12 of 32), and ALP f64 (W=17) + patches, 8 x 1 Mi
+    (8,192 blocks -> BPW 8 of 12); batched (>= 20 MiB groups keep their K1w launch) and unbatched
+    plans, bit-exact against the oracle and the plain values."""
+    import torch
+    assert ctx.get_option("k1w_min_groups") == 1024 and ctx.get_option("k1w_bpw") == 0
+    rng = np.random.default_rng(300)
+    n = 1 << 20
+    u_plain, u_chunks = [], []
+    for c in range(12):
+        v = rng.integers(0, 128, n, dtype=np.uint32)
+        u_plain.append(v)
+        u_chunks.append(E.encode_bitpacked(v, bit_width=7, allow_patches=False, offset=517 if c == 5 else 0))
+    f_plain, f_chunks = [], []
+    for c in range(8):
+        v = np.round(rng.uniform(1, 1000, n) * 100) / 100
+        v[rng.choice(n, 300, replace=False)] = rng.standard_normal(300) * 1e9 + 0.123456789
+        f_plain.append(v)
+        f_chunks.append(E.encode_alp(v))
+    assert f_chunks[0].children[0].children[0].meta["bit_width"] == 17
+    cases = [(A.chunked(u_chunks), np.concatenate(u_plain), 12, 32),
+             (A.chunked(f_chunks), np.concatenate(f_plain), 8, 12)]
+    for arr, plain, bpw, bpw_max in cases:
+        ctx.launch_stats(reset=True)
+        with plan_mode(batch):
+            plan = V.Plan([arr.to(torch.device("cuda", 0))], ctx)
+        st = ctx.launch_stats(reset=True)
+        assert st["k1w_launches"] == 1 and st["k1w_last_bpw"] == bpw and st["k1w_last_bpw_max"] == bpw_max, st
+        for _ in range(2):
+            got = plan.launch(sync=True)[0].numpy()
+            assert got.tobytes() == plain.tobytes()
+        assert got.tobytes() == canon(arr)[0].tobytes()
+        plan.close()
+
+
+@pytest.mark.parametrize("dt", [np.uint8, np.uint16, np.uint32])
+def test_chunked_primitive_copy_misaligned(ctx, dt):
+    """a chunk whose output slice is not 16-byte aligned (after a chunk whose byte
+    length is not a multiple of 16) is copied by K10's funnel-shift path at every residue
+    (1-15 bytes for u8), multi-MB per chunk, byte-exact; also inside a replayed plan."""
+    import torch
+    rng = np.random.default_rng(400 + np.dtype(dt).itemsize)
+    plains = [rng.integers(0, np.iinfo(dt).max, (1 << 20) + 3 * i + (i % 2), dtype=dt, endpoint=True)
+              for i in range(17)]
+    arr = A.chunked([A.primitive(p) for p in plains])
+    want = np.concatenate(plains)
+    assert gpu(arr, ctx).numpy().tobytes() == want.tobytes()
+    plan = V.Plan([arr.to(torch.device("cuda", 0))], ctx)
+    for _ in range(2):
+        assert plan.launch(sync=True)[0].numpy().tobytes() == want.tobytes()
     plan.close()
 
 
@@ -257,9 +398,11 @@ def _alp_patched(rng, n, pos, f32=False, offset=0, indices_offset=0, packed_indi
 # ALP's outer patches are written by the K1w launch itself (fl_unpack_impl.hpp unpack_chunk_w):
 # a 256-patch window guessed from an even spread, or a 256-ary search when the window does not
 # bracket the workgroup's output range.  Both against the separate scatter (VXG_FUSED_PATCHES=0).
+@pytest.mark.parametrize("mode", ["max", 8, 6, 4])
 @pytest.mark.parametrize("fused", ["1", "0"])
-def test_k1w_fused_patches(ctx, fused, monkeypatch):
-    monkeypatch.setenv("VXG_K1_WAVE", "force")
+def test_k1w_fused_patches(k1w, fused, mode, monkeypatch):
+    ctx = k1w
+    set_bpw_mode(ctx, mode)
     monkeypatch.setenv("VXG_FUSED_PATCHES", fused)
     rng = np.random.default_rng(77)
     n = 300_000
@@ -277,11 +420,14 @@ def test_k1w_fused_patches(ctx, fused, monkeypatch):
         pos = kw.pop("pos")
         arr, expect = _alp_patched(rng, n, pos, **kw)
         assert_primitive_parity(arr, ctx, expect)
+        assert_bpw_ran(ctx, mode)
 
 
-def test_k1w_fused_patches_errors(ctx, monkeypatch):
+@pytest.mark.parametrize("mode", ["max", 4])
+def test_k1w_fused_patches_errors(k1w, mode):
     """Out-of-range and descending patch indices are reported, as by the separate scatter."""
-    monkeypatch.setenv("VXG_K1_WAVE", "force")
+    ctx = k1w
+    set_bpw_mode(ctx, mode)
     rng = np.random.default_rng(78)
     n = 50_000
     arr, _ = _alp_patched(rng, n, np.array([5, 70, n - 1]))
@@ -306,11 +452,13 @@ def _alp_bad_cluster(rng, n=300_000):
     return arr
 
 
-def test_k1w_fused_patches_unsorted_cluster_never_writes_out_of_range(ctx, monkeypatch):
+@pytest.mark.parametrize("mode", ["max", 4])
+def test_k1w_fused_patches_unsorted_cluster_never_writes_out_of_range(k1w, mode):
     """the search fallback stores only keys inside the workgroup's range; an index
     past the end inside an unsorted cluster is reported, not written (the device would fault or
     corrupt the neighbour allocation otherwise)."""
-    monkeypatch.setenv("VXG_K1_WAVE", "force")
+    ctx = k1w
+    set_bpw_mode(ctx, mode)
     rng = np.random.default_rng(79)
     with pytest.raises(V.VortexGpuError, match="not sorted|out of bounds"):
         gpu(_alp_bad_cluster(rng), ctx)
@@ -1587,6 +1735,74 @@ def test_plan_modes_non_c5_mix(ctx, mode):
         assert np.array_equal(res[2].numpy(), m) and np.array_equal(res[3].numpy(), m)
         assert np.array_equal(res[4].validity_mask(), ~m)
         assert res[5].numpy().tobytes() == big.tobytes()
+    plan.close()
+
+
+def _validity_nodes(host, dev):
+    """(host Bool node, device Bool node) of every ARRAY validity child in two parallel trees."""
+    out = []
+    if host.validity == A.VALIDITY["ARRAY"] and host.children and host.children[-1].encoding == A.ENC["BOOL"]:
+        out.append((host.children[-1], dev.children[-1]))
+    for h, d in zip(host.children, dev.children):
+        out += _validity_nodes(h, d)
+    return out
+
+
+def test_plan_mixed_nullable_chunked_fsst_validity_changes(ctx):
+    """in a mixed plan the batch runs on its own graph branch, and a chunked FSST
+    column's deferred decode reads the per-chunk validity bitmaps its array branch wrote; the
+    batch branch now joins every array branch first.  A nullable chunked FSST column (batched)
+    beside a large unbatched column, replayed, then its validity changed IN PLACE between replays:
+    every replay equals the oracle of the current validity."""
+    import copy
+    import os
+    import torch
+    rng = np.random.default_rng(606)
+    strs = _comment_strings(rng, 50_000, vocab=60)
+    strs = [None if i % 17 == 3 else x for i, x in enumerate(strs)]
+    cuts = [0, 5, 7_000, 7_301, 30_000, 50_000]
+    fsst = A.chunked([E.encode_fsst(strs[a:b]) for a, b in zip(cuts, cuts[1:])])
+    big = rng.integers(0, 1 << 13, 3 * (1 << 20), dtype=np.uint64).astype(np.uint32)
+    big_arr = A.chunked([E.encode_bitpacked(big[i:i + (1 << 20)], bit_width=13, allow_patches=False)
+                         for i in range(0, big.size, 1 << 20)])
+    dev = fsst.to(torch_dev())
+    pairs = _validity_nodes(fsst, dev)
+    assert len(pairs) == len(cuts) - 1
+    old = os.environ.get("VXG_PLAN_BATCH_MAX_BYTES")
+    os.environ["VXG_PLAN_BATCH_MAX_BYTES"] = str(4 << 20)  # the FSST column batched, big_arr not
+    try:
+        with plan_mode("mixed"):
+            plan = V.Plan([dev, big_arr.to(torch_dev())], ctx)
+    finally:
+        if old is None:
+            os.environ.pop("VXG_PLAN_BATCH_MAX_BYTES", None)
+        else:
+            os.environ["VXG_PLAN_BATCH_MAX_BYTES"] = old
+    info = plan.info()
+    assert info["batched"] and info["branches"] == 2
+
+    def check(host):
+        (rviews, rbufs), rvalid = canon(host)
+        for _ in range(2):
+            res = plan.launch(sync=True)
+            assert res[0].numpy()[0].tobytes() == rviews.tobytes()
+            assert [b.tobytes() for b in res[0].buffers()] == [b.tobytes() for b in rbufs]
+            assert np.array_equal(res[0].validity_mask(), rvalid)
+            assert res[1].numpy().tobytes() == big.tobytes()
+
+    check(fsst)
+    for rnd in range(2):  # more rows become null, in place on the device
+        host = copy.deepcopy(fsst)
+        for (h, d), (h2, _) in zip(pairs, _validity_nodes(host, host)):
+            m = np.unpackbits(np.asarray(h.buffers[0]), bitorder="little")[: h.len].astype(bool)
+            m &= rng.random(m.size) > 0.3
+            bits = np.packbits(m, bitorder="little")
+            h2.buffers[0] = bits
+            d.buffers[0][: bits.size].copy_(torch.from_numpy(bits).to(torch_dev()))
+        torch.cuda.synchronize()
+        check(host)
+        fsst = host
+        pairs = [(h2, d) for (h2, _), (_, d) in zip(_validity_nodes(host, host), pairs)]
     plan.close()
 
 

@@ -691,3 +691,60 @@ def test_kat_chunked_pack_sliced_varbin():
     chunks = [slice_checked(base, *s) for s in k["slices"]]
     (views, bufs), _ = canon(A.chunked(chunks))
     assert [view_bytes(views, bufs, i).decode() for i in range(views.shape[0])] == k["expect"]
+
+
+# ---- round 6: the last literal-holding reference tests on the path (VERDICT r05 Missing 2) ----
+def test_kat_dict_flatten_nullable_primitive():
+    """dict/compute.rs:76-90: the canonical BUFFER equals from_nullable_vec's, null slots (0)
+    included -- every byte pinned, not only the valid rows."""
+    import kat_trees as K
+    k = KATS["dict_flatten_nullable_primitive"]
+    codes, dv, vvalid = E.dict_encode_nullable(np.array(k["values"], np.int32), k["validity"])
+    assert codes.tolist() == k["expect_codes"]
+    assert [None if not ok else int(x) for x, ok in zip(dv, vvalid)] == k["expect_values"]
+    for label, arr in K.dict_nullable_primitive(k):
+        got, valid = canon(arr)
+        assert got.tobytes().hex() == k["expect_buffer_hex"], label
+        assert valid.tolist() == k["validity"], label
+
+
+def test_kat_dict_flatten_nullable_varbin():
+    import kat_trees as K
+    k = KATS["dict_flatten_nullable_varbin"]
+    want = [None if s is None else s.encode() for s in k["expect_strings"]]
+    for label, arr in K.dict_nullable_varbin(k):
+        assert canon(arr.children[1])[0].tolist() == k["expect_codes"], label
+        (views, heap), valid = canon(arr)
+        assert K.masked([view_bytes(views, heap, i) for i in range(arr.len)], valid) == want, label
+
+
+def test_kat_for_scalar_at_negative():
+    import kat_trees as K
+    k = KATS["for_scalar_at_negative"]
+    enc, ref, shift = E.for_compress(np.array(k["values"], np.int32))
+    assert (ref, shift, enc.tolist()) == (k["expect_reference"], k["expect_shift"], k["expect_encoded"])
+    for label, arr in K.for_negative(k):
+        assert canon(arr)[0].tolist() == k["expect_decoded"], label
+
+
+def test_kat_zigzag_nullable_scalar_at():
+    import kat_trees as K
+    k = KATS["zigzag_nullable_scalar_at"]
+    assert E.zigzag_encode(np.array(k["values"], np.int32)).tolist() == k["expect_encoded"]
+    for label, arr in K.zigzag_nullable(k):
+        got, valid = canon(arr)
+        assert got.tolist() == k["expect_decoded"] and (valid is None or valid.all()), label
+        for i, v in k["expect_at"]:
+            assert int(got[i]) == v
+
+
+def test_kat_alp_f32_compare_with_patches():
+    import kat_trees as K
+    k = KATS["alp_f32_compare_with_patches"]
+    vals = K.f32(k["values_bits"])
+    for label, arr in K.alp_compare_with_patches(k):
+        assert arr.meta["has_patches"] == k["expect_has_patches"], label
+        got, _ = canon(arr)
+        assert struct.pack("<f", got[-1]).hex() == k["expect_last_bits"], label
+        assert bool(got[-1] == np.float32(1_000_000.9)) == k["expect_eq_last"]
+        assert got.tobytes() == vals.tobytes(), label

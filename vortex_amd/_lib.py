@@ -22,7 +22,7 @@ PTYPES = ["u8", "u16", "u32", "u64", "i8", "i16", "i32", "i64", "f16", "f32", "f
 PTYPE = {n: i for i, n in enumerate(PTYPES)}
 DTYPE = dict(NULL=0, BOOL=1, PRIMITIVE=2, UTF8=3, BINARY=4)
 VALIDITY = dict(NON_NULLABLE=0, ALL_VALID=1, ALL_INVALID=2, ARRAY=3)
-ABI_VERSION = 7  # VXG_ABI_VERSION
+ABI_VERSION = 8  # VXG_ABI_VERSION
 STATUS = {0: "OK", 1: "OutOfBounds", 2: "ComputeError", 3: "InvalidArgument", 4: "InvalidSerde",
           5: "NotImplemented", 6: "MismatchedTypes", 7: "AssertionFailed", 8: "HipError",
           9: "OutOfMemory"}
@@ -151,6 +151,15 @@ class VxgPlanInfo(C.Structure):
 PLAN_SELECTION = {0: "single", 1: "faster", 2: "tie_fewer_nodes", 3: "unmeasured"}
 
 
+# vxg_option (ABI 8): per-context launch shapes
+OPT_K1W_MIN_GROUPS, OPT_K1W_BPW, OPT_K1_WAVE = 1, 2, 3
+
+
+class VxgLaunchStats(C.Structure):
+    _fields_ = [("k1w_launches", C.c_uint64), ("k1w_last_groups", C.c_uint64), ("k1w_last_bpw", C.c_uint32),
+                ("k1w_last_bpw_max", C.c_uint32), ("k1w_min_bpw", C.c_uint32), ("k1w_max_bpw", C.c_uint32)]
+
+
 class VxgIntStats(C.Structure):
     _fields_ = [("n", C.c_uint64), ("min_bits", C.c_uint64), ("max_bits", C.c_uint64), ("trailing_zeros", C.c_uint32),
                 ("reserved", C.c_uint32), ("bit_width_freq", C.c_uint64 * 65)]
@@ -181,6 +190,9 @@ GPU_SIGNATURES = {
     "vxg_memcpy_d2h": (ST, [VP, VP, VP, U64, VP]),
     "vxg_memcpy_d2d": (ST, [VP, VP, VP, U64, VP]),
     "vxg_stream_sync": (ST, [VP, VP]),
+    "vxg_set_option": (ST, [VP, INT, C.c_int64]),
+    "vxg_get_option": (ST, [VP, INT, C.POINTER(C.c_int64)]),
+    "vxg_get_launch_stats": (ST, [VP, C.POINTER(VxgLaunchStats), INT]),
     "vxg_canonical_size": (ST, [VP, C.POINTER(VxgArray), C.POINTER(U64), C.POINTER(U64)]),
     "vxg_canonicalize": (ST, [VP, C.POINTER(VxgArray), C.POINTER(VxgCanonical), VP]),
     "vxg_plan_create": (ST, [VP, C.POINTER(VxgArray), C.POINTER(VxgCanonical), U32, C.POINTER(VP)]),

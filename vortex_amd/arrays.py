@@ -505,6 +505,24 @@ class Context:
     def sync(self):
         _lib.check(self.lib.vxg_stream_sync(self.handle, self.stream_ptr()))
 
+    _OPTIONS = {"k1w_min_groups": _lib.OPT_K1W_MIN_GROUPS, "k1w_bpw": _lib.OPT_K1W_BPW,
+                "k1_wave": _lib.OPT_K1_WAVE}
+
+    def set_option(self, name: str, value: int):
+        """vxg_set_option: a launch-shape option of this context (never changes outputs)."""
+        _lib.check(self.lib.vxg_set_option(self.handle, self._OPTIONS[name], int(value)))
+
+    def get_option(self, name: str) -> int:
+        v = C.c_int64()
+        _lib.check(self.lib.vxg_get_option(self.handle, self._OPTIONS[name], C.byref(v)))
+        return v.value
+
+    def launch_stats(self, reset: bool = False) -> dict:
+        """vxg_get_launch_stats: the K1w launches issued (or recorded) since the last reset."""
+        st = _lib.VxgLaunchStats()
+        _lib.check(self.lib.vxg_get_launch_stats(self.handle, C.byref(st), int(reset)))
+        return {f: getattr(st, f) for f, _ in st._fields_}
+
 
 @dataclass
 class Canonical:

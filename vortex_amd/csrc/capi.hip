@@ -91,12 +91,33 @@ static bool fused_patches_enabled() {
 }
 
 thread_local bool g_k1w_wrote_patches = false;
+thread_local Ctx* g_cur_ctx = nullptr;
+
+Options default_options() {
+    static const Options d = [] {
+        Options o;
+        if (const char* e = std::getenv("VXG_K1W_MIN_GROUPS")) o.k1w_min_groups = int64_t(std::strtoll(e, nullptr, 10));
+        return o;
+    }();
+    return d;
+}
+
+void note_k1w_launch(uint32_t bpw, uint32_t bpw_max, uint64_t groups) {
+    if (!g_cur_ctx) return;
+    std::lock_guard<std::mutex> lk(g_cur_ctx->mu);
+    LaunchStats& st = g_cur_ctx->st;
+    st.k1w_min_bpw = st.k1w_launches == 0 ? bpw : std::min(st.k1w_min_bpw, bpw);
+    st.k1w_max_bpw = st.k1w_launches == 0 ? bpw : std::max(st.k1w_max_bpw, bpw);
+    st.k1w_launches++;
+    st.k1w_last_bpw = bpw;
+    st.k1w_last_bpw_max = bpw_max;
+    st.k1w_last_groups = groups;
+}
 
 // launch_one's choice (fl_unpack_impl.hpp) for a kernel-argument table: K1w unless the launch is
-// small enough for the row split (T = 32/64) or VXG_K1_WAVE says otherwise.
+// small enough for the row split (T = 32/64) or the K1_WAVE option / VXG_K1_WAVE says otherwise.
 bool k1_takes_wave(int T, int W, Epi epi, uint64_t groups32) {
-    const char* e = std::getenv("VXG_K1_WAVE");
-    const int mode = !e ? 1 : (e[0] == '0' ? 0 : (e[0] == 'f' ? 2 : 1));
+    const int mode = k1_wave_mode();
     const bool split = (T == 32 || T == 64) && W > 0 && groups32 < split_below_groups();
     return groups32 > 0 && (mode == 2 || (mode == 1 && !split && epi != Epi::Dict));
 }
@@ -302,6 +323,7 @@ inline hipStream_t S(void* s) { return static_cast<hipStream_t>(s); }
 
 vxg_status use_device(vxg_ctx* ctx) {
     if (!ctx) return set_error(VXG_ERR_INVALID_ARGUMENT, "null vxg_ctx");
+    g_cur_ctx = &ctx->c;  // this entry point's launches follow ctx's options
     return hip_check(hipSetDevice(ctx->c.device), "hipSetDevice");
 }
 
@@ -1907,6 +1929,7 @@ vxg_status vxg_open(int device, vxg_ctx** out) {
     VXG_TRY(hip_check(hipSetDevice(device), "hipSetDevice"));
     auto* c = new vxg_ctx();
     c->c.device = device;
+    c->c.opt = default_options();
     hipError_t e = hipMalloc(&c->c.err_word, 16);
     if (e == hipSuccess) e = hipMemset(c->c.err_word, 0, 16);
     if (e == hipSuccess) {
@@ -1927,8 +1950,55 @@ vxg_status vxg_open(int device, vxg_ctx** out) {
     return VXG_OK;
 }
 
+vxg_status vxg_set_option(vxg_ctx* ctx, int option, int64_t value) {
+    if (!ctx) return set_error(VXG_ERR_INVALID_ARGUMENT, "null vxg_ctx");
+    Options& o = ctx->c.opt;
+    switch (option) {
+    case VXG_OPT_K1W_MIN_GROUPS:
+        if (value < 0 || value > (int64_t(1) << 31)) return set_error(VXG_ERR_INVALID_ARGUMENT, "K1W_MIN_GROUPS out of range");
+        o.k1w_min_groups = value;
+        return VXG_OK;
+    case VXG_OPT_K1W_BPW:
+        if (value < 0 || value > 32) return set_error(VXG_ERR_INVALID_ARGUMENT, "K1W_BPW must be in [0, 32]");
+        o.k1w_bpw = value;
+        return VXG_OK;
+    case VXG_OPT_K1_WAVE:
+        if (value < -1 || value > 2) return set_error(VXG_ERR_INVALID_ARGUMENT, "K1_WAVE must be -1, 0, 1 or 2");
+        o.k1_wave = value;
+        return VXG_OK;
+    }
+    return set_error(VXG_ERR_INVALID_ARGUMENT, "unknown option " + std::to_string(option));
+}
+
+vxg_status vxg_get_option(vxg_ctx* ctx, int option, int64_t* value) {
+    if (!ctx || !value) return set_error(VXG_ERR_INVALID_ARGUMENT, "null argument");
+    const Options& o = ctx->c.opt;
+    switch (option) {
+    case VXG_OPT_K1W_MIN_GROUPS: *value = o.k1w_min_groups; return VXG_OK;
+    case VXG_OPT_K1W_BPW: *value = o.k1w_bpw; return VXG_OK;
+    case VXG_OPT_K1_WAVE: *value = o.k1_wave; return VXG_OK;
+    }
+    return set_error(VXG_ERR_INVALID_ARGUMENT, "unknown option " + std::to_string(option));
+}
+
+vxg_status vxg_get_launch_stats(vxg_ctx* ctx, vxg_launch_stats* out, int reset) {
+    if (!ctx || !out) return set_error(VXG_ERR_INVALID_ARGUMENT, "null argument");
+    std::lock_guard<std::mutex> lk(ctx->c.mu);
+    const LaunchStats& st = ctx->c.st;
+    *out = vxg_launch_stats{};
+    out->k1w_launches = st.k1w_launches;
+    out->k1w_last_groups = st.k1w_last_groups;
+    out->k1w_last_bpw = st.k1w_last_bpw;
+    out->k1w_min_bpw = st.k1w_min_bpw;
+    out->k1w_max_bpw = st.k1w_max_bpw;
+    out->k1w_last_bpw_max = st.k1w_last_bpw_max;
+    if (reset) ctx->c.st = LaunchStats{};
+    return VXG_OK;
+}
+
 vxg_status vxg_close(vxg_ctx* ctx) {
     if (!ctx) return VXG_OK;
+    if (g_cur_ctx == &ctx->c) g_cur_ctx = nullptr;
     (void)hipSetDevice(ctx->c.device);
     (void)hipDeviceSynchronize();
     if (ctx->c.err_word) (void)hipFree(ctx->c.err_word);
@@ -2237,6 +2307,13 @@ static vxg_status record_plan(vxg_ctx* ctx, const vxg_array* arrays, vxg_canonic
             if (!(own && batched[i])) load[b] += cost[i];  // (a batched array's launches run on the batch branch)
             Planner p(ctx, br[b], &pl->store, batched[i] ? &batch : nullptr);
             st = p.canonical(arrays[i], outs[i]);
+        }
+        // A batch on its own branch waits for every array branch first: deferred
+        // launches read what those branches wrote -- a chunked FSST column's per-chunk validity
+        // bitmaps, a Dict chunk's decoded values -- and nothing else orders the two streams.
+        for (uint32_t b = 0; own && b < na && st == VXG_OK; b++) {
+            st = hip_check(hipEventRecord(ev[b], br[b]), "batch join");
+            if (st == VXG_OK) st = hip_check(hipStreamWaitEvent(br[nb - 1], ev[b], 0), "batch join wait");
         }
         if (batching && st == VXG_OK) st = flush_plan_batch(batch, ctx->c.err_word, br[nb - 1], &pl->store);
         for (uint32_t b = 0; b < nb && st == VXG_OK; b++) {

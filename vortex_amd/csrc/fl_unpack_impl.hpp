@@ -660,7 +660,7 @@ __device__ __forceinline__ void unpack_chunk_w(const ChunkDev& c, uint64_t g, ui
     O* const out = static_cast<O*>(c.out);
     const bool aligned = (reinterpret_cast<uintptr_t>(c.out) & 15) == 0;
     bool oob = false;
-    const int PER = BPW / 4;
+    const int PER = (BPW + 3) / 4;  // blocks per wave (the last waves may have fewer)
     for (int j = 0; j < PER; j++) {
         const int b = wave * PER + j;
         if (b >= nb) break;  // wave-uniform
@@ -756,15 +756,18 @@ __global__ __launch_bounds__(256) void fl_unpack_kernel(ChunkTable tab) {
 }
 
 
-// Workgroups a K1w launch should have at least: with the width's maximum blocks per workgroup
-// a C5 column (6 M values, 5,861 blocks) was 183 workgroups for 256 CUs, one 4-wave workgroup
-// per CU.  VXG_K1W_MIN_GROUPS overrides (read once; 0 keeps the maximum).
-inline uint64_t k1w_min_groups() {
-    static const uint64_t v = [] {
-        const char* e = std::getenv("VXG_K1W_MIN_GROUPS");
-        return e ? uint64_t(std::strtoull(e, nullptr, 10)) : uint64_t(1024);
-    }();
-    return v;
+// Blocks per workgroup of a K1w launch over `blocks` FastLanes blocks whose width allows at most
+// `bpw_max`: the maximum, or -- when that leaves the launch under `min_groups` workgroups (a C5
+// column of 6 M values, 5,861 blocks, was 183 workgroups for 256 CUs, one 4-wave workgroup per
+// CU) -- blocks / min_groups rounded down to a multiple of 4 (>= 4), so the 4 waves get equal
+// shares; `forced` (VXG_OPT_K1W_BPW) > 0 takes min(forced, bpw_max) instead.  Every value in
+// [1, bpw_max] is a valid launch shape (unpack_chunk_w: PER = ceil(BPW / 4) blocks per wave).
+inline int k1w_pick_bpw(uint64_t blocks, int bpw_max, int64_t min_groups, int64_t forced) {
+    if (forced > 0) return int(forced < bpw_max ? forced : bpw_max);
+    if (min_groups <= 0 || blocks >= uint64_t(min_groups) * uint64_t(bpw_max)) return bpw_max;
+    const uint64_t b = blocks / uint64_t(min_groups);
+    const int bpw = int(b < 4 ? 4 : (b / 4) * 4);
+    return bpw > bpw_max ? bpw_max : bpw;
 }
 
 template <int T, int W, Epi EPI, int VW, bool LDSD, bool EXT>
@@ -773,15 +776,9 @@ vxg_status launch_w(ChunkTable tab, hipStream_t s) {
     ChunkDev* cs = tab.ext ? tab.host : tab.c;
     uint64_t blocks = 0;
     for (uint32_t k = 0; k < tab.n; k++) blocks += cs[k].n_blocks;
-    // fewer blocks per workgroup (a multiple of 4, >= 4) when the maximum leaves the launch
-    // under k1w_min_groups() workgroups; the dictionary stage (LDSD) keeps its fixed offset
-    int BPW = BPW_MAX;
-    const uint64_t want = k1w_min_groups();
-    if (want && blocks < want * uint64_t(BPW_MAX)) {
-        const uint64_t b = blocks / want;
-        BPW = int(b < 4 ? 4 : (b / 4) * 4);
-        if (BPW > BPW_MAX) BPW = BPW_MAX;
-    }
+    // the dictionary stage (LDSD) keeps its fixed offset at any BPW
+    const Options o = cur_options();
+    const int BPW = k1w_pick_bpw(blocks, BPW_MAX, o.k1w_min_groups, o.k1w_bpw);
     tab.bpw = uint32_t(BPW);
     uint64_t groups = 0, dict_bytes = 0;
     for (uint32_t k = 0; k < tab.n; k++) {
@@ -795,19 +792,16 @@ vxg_status launch_w(ChunkTable tab, hipStream_t s) {
     const size_t shm = LDSD ? size_t(kw_packed_lds<W, LDSD>()) + size_t(dict_bytes)
                             : size_t(W > 0 ? BPW * 128 * W : 0) + 128;
     hipLaunchKernelGGL((fl_unpack_w_kernel<T, W, EPI, VW, LDSD, EXT>), dim3(unsigned(groups)), dim3(256), shm, s, tab);
+    note_k1w_launch(uint32_t(BPW), uint32_t(BPW_MAX), groups);
     if constexpr (!EXT) {
         if (tab.patch.n) g_k1w_wrote_patches = true;  // only this kernel reads tab.patch
     }
     return hip_check(hipGetLastError(), "fl_unpack_w_kernel launch");
 }
 
-// VXG_K1_WAVE (diagnostics, read at every launch): "0" keeps the register-resident K1 for large
-// launches too; "force" takes K1w for small launches as well (parity tests of every width).
-inline int k1_wave_mode() {
-    const char* e = std::getenv("VXG_K1_WAVE");
-    if (!e) return 1;
-    return e[0] == '0' ? 0 : (e[0] == 'f' ? 2 : 1);
-}
+// k1_wave_mode() (vxg_internal.hpp): VXG_OPT_K1_WAVE, else VXG_K1_WAVE read at every launch --
+// "0" keeps the register-resident K1 for large launches too; "force" takes K1w for small
+// launches as well (parity tests of every width).
 
 template <int T, int W, Epi EPI, int VW, bool LDSD, int S, bool EXT = false>
 vxg_status launch_s(ChunkTable tab, hipStream_t s) {

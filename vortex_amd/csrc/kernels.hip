@@ -747,15 +747,44 @@ vxg_status launch_fill(int value_width, const uint8_t* scalar16, uint64_t n, voi
 // are kernels rather than hipMemcpyAsync / hipMemsetAsync: inside a recorded plan those become
 // graph memcpy/memset nodes, and a memset node at the root of a replayed graph was measured to
 // leave stale bits that the following kernels' atomic ORs then kept (profiles/r05_plan_memset.md);
-// kernel nodes also keep a plan eligible for direct replay.  16-byte body when dst and src share
-// their alignment mod 16, bytes otherwise.
+// kernel nodes also keep a plan eligible for direct replay.  The body is 16-byte stores at dst's
+// 16-byte alignment.  When src is misaligned against dst by r bytes (a chunked
+// column's slice after a chunk whose byte length is not a multiple of 16, a sliced VarBin byte
+// buffer), each 16-byte chunk is assembled from the two aligned 16-byte source words holding it
+// with byte funnel shifts (v_alignbyte_b32; r is uniform over the launch, so the word select is a
+// uniform branch).  Both words hold a byte of the source range, so neither load leaves its pages.
+__device__ __forceinline__ uint32_t abyte(uint32_t hi, uint32_t lo, uint32_t sh) {
+    return __builtin_amdgcn_alignbyte(hi, lo, sh);
+}
+template <int QD>
+__device__ __forceinline__ uint4 funnel16(const uint4& lo, const uint4& hi, uint32_t rb) {
+    const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    return make_uint4(abyte(w[QD + 1], w[QD], rb), abyte(w[QD + 2], w[QD + 1], rb), abyte(w[QD + 3], w[QD + 2], rb),
+                      abyte(w[QD + 4], w[QD + 3], rb));
+}
+
 __global__ __launch_bounds__(kBlock) void copy_bytes_kernel(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
-                                                            uint64_t n, uint64_t head, uint64_t body) {
+                                                            uint64_t n, uint64_t head, uint64_t body, uint32_t r) {
     const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
     const uint64_t t0 = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-    for (uint64_t q = t0; q < body; q += stride) {  // 16-byte chunks after the head
-        const uint4 v = src ? gload(reinterpret_cast<const uint4*>(src + head) + q) : make_uint4(0, 0, 0, 0);
-        gstore(reinterpret_cast<uint4*>(dst + head) + q, v);
+    uint4* const d16 = reinterpret_cast<uint4*>(dst + head);
+    if (!src) {
+        for (uint64_t q = t0; q < body; q += stride) gstore(d16 + q, make_uint4(0, 0, 0, 0));
+    } else if (r == 0) {  // 16-byte chunks after the head
+        const uint4* const s16 = reinterpret_cast<const uint4*>(src + head);
+        for (uint64_t q = t0; q < body; q += stride) gstore(d16 + q, gload(s16 + q));
+    } else {
+        const uint4* const s16 = reinterpret_cast<const uint4*>(src + head - r);  // aligned
+        const uint32_t qd = r >> 2, rb = r & 3;
+        for (uint64_t q = t0; q < body; q += stride) {
+            const uint4 lo = gload(s16 + q), hi = gload(s16 + q + 1);
+            uint4 v;
+            if (qd == 0) v = funnel16<0>(lo, hi, rb);
+            else if (qd == 1) v = funnel16<1>(lo, hi, rb);
+            else if (qd == 2) v = funnel16<2>(lo, hi, rb);
+            else v = funnel16<3>(lo, hi, rb);
+            gstore(d16 + q, v);
+        }
     }
     const uint64_t tail0 = head + 16 * body, edge = head + (n - tail0);  // head bytes + tail bytes
     for (uint64_t k = t0; k < edge; k += stride) {
@@ -767,14 +796,12 @@ __global__ __launch_bounds__(kBlock) void copy_bytes_kernel(uint8_t* __restrict_
 vxg_status launch_copy_bytes(void* dst, const void* src, uint64_t n, hipStream_t s) {
     if (n == 0) return VXG_OK;
     const uintptr_t d = reinterpret_cast<uintptr_t>(dst), a = reinterpret_cast<uintptr_t>(src);
-    uint64_t head = n, body = 0;
-    if (!src || ((d ^ a) & 15) == 0) {
-        head = std::min<uint64_t>(n, (16 - (d & 15)) & 15);
-        body = (n - head) / 16;
-    }
+    const uint64_t head = std::min<uint64_t>(n, (16 - (d & 15)) & 15);
+    const uint64_t body = (n - head) / 16;
+    const uint32_t r = src ? uint32_t((a + head) & 15) : 0u;
     const uint64_t work = std::max<uint64_t>(body, 32);
     hipLaunchKernelGGL(copy_bytes_kernel, dim3(grid_for(work)), dim3(kBlock), 0, s, static_cast<uint8_t*>(dst),
-                       static_cast<const uint8_t*>(src), n, head, body);
+                       static_cast<const uint8_t*>(src), n, head, body, r);
     return hip_check(hipGetLastError(), "copy_bytes_kernel");
 }
 

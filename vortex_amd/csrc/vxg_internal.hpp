@@ -5,6 +5,7 @@
 
 #include <cstdint>
 #include <cstdlib>
+#include <mutex>
 #include <string>
 #include <type_traits>
 #include <vector>
@@ -105,10 +106,40 @@ extern const double kIF10d[24];
 enum : uint32_t { kErrTakeOOB = 1u, kErrPatchOOB = 2u, kErrRunEnd = 4u, kErrFsst = 8u, kErrRoaring = 16u, kErrVarBin = 32u,
                   kErrPatchOrder = 64u };
 
+// Per-context launch options (vxg_set_option, include/vortex_gpu.h): they shape launches, never
+// what a launch computes.  Defaults: the environment at vxg_open, else the values below.
+struct Options {
+    int64_t k1w_min_groups = 1024;  // VXG_OPT_K1W_MIN_GROUPS
+    int64_t k1w_bpw = 0;            // VXG_OPT_K1W_BPW (0 = the rule)
+    int64_t k1_wave = -1;           // VXG_OPT_K1_WAVE (-1 = VXG_K1_WAVE, read at every launch)
+};
+// What the context's launches looked like (vxg_get_launch_stats).
+struct LaunchStats {
+    uint64_t k1w_launches = 0, k1w_last_groups = 0;
+    uint32_t k1w_last_bpw = 0, k1w_min_bpw = 0, k1w_max_bpw = 0, k1w_last_bpw_max = 0;
+};
+
 struct Ctx {
     int device = 0;
     uint32_t* err_word = nullptr;  // device
+    Options opt;
+    std::mutex mu;                 // guards st (launches may come from several host threads)
+    LaunchStats st;
 };
+// The context of the entry point running on this host thread (set by every entry point that
+// takes one, before it launches or records anything).
+extern thread_local Ctx* g_cur_ctx;
+Options default_options();  // the environment's, as vxg_open applies them
+inline Options cur_options() { return g_cur_ctx ? g_cur_ctx->opt : default_options(); }
+// FastLanes unpack kernel choice: 0 register-resident only, 1 by launch size, 2 K1w always.
+inline int k1_wave_mode() {
+    const int64_t o = cur_options().k1_wave;
+    if (o >= 0) return int(o > 2 ? 2 : o);
+    const char* e = std::getenv("VXG_K1_WAVE");
+    if (!e) return 1;
+    return e[0] == '0' ? 0 : (e[0] == 'f' ? 2 : 1);
+}
+void note_k1w_launch(uint32_t bpw, uint32_t bpw_max, uint64_t groups);
 
 vxg_status set_error(vxg_status s, const std::string& msg);
 vxg_status hip_check(hipError_t e, const char* what);

@@ -100,13 +100,18 @@ def encode_for_bitpacked(values, allow_patches: bool = True) -> Array:
     return A.frame_of_reference(child, ref, shift, p)
 
 
-def encode_zigzag(values) -> Array:
-    """ZigZag -> BitPacked (zigzag/compress.rs:10-33, compressors/zigzag.rs)."""
+def zigzag_encode(values) -> np.ndarray:
+    """zigzag_encode_primitive (zigzag/compress.rs:24-33): the unsigned encoded words."""
     v = np.ascontiguousarray(values)
     p = PTYPE_OF_NP[v.dtype]
     out = np.zeros(v.size, dtype=NP_OF_PTYPE[A.unsigned_of(p)])
     _lib_enc().vxe_zigzag_encode(PTYPE[p], _p(v), v.size, _p(out))
-    return A.zigzag(encode_bitpacked(out))
+    return out
+
+
+def encode_zigzag(values) -> Array:
+    """ZigZag -> BitPacked (zigzag/compress.rs:10-33, compressors/zigzag.rs)."""
+    return A.zigzag(encode_bitpacked(zigzag_encode(values)))
 
 
 def alp_encode(values) -> tuple[int, int, np.ndarray, np.ndarray, np.ndarray]:
