@@ -245,27 +245,28 @@ def test_k1w_epilogues_and_chunks(k1w, mode):
 
 @pytest.mark.parametrize("batch", ["1", "0"])
 def test_k1w_mid_size_default_rule(ctx, batch):
-    """plan columns of 4-30 Mi values take an intermediate BPW under the DEFAULT rule
-    (K1W_MIN_GROUPS 1024) -- the production path of C5's columns.  u32 W=7, 12 x 1 Mi values with
-    a sliced chunk (12,288 blocks -> BPW 12 of 32), and ALP f64 (W=17) + patches, 8 x 1 Mi
-    (8,192 blocks -> BPW 8 of 12); batched (>= 20 MiB groups keep their K1w launch) and unbatched
-    plans, bit-exact against the oracle and the plain values."""
+    """plan columns of 4-30 Mi values over a device chunk table (> 32 chunks, as
+    C5's 92-chunk columns) take an intermediate BPW under the DEFAULT rule (K1W_MIN_GROUPS 1024)
+    -- the production path of C5's numeric columns.  u32 W=7, 48 x 256 Ki values with a sliced
+    chunk (12,288 blocks -> BPW 12 of 32), and ALP f64 (W=17) + patches, 34 x 256 Ki (8,704
+    blocks -> BPW 8 of 12); batched (>= 20 MiB groups keep their K1w launch) and unbatched plans,
+    bit-exact against the oracle and the plain values."""
     import torch
     assert ctx.get_option("k1w_min_groups") == 1024 and ctx.get_option("k1w_bpw") == 0
     rng = np.random.default_rng(300)
-    n = 1 << 20
+    n = 1 << 18
     u_plain, u_chunks = [], []
-    for c in range(12):
+    for c in range(48):
         v = rng.integers(0, 128, n, dtype=np.uint32)
         u_plain.append(v)
         u_chunks.append(E.encode_bitpacked(v, bit_width=7, allow_patches=False, offset=517 if c == 5 else 0))
     f_plain, f_chunks = [], []
-    for c in range(8):
+    for c in range(34):
         v = np.round(rng.uniform(1, 1000, n) * 100) / 100
-        v[rng.choice(n, 300, replace=False)] = rng.standard_normal(300) * 1e9 + 0.123456789
+        v[rng.choice(n, 100, replace=False)] = rng.standard_normal(100) * 1e9 + 0.123456789
         f_plain.append(v)
         f_chunks.append(E.encode_alp(v))
-    assert f_chunks[0].children[0].children[0].meta["bit_width"] == 17
+    assert all(f.children[0].children[0].meta["bit_width"] == 17 for f in f_chunks)
     cases = [(A.chunked(u_chunks), np.concatenate(u_plain), 12, 32),
              (A.chunked(f_chunks), np.concatenate(f_plain), 8, 12)]
     for arr, plain, bpw, bpw_max in cases:
