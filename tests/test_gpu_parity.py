@@ -125,7 +125,8 @@ def kw_rule_bpw(blocks, bpw_max, min_groups):
     return min(bpw_max, 4 if b < 4 else b // 4 * 4)
 
 
-BPW_MODES = ["max", 16, 8, 6, 4]
+# 5: the shape of the r05e failure (profiles/r05e_k1w_bpw_failure.md) -- waves of 2, 2, 1, 0 blocks
+BPW_MODES = ["max", 16, 8, 6, 5, 4]
 
 
 @pytest.fixture
