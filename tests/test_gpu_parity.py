@@ -5,6 +5,7 @@ MI355X with vxg_canonicalize (or a per-encoding entry point), and compares every
 with the oracle's CPU canonicalize of the same tree (tests/oracle_tree.py) — and with the
 original data (decode(encode(x)) == x).  Floating point is compared as raw bits.
 """
+import contextlib
 import ctypes as C
 import dataclasses
 
@@ -1215,15 +1216,33 @@ def test_plan_graph_replay_matches_direct(ctx):
     plan.close()
 
 
-@pytest.mark.parametrize("fuse", ["1", "0"])
-def test_plan_fused_fsst_k1g(ctx, fuse):
+@contextlib.contextmanager
+def env_set(**kv):
+    """Environment variables set for the block (the planner reads these at plan recording)."""
+    import os
+    old = {k: os.environ.get(k) for k in kv}
+    os.environ.update({k: str(v) for k, v in kv.items()})
+    try:
+        yield
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("fuse,prepass", [("1", "ingrid"), ("1", "separate"), ("0", "separate")])
+def test_plan_fused_fsst_k1g(ctx, fuse, prepass):
     """A batched plan decodes one FSST accessor group's tiles inside its K1g launch
     (fsst_k1g_kernel, the tiles spread between the K1g workgroups): lineitem columns (Dict(VarBin)
     strings, RunEnd, numeric cascades -- K1g jobs) beside chunked FSST columns with FastLanes-
     packed offsets/lengths (the fused group), plain i32 offsets/lengths (a second group: its own
     launch), nulls and ragged chunk sizes, and a FSST-only plan (a K1g launch with no K1g jobs).
-    VXG_PLAN_FUSE=0 records the unfused form; both equal the oracle on every replay."""
-    import os
+    `ingrid` (round 6, the default for groups of <= 8,192 tiles): the group's length pre-pass runs
+    as the fused launch's first workgroups, 32 tiles each (a 31,000-string chunk is 4 such scan
+    blocks), publishing tagged records the tiles wait for; `separate`: its own kernel before.
+    VXG_PLAN_FUSE=0 records the unfused form; all equal the oracle on every replay."""
     import torch
     sys_path_bench()
     from tools import lineitem as L
@@ -1237,16 +1256,9 @@ def test_plan_fused_fsst_k1g(ctx, fuse):
     plain = A.chunked([E.encode_fsst(strs[a:b], compress_children=False) for a, b in zip(cuts[:3], cuts[1:4])])
     arrs = [cols[name] for name, _ in L.COLUMNS] + [packed, plain]
     kinds = [kind for _, kind in L.COLUMNS] + ["utf8", "utf8"]
-    old = os.environ.get("VXG_PLAN_FUSE")
-    os.environ["VXG_PLAN_FUSE"] = fuse
-    try:
+    with env_set(VXG_PLAN_FUSE=fuse, VXG_FUSED_PREPASS_MAX_TILES=8192 if prepass == "ingrid" else 0):
         with plan_mode("1"):
             plans = [V.Plan([a.to(torch_dev()) for a in arrs], ctx), V.Plan([packed.to(torch_dev())], ctx)]
-    finally:
-        if old is None:
-            os.environ.pop("VXG_PLAN_FUSE", None)
-        else:
-            os.environ["VXG_PLAN_FUSE"] = old
     assert all(p.info()["batched"] for p in plans)
     want = [canon(a) if k == "utf8" else np.concatenate(plain_vals[n]) for a, k, n in
             zip(arrs, kinds, [name for name, _ in L.COLUMNS] + ["", ""])]
@@ -1263,6 +1275,30 @@ def test_plan_fused_fsst_k1g(ctx, fuse):
                     assert r.numpy().tobytes() == want[i].tobytes(), i
     for p in plans:
         p.close()
+
+
+def test_plan_fused_prepass_tag_wraps(ctx):
+    """The in-grid pre-pass's record tag (1-65535) is advanced by every vxg_plan_launch: 65,600
+    back-to-back replays of a small fused plan (a FSST column beside a K1g job) wrap it.  Every
+    replay's tiles find records carrying their own tag (a wait that never ends reports
+    kErrPlanSync, which the synchronising launch would raise) and the last replay equals the
+    oracle."""
+    rng = np.random.default_rng(65600)
+    s1 = _comment_strings(rng, 3_000, vocab=30)
+    codes = A.chunked([E.encode_bitpacked(rng.integers(0, 100, 5_000).astype(np.uint32), bit_width=7,
+                                          allow_patches=False) for _ in range(2)])
+    f1 = A.chunked([E.encode_fsst(s1[:1_000]), E.encode_fsst(s1[1_000:])])
+    with env_set(VXG_FUSED_PREPASS_MAX_TILES=8192), plan_mode("1"):
+        d1 = f1.to(torch_dev())
+        plan = V.Plan([d1, codes.to(torch_dev())], ctx)
+    assert plan.info()["batched"]
+    for _ in range(65_600):
+        plan.launch(sync=False)
+    ctx.sync()
+    (rv, rb), _ = canon(f1)
+    r = plan.launch(sync=True)[0]
+    assert r.numpy()[0].tobytes() == rv.tobytes() and [b.tobytes() for b in r.buffers()] == [b.tobytes() for b in rb]
+    plan.close()
 
 
 @pytest.mark.parametrize("rows,cr", [(3 * 8192 + 99, 8192), (100 * 1024 + 77, 1024)])

@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <memory>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -1912,6 +1913,9 @@ static vxg_status status_of_err_word(uint32_t err) {
     if (err & kErrFsst) return set_error(VXG_ERR_INVALID_ARGUMENT, "FSST codes do not decode to uncompressed_lengths");
     if (err & kErrRoaring) return set_error(VXG_ERR_INVALID_SERDE, "RoaringBool buffer is not a croaring Native bitmap");
     if (err & kErrVarBin) return set_error(VXG_ERR_INVALID_ARGUMENT, "VarBin offsets out of range of the bytes");
+    if (err & kErrPlanSync)
+        return set_error(VXG_ERR_ASSERTION_FAILED, "plan launch: in-grid pre-pass records never published "
+                                                   "(overlapping replays of one plan?)");
     return set_error(VXG_ERR_ASSERTION_FAILED, "unknown device error bit");
 }
 
@@ -2179,8 +2183,35 @@ static uint64_t canonical_out_bytes(const vxg_array& a) {
     return a.dtype == VXG_DTYPE_BOOL ? a.len / 8 : a.len * (str ? 16 : ptype_width(a.ptype));
 }
 
+// A batched plan's fused FSST+K1g launch with the in-grid pre-pass (fsst.hip): its arguments live
+// here so that every replay can give it a new record tag (FsstFusedArgs::tag).
+struct FusedNode {
+    FsstFusedArgs fa;
+    const GenChunk* gtab;
+    uint32_t gn, dict_off;
+    bool dict_lds;
+    uint32_t* err;
+    uint64_t gpe;
+    void* args[7];
+    hipGraphNode_t node = nullptr;
+    hipKernelNodeParams p{};
+    explicit FusedNode(void** a) {
+        fa = *static_cast<const FsstFusedArgs*>(a[0]);
+        gtab = *static_cast<const GenChunk* const*>(a[1]);
+        gn = *static_cast<const uint32_t*>(a[2]);
+        dict_off = *static_cast<const uint32_t*>(a[3]);
+        dict_lds = *static_cast<const bool*>(a[4]);
+        err = *static_cast<uint32_t* const*>(a[5]);
+        gpe = *static_cast<const uint64_t*>(a[6]);
+        void* const mine[7] = {&fa, &gtab, &gn, &dict_off, &dict_lds, &err, &gpe};
+        std::copy(mine, mine + 7, args);
+    }
+};
+
 struct vxg_plan {
     vxg_ctx* ctx = nullptr;
+    std::vector<std::unique_ptr<FusedNode>> fused;  // in-grid pre-pass launches (tag per replay)
+    uint64_t launches = 0;
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
     DevTables store;  // the recorded launches' temporaries and device chunk tables
@@ -2255,6 +2286,30 @@ static std::vector<hipKernelNodeParams> kernel_chain(hipGraph_t g) {
         out.push_back(p);
     }
     return out;
+}
+
+// The plan's fused launches with an in-grid pre-pass: arguments copied into the plan (the direct
+// chain's entry repointed at them; graph replays set them on the executable graph).
+static vxg_status bind_fused_nodes(vxg_plan* pl, hipGraph_t g) {
+    size_t nn = 0;
+    if (hipGraphGetNodes(g, nullptr, &nn) != hipSuccess) return set_error(VXG_ERR_ASSERTION_FAILED, "graph nodes");
+    std::vector<hipGraphNode_t> nodes(nn);
+    if (nn && hipGraphGetNodes(g, nodes.data(), &nn) != hipSuccess) return set_error(VXG_ERR_ASSERTION_FAILED, "graph nodes");
+    for (hipGraphNode_t nd : nodes) {
+        hipGraphNodeType t{};
+        if (hipGraphNodeGetType(nd, &t) != hipSuccess || t != hipGraphNodeTypeKernel) continue;
+        hipKernelNodeParams p{};
+        if (hipGraphKernelNodeGetParams(nd, &p) != hipSuccess || !p.kernelParams || !is_fsst_fused_kernel(p.func)) continue;
+        if (static_cast<const FsstFusedArgs*>(p.kernelParams[0])->prepass == 0) continue;
+        auto f = std::make_unique<FusedNode>(p.kernelParams);
+        f->node = nd;
+        f->p = p;
+        f->p.kernelParams = f->args;
+        for (hipKernelNodeParams& d : pl->direct)
+            if (d.func == p.func) d.kernelParams = f->args;  // (one fused launch per plan)
+        pl->fused.push_back(std::move(f));
+    }
+    return VXG_OK;
 }
 
 // Record one candidate plan: arrays with batched[i] defer their deferrable launches into one
@@ -2333,6 +2388,7 @@ static vxg_status record_plan(vxg_ctx* ctx, const vxg_array* arrays, vxg_canonic
             st = hip_check(hipGraphInstantiate(&pl->exec, g, nullptr, nullptr, 0), "hipGraphInstantiate");
         if (st == VXG_OK) st = pl->store.upload();  // device chunk tables, once for all replays
         if (st == VXG_OK && plan_direct_enabled()) pl->direct = kernel_chain(g);
+        if (st == VXG_OK) st = bind_fused_nodes(pl, g);
     }
     for (hipEvent_t e : ev)
         if (e) (void)hipEventDestroy(e);
@@ -2529,12 +2585,18 @@ vxg_status vxg_plan_get_info(const vxg_plan* plan, vxg_plan_info* info) {
 vxg_status vxg_plan_launch(vxg_plan* plan, void* stream) {
     if (!plan || !plan->exec) return set_error(VXG_ERR_INVALID_ARGUMENT, "null plan");
     VXG_TRY(use_device(plan->ctx));
+    // a new record tag per launch for the in-grid pre-pass (the previous launch's records carry
+    // the previous tag)
+    const uint32_t tag = uint32_t(++plan->launches % 65535u) + 1u;
+    for (auto& f : plan->fused) f->fa.tag = tag;
     if (!plan->direct.empty()) {
         for (const hipKernelNodeParams& p : plan->direct)
             VXG_TRY(hip_check(hipLaunchKernel(p.func, p.gridDim, p.blockDim, p.kernelParams, p.sharedMemBytes, S(stream)),
                               "plan kernel"));
         return VXG_OK;
     }
+    for (auto& f : plan->fused)
+        VXG_TRY(hip_check(hipGraphExecKernelNodeSetParams(plan->exec, f->node, &f->p), "plan fused launch tag"));
     return hip_check(hipGraphLaunch(plan->exec, S(stream)), "hipGraphLaunch");
 }
 

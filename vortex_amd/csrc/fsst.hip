@@ -372,6 +372,155 @@ __global__ __launch_bounds__(kScanThreads) void fsst_tile_scan_fl32(FsstTable ta
     if (tid == 0) block_totals[sb] = ws[0] + ws[1];
 }
 
+// ----- In-grid pre-pass records (the fused plan launch, round 6) -----
+// A batched plan's fused launch runs its FSST group's length pre-pass as its FIRST workgroups
+// (one per kFusedScanTiles tiles) instead of as a kernel of its own before it: on an 8-GPU C5
+// shard that kernel was ~24 workgroups of 1,024 threads alone on the chip, latency-bound, plus a
+// launch boundary.  The records are published with the launch's tag in their top 16 bits (value:
+// low 48 bits, two's complement) by single-copy-atomic 8-byte device-scope stores, so a tile
+// reads a record and its validity in ONE load: in the common case (the pre-pass workgroups,
+// dispatched first, finished long before) the tile's prologue keeps its two round trips; a record
+// with another tag (the previous launch's) is re-read until it carries this one.  Workgroups are
+// dispatched in grid order, so every pre-pass workgroup is resident or done before any tile that
+// waits for it: the wait always ends.  (A bound on it reports kErrPlanSync instead of hanging
+// should two replays of one plan ever overlap.)  The tag (1-65535, never 0, the zero-initialised
+// records' tag) is a kernel argument that vxg_plan_launch advances before every launch.  (A
+// device-side epoch advanced by the launch's last workgroup -- one same-address device-scope
+// atomic per workgroup -- serialised to ~75 ns per workgroup: the 8-GPU C5 shard's fused launch
+// took 448 us instead of ~38.)
+constexpr int kFusedScanTiles = 32;  // tiles per in-grid pre-pass workgroup = 8 FastLanes length blocks
+static_assert(kFusedScanTiles * kTS == 8 * 1024, "an in-grid scan block is 8 FastLanes blocks of lengths");
+
+__device__ __forceinline__ int64_t rec_load(const int64_t* p) {
+    return __hip_atomic_load((gptr<const int64_t>)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void rec_store(int64_t* p, int64_t v) {
+    __hip_atomic_store((gptr<int64_t>)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t rec_tag(int64_t r) { return uint32_t(uint64_t(r) >> 48); }
+__device__ __forceinline__ int64_t rec_val(int64_t r) { return int64_t(uint64_t(r) << 16) >> 16; }
+// (a value outside [-2^47, 2^47) -- only corrupt lengths or offsets give one -- is reported)
+__device__ __forceinline__ int64_t rec_make(int64_t v, uint32_t tag, uint32_t* err) {
+    if (v != rec_val(v)) __hip_atomic_fetch_or(err, kErrFsst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return int64_t((uint64_t(v) & ((1ull << 48) - 1)) | (uint64_t(tag) << 48));
+}
+// The record at p once it carries `tag` (r: the value already loaded from p).
+__device__ __forceinline__ int64_t rec_wait(const int64_t* p, int64_t r, uint32_t tag, uint32_t* err) {
+    for (uint32_t k = 0; rec_tag(r) != tag; k++) {
+        if (k == (1u << 18)) {  // ~0.3 s: never in a well-formed replay
+            __hip_atomic_fetch_or(err, kErrPlanSync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+        r = rec_load(p);
+    }
+    return rec_val(r);
+}
+__device__ __forceinline__ int64_t uni64(int64_t x) {
+    const uint64_t u = uint64_t(x);
+    return int64_t(uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(u))))) |
+                   (uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(int(uint32_t(u >> 32))))) << 32));
+}
+
+// One in-grid pre-pass workgroup: scan block sb (kFusedScanTiles tiles) of chunk c -- the tile
+// length sums, their exclusive scan, the block total and each tile's code end, tagged.  Patch-free
+// FoR(BitPacked u32) lengths at offset 0 (the file reader's cascade) are staged 4 FastLanes blocks
+// at a time (<= 16 KiB) and extracted one lane's 16 rows per thread (runtime width: rows R W of
+// the lane's words, funnel-shifted from LDS); any other length column is read element-wise.
+template <class LenAcc>
+__device__ __forceinline__ void fsst_prepass_ingrid(const FsstChunk& c, uint64_t sb, int64_t* __restrict__ tp_all,
+                                                    int64_t* __restrict__ bt_all, int64_t* __restrict__ tc_all,
+                                                    uint32_t tag, uint8_t* lds, uint32_t* err) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    int64_t* const s_ts = reinterpret_cast<int64_t*>(lds);  // kFusedScanTiles tile sums
+    uint32_t* const stage = reinterpret_cast<uint32_t*>(lds + 256);
+    const uint64_t n = c.n, n_tiles = (n + kTS - 1) / kTS, t0 = sb * kFusedScanTiles;
+    const uint64_t tt = t0 + uint64_t(tid);
+    int64_t code_end = 0;  // (issued first; used last)
+    if (tid < kFusedScanTiles && tt < n_tiles) code_end = intcol_get(c.offs, (tt + 1) * kTS < n ? (tt + 1) * kTS : n);
+    const IntCol& L = c.lens;
+    if (L.packed && L.width == 4 && L.offset == 0 && L.W <= 32) {  // uniform
+        const uint32_t W = L.W, shift = L.shift, ref = uint32_t(L.reference);
+        const uint32_t mask = W >= 32 ? 0xFFFFFFFFu : ((1u << W) - 1u);
+        const uint64_t nblk = (n + 1023) / 1024;
+        const int l32 = lane & 31, half = lane >> 5;
+        for (int pass = 0; pass < 2; pass++) {
+            const uint64_t blk0 = sb * 8 + uint64_t(pass) * 4;
+            const uint64_t have = blk0 < nblk ? (nblk - blk0 < 4 ? nblk - blk0 : 4) : 0;
+            const uint4* src = reinterpret_cast<const uint4*>(static_cast<const uint8_t*>(L.p) + blk0 * (128ull * W));
+            for (uint32_t q = tid; q < uint32_t(have) * 8u * W; q += kTile)
+                reinterpret_cast<uint4*>(stage)[q] = gload(src + q);
+            __syncthreads();
+            // wave w: block blk0 + w; lanes 0-31 rows 0-15 of lane l32, lanes 32-63 rows 16-31
+            int64_t acc[kTPB] = {0, 0, 0, 0};
+            const uint64_t blk = blk0 + uint64_t(wave);
+            if (blk < nblk) {
+                const uint32_t left = blk * 1024 + 1024 <= n ? 1024u : uint32_t(n - blk * 1024);
+                const uint32_t* words = stage + 32u * W * uint32_t(wave);
+#pragma unroll 4  // (fully unrolled: 152 B/lane of scratch in the fused kernel)
+                for (int r = 0; r < 16; r++) {
+                    const uint32_t R = uint32_t(16 * half + r);
+                    uint32_t v = 0;
+                    if (W) {
+                        const uint32_t start = R * W, w0 = start >> 5, w1 = w0 + 1 < W ? w0 + 1 : w0;
+                        v = __builtin_amdgcn_alignbit(words[32 * w1 + l32], words[32 * w0 + l32], start & 31) & mask;
+                    }
+                    const uint32_t u = uint32_t(v << shift) + ref;
+                    const int64_t x = L.sgn ? int64_t(int32_t(u)) : int64_t(u);
+                    acc[(R % 8) * 128 / kTS] += uint32_t(fl_index(int(R), l32)) < left ? x : 0;
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < kTPB; k++) {
+                const int64_t s = wave_total64(acc[k]);
+                if (lane == 0) s_ts[(pass * 4 + wave) * kTPB + k] = s;
+            }
+            __syncthreads();  // (the stage is refilled by the next pass; s_ts published)
+        }
+    } else {
+        // wave w sums tiles t0 + w + 4 r (r < 8), kTS / 64 consecutive lengths per lane, four tiles'
+        // loads in flight at a time (the fused kernel's 64-VGPR budget)
+        const LenAcc lens(L);
+        constexpr int PL = kTS / 64, RB = 4;
+#pragma unroll 1
+        for (int r0 = 0; r0 < kFusedScanTiles / 4; r0 += RB) {
+            int64_t v[RB];
+#pragma unroll
+            for (int r = 0; r < RB; r++) {
+                const uint64_t base = (t0 + 4 * (r0 + r) + wave) * kTS + PL * lane;
+                int64_t a = 0;
+#pragma unroll
+                for (int e = 0; e < PL; e++) {
+                    const uint64_t i = base + e;
+                    const int64_t x = lens(i < n ? i : n - 1);
+                    a += i < n ? x : 0;
+                }
+                v[r] = a;
+            }
+#pragma unroll
+            for (int r = 0; r < RB; r++) {
+                const int64_t s = wave_total64(v[r]);
+                if (lane == 0) s_ts[4 * (r0 + r) + wave] = s;
+            }
+        }
+        __syncthreads();
+    }
+    if (wave == 0) {  // exclusive scan of the block's tile sums, tagged records
+        const int64_t x0 = lane < kFusedScanTiles ? s_ts[lane] : 0;
+        int64_t x = x0;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int64_t y = __shfl_up(x, d, 64);
+            if (lane >= d) x += y;
+        }
+        if (lane < kFusedScanTiles && t0 + uint64_t(lane) < n_tiles) {
+            rec_store(tp_all + c.first_tile + t0 + lane, rec_make(x - x0, tag, err));
+            rec_store(tc_all + c.first_tile + t0 + lane, rec_make(code_end, tag, err));
+        }
+        if (lane == kFusedScanTiles - 1) rec_store(bt_all + c.first_scan + sb, rec_make(x, tag, err));
+    }
+}
+
 // Length of string first + k of a tile (k clamped by the caller), in two steps so the load can
 // be issued together with the prologue's other loads and used after all of them: issue() starts
 // the load(s), value() finishes.  A packed (FastLanes) length column's tile lies in at most two
@@ -593,9 +742,12 @@ struct TileIn {
     uint4 cx, cy;
 };
 
-template <class OffAcc, class LenAcc>
+// TAG (the fused launch's in-grid pre-pass): the records are tagged (rec_*), read with device-
+// scope loads and waited for after the tile's other prologue loads are issued.
+template <class OffAcc, class LenAcc, bool TAG = false>
 __device__ __forceinline__ void tile_issue(const FsstChunk& ch, uint64_t g, const int64_t* __restrict__ tile_prefix_all,
-                                           const int64_t* __restrict__ tile_code_all, TileIn<LenAcc>& in) {
+                                           const int64_t* __restrict__ tile_code_all, TileIn<LenAcc>& in,
+                                           uint32_t tag = 0, uint32_t* err = nullptr) {
     const int tid = threadIdx.x;
     const OffAcc code_offs(ch.offs);
     const LenAcc lens(ch.lens);
@@ -606,15 +758,26 @@ __device__ __forceinline__ void tile_issue(const FsstChunk& ch, uint64_t g, cons
     // records, so the code bytes are requested in the same round trip as the other loads.  The
     // records are indexed by the launch-global tile g (= first_tile + tile): their loads do not
     // wait for the chunk's fields
-    in.tp = tile_prefix_all[g];
-    in.cl = tile_code_all[g];
-    const int64_t prev = tile_code_all[g > 0 ? g - 1 : 0];
-    in.cf = tile > 0 ? prev : code_offs(0);
+    const int64_t* const pp = tile_code_all + (g > 0 ? g - 1 : 0);
+    int64_t prev;
+    if constexpr (TAG) {
+        // (waited for before the length and validity loads are issued: the record values are
+        // uniform from then on, and those loads are needed only after the code round trip)
+        const int64_t rtp = rec_load(tile_prefix_all + g), rcl = rec_load(tile_code_all + g), rpv = rec_load(pp);
+        in.tp = uni64(rec_wait(tile_prefix_all + g, rtp, tag, err));
+        in.cl = uni64(rec_wait(tile_code_all + g, rcl, tag, err));
+        prev = tile > 0 ? uni64(rec_wait(pp, rpv, tag, err)) : 0;
+    } else {
+        in.tp = tile_prefix_all[g];
+        in.cl = tile_code_all[g];
+        prev = *pp;
+    }
     const uint64_t first = uint64_t(tile) * kTile;
     const bool live = first + uint64_t(tid) < n;
     const uint32_t kc = live ? uint32_t(tid) : uint32_t(n - 1 - first);  // clamped index in the tile
     in.tl.issue(lens, first, kc);
     in.vbyte = ch.validity ? gload(ch.validity + ((first + kc) >> 3)) : uint8_t(0xFF);
+    in.cf = tile > 0 ? prev : code_offs(0);
     const int cshift = int((reinterpret_cast<uintptr_t>(ch.codes) + uintptr_t(in.cf)) & 15);
     const int64_t span64 = in.cl - in.cf;
     const int span = span64 >= 0 && span64 <= kCodeLds ? int(span64) : 0;
@@ -653,10 +816,11 @@ __device__ __forceinline__ void symbol_store(const FsstChunk& ch, const DecLds& 
 // Prefix of the scan blocks before the tile's (<= a few hundred totals), by wave 0 into
 // s_block_prefix: four loads per lane in flight per round (clamped index, no per-element
 // branch), so a tile deep in a large chunk pays one memory round trip here, not one per 64 blocks.
+template <int SCAN_TILES = kScanTiles, bool TAG = false>
 __device__ __forceinline__ void block_prefix(const FsstChunk& ch, uint32_t tile, const int64_t* __restrict__ block_totals_all,
-                                             const DecLds& L) {
+                                             const DecLds& L, uint32_t tag = 0, uint32_t* err = nullptr) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t nb = tile / kScanTiles;
+    const uint32_t nb = tile / SCAN_TILES;
     if (wave != 0) return;
     if (nb == 0) {
         if (lane == 0) *L.s_block_prefix = 0;
@@ -669,10 +833,14 @@ __device__ __forceinline__ void block_prefix(const FsstChunk& ch, uint32_t tile,
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             const uint32_t b = b0 + 64 * k + lane;
-            v[k] = block_totals[b < nb ? b : nb - 1];
+            v[k] = TAG ? rec_load(block_totals + (b < nb ? b : nb - 1)) : block_totals[b < nb ? b : nb - 1];
         }
 #pragma unroll
-        for (int k = 0; k < 4; k++) acc += b0 + 64 * k + lane < nb ? v[k] : 0;
+        for (int k = 0; k < 4; k++) {
+            const uint32_t b = b0 + 64 * k + lane;
+            if constexpr (TAG) v[k] = b < nb ? rec_wait(block_totals + b, v[k], tag, err) : 0;
+            acc += b < nb ? v[k] : 0;
+        }
     }
     acc = wave_total64(acc);
     if (lane == 0) *L.s_block_prefix = acc;
@@ -846,17 +1014,17 @@ __device__ __forceinline__ DecLds dec_lds(uint8_t* p) {
 // table and the scan-block prefix are loaded.  (Two consecutive tiles per workgroup with both
 // tiles' loads issued in the prologue was measured 10 % slower on C4 -- 6 instead of 8 waves per
 // SIMD; profiles/r04_fsst_decode.md.)
-template <class OffAcc, class LenAcc>
+template <class OffAcc, class LenAcc, bool TAG = false>
 __device__ __forceinline__ void fsst_decode_tile(const FsstChunk& ch, uint64_t g, const int64_t* __restrict__ tile_prefix_all,
                                                  const int64_t* __restrict__ block_totals_all,
                                                  const int64_t* __restrict__ tile_code_all, uint32_t* __restrict__ err,
-                                                 const DecLds& L) {
+                                                 const DecLds& L, uint32_t tag = 0) {
     TileIn<LenAcc> in;
-    tile_issue<OffAcc, LenAcc>(ch, g, tile_prefix_all, tile_code_all, in);
     uint64_t sym_v;
     uint32_t sl;
+    tile_issue<OffAcc, LenAcc, TAG>(ch, g, tile_prefix_all, tile_code_all, in, tag, err);
     symbol_load(ch, sym_v, sl);
-    block_prefix(ch, in.tile, block_totals_all, L);
+    block_prefix<TAG ? kFusedScanTiles : kScanTiles, TAG>(ch, in.tile, block_totals_all, L, tag, err);
     symbol_store(ch, L, sym_v, sl, err);
     tile_run<OffAcc, LenAcc>(ch, in, L, err);
 }
@@ -892,28 +1060,50 @@ __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) v
 // The plan launch of a batched plan (FsstFused): one recorded group's decode tiles and the
 // plan's K1g jobs (k1g_impl.hpp) in ONE grid, so that the decode's latency-bound tiles (two
 // dependent memory round trips and two barriers per 256 strings) run beside the K1g jobs' store
-// streams instead of alone.  The decode tiles are spread evenly over the first `mix` workgroups
-// of the grid (the rest are K1g jobs): workgroup b < mix is tile floor(b T / mix) when that
-// floor steps at b.  Every workgroup has the decode's LDS (8 per CU, the wave limit anyway).
+// streams instead of alone.  Grid: [fa.prepass in-grid pre-pass workgroups] then the K1g and
+// decode workgroups; after `delay` K1g workgroups the decode tiles are spread evenly over the next
+// `mix` workgroups (the rest are K1g jobs): workgroup b < mix of that range is tile floor(b T /
+// mix) when that floor steps at b.  Every workgroup has the decode's LDS (8 per CU, the wave
+// limit anyway).
 template <class OffAcc, class LenAcc>
 __global__ __launch_bounds__(kTile) __attribute__((amdgpu_waves_per_eu(8, 8))) void fsst_k1g_kernel(
     FsstFusedArgs fa, const GenChunk* __restrict__ gtab, uint32_t gn, uint32_t dict_off, bool dict_lds,
     uint32_t* __restrict__ err, uint64_t gpe) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    const uint64_t b = blockIdx.x, T = fa.tiles, M = fa.mix;
-    uint64_t gg;  // K1g workgroup
-    if (b < M) {
-        const uint64_t d0 = b * T / M, d1 = (b + 1) * T / M;
-        if (d1 > d0) {
-            fsst_decode_tile<OffAcc, LenAcc>(fa.ext[fa.wg_chunk[d0]], d0, fa.tp, fa.bt, fa.tc, err, dec_lds(lds));
-            return;
-        }
-        gg = b - d1;
+    const uint64_t P = fa.prepass, T = fa.tiles, M = fa.mix, D = fa.delay;
+    const uint32_t tag = fa.tag;
+    const uint64_t b = blockIdx.x;
+    if (b < P) {
+        fsst_prepass_ingrid<LenAcc>(fa.ext[fa.scan_chunk[b]], b - fa.ext[fa.scan_chunk[b]].first_scan,
+                                    const_cast<int64_t*>(fa.tp), const_cast<int64_t*>(fa.bt), const_cast<int64_t*>(fa.tc),
+                                    tag, lds, err);
     } else {
-        gg = b - T;
+        const uint64_t bb = b - P;
+        uint64_t gg = ~0ull;  // K1g workgroup, or a decode tile
+        if (bb < D) {
+            gg = bb;
+        } else if (bb - D < M) {
+            const uint64_t c = bb - D, d0 = c * T / M, d1 = (c + 1) * T / M;
+            if (d1 > d0) {
+                const FsstChunk& ch = fa.ext[fa.wg_chunk[d0]];
+                if (P) fsst_decode_tile<OffAcc, LenAcc, true>(ch, d0, fa.tp, fa.bt, fa.tc, err, dec_lds(lds), tag);
+                else fsst_decode_tile<OffAcc, LenAcc>(ch, d0, fa.tp, fa.bt, fa.tc, err, dec_lds(lds));
+            } else {
+                gg = D + c - d1;
+            }
+        } else {
+            gg = bb - T;
+        }
+        if (gg != ~0ull) {
+            const GenChunk& gc = gtab[ext_chunk_index_gpe(gtab, gn, gg, gpe, [](const GenChunk& d) { return d.d.first_group; })];
+            gen_dispatch(int(gc.kind), gc, gg, lds, dict_off, dict_lds, err);
+        }
     }
-    const GenChunk& gc = gtab[ext_chunk_index_gpe(gtab, gn, gg, gpe, [](const GenChunk& d) { return d.d.first_group; })];
-    gen_dispatch(int(gc.kind), gc, gg, lds, dict_off, dict_lds, err);
+}
+
+bool is_fsst_fused_kernel(const void* func) {
+    return func == reinterpret_cast<const void*>(&fsst_k1g_kernel<PackedCol<32>, PackedCol<32>>) ||
+           func == reinterpret_cast<const void*>(&fsst_k1g_kernel<PlainCol<4>, PlainCol<4>>);
 }
 
 uint64_t fsst_scratch_bytes(uint64_t n) {
@@ -1000,13 +1190,35 @@ static uint64_t fused_mix_pct() {
     return v;
 }
 
+// In-grid pre-pass of the fused launch for groups of at most VXG_FUSED_PREPASS_MAX_TILES decode
+// tiles (read at every plan recording; default 8,192; 0: always the separate pre-pass kernel), and
+// the K1g workgroups placed before the first decode tile (VXG_FUSED_DELAY, read once; default:
+// all of them with the in-grid pre-pass -- the tiles then find their records published --, none
+// without).  C5, same box, ms per step (session r06g): 8-GPU shard (2,930 tiles) 0.0434 separate
+// pre-pass -> 0.0392 in-grid with the tiles last (0.0422 spread from the start); 4-GPU (5,860)
+// 0.0745 -> 0.0735 (0.0803); 2-GPU (11,720) 0.1454 -> 0.1475; 1 GPU (23,443) 0.272 -> 0.280-0.288:
+// the tiles' device-scope record loads (past the XCD's L2, which may hold the previous replay's
+// record) lengthen every tile's first round trip, which a large group pays ~11 times per CU.
+static uint64_t fused_prepass_max_tiles() {
+    const char* e = std::getenv("VXG_FUSED_PREPASS_MAX_TILES");
+    return e ? uint64_t(std::strtoull(e, nullptr, 10)) : uint64_t(8192);
+}
+static int64_t fused_delay() {
+    static const int64_t v = [] {
+        const char* e = std::getenv("VXG_FUSED_DELAY");
+        return e ? int64_t(std::strtoull(e, nullptr, 10)) : int64_t(-1);
+    }();
+    return v;
+}
+
 vxg_status launch_fsst_k1g(const FsstFused& fuse, const GenChunk* ext, uint32_t n, uint64_t groups, uint32_t dict_off,
                            bool dict_lds, size_t shm, uint32_t* err, hipStream_t s, uint64_t gpe) {
     if (!fuse.valid || !fused_acc(fuse.oa, fuse.la)) return set_error(VXG_ERR_INVALID_ARGUMENT, "internal: fused FSST group");
     if (n == 0) groups = 0;
     FsstFusedArgs a = fuse.a;
-    a.mix = a.tiles + groups * fused_mix_pct() / 100;
-    const uint64_t grid = a.tiles + groups;
+    a.delay = fused_delay() >= 0 ? std::min(uint64_t(fused_delay()), groups) : (a.prepass ? groups : 0);
+    a.mix = a.tiles + (groups - a.delay) * fused_mix_pct() / 100;
+    const uint64_t grid = a.prepass + a.tiles + groups;
     if (grid == 0) return VXG_OK;
     if (grid > 0xFFFFFFFFull) return set_error(VXG_ERR_INVALID_ARGUMENT, "array too long for one launch");
     shm = std::max<size_t>(shm, kDecLdsBytes + fsst_pad_lds());
@@ -1045,6 +1257,10 @@ vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint
         // the first group the fused launch covers (a device table: the fused kernel reads no kernarg table)
         const bool fusing = fuse && dt && !fuse->valid && live &&
                             fused_acc(std::get<0>(fsst_key(chunks[i])), std::get<1>(fsst_key(chunks[i])));
+        uint64_t group_tiles = 0;
+        for (size_t k = i; k < j; k++) group_tiles += (chunks[k].n + kTS - 1) / kTS;
+        const bool ingrid = fusing && group_tiles <= fused_prepass_max_tiles();
+        const uint64_t scan_tiles = ingrid ? uint64_t(kFusedScanTiles) : uint64_t(kScanTiles);
         FsstChunk* cs = tab.c;
         if (live > size_t(kFsstArgChunks) || fusing) {
             FsstChunk* host;
@@ -1060,7 +1276,7 @@ vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint
             c.first_tile = tiles;
             c.first_scan = scans;
             tiles += nt;
-            scans += (nt + kScanTiles - 1) / kScanTiles;
+            scans += (nt + scan_tiles - 1) / scan_tiles;
         }
         if (tab.n) {
             const uint32_t* wg_chunk = nullptr;  // device table launches: chunk of every decode workgroup
@@ -1074,11 +1290,33 @@ vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint
                     for (uint64_t t = 0; t < nt; t++) host_map[c.first_tile + t] = k;
                 }
             }
+            const auto key = fsst_key(cs[0]);
+            if (ingrid) {  // records zeroed once (tag 0), written by the fused launch's first workgroups
+                int64_t* rec_host;
+                const int64_t* rec;
+                uint32_t* scan_host;
+                const uint32_t* scan_chunk;
+                vxg_status st = dt->table(2 * tiles + scans, &rec_host, &rec);
+                if (st == VXG_OK) st = dt->table(scans, &scan_host, &scan_chunk);
+                if (st != VXG_OK) return st;
+                for (uint32_t k = 0; k < tab.n; k++) {
+                    const FsstChunk& c = cs[k];
+                    const uint64_t ns = ((c.n + kTS - 1) / kTS + kFusedScanTiles - 1) / kFusedScanTiles;
+                    for (uint64_t b = 0; b < ns; b++) scan_host[c.first_scan + b] = k;
+                }
+                int64_t* r = const_cast<int64_t*>(rec);
+                fuse->valid = true;
+                fuse->oa = std::get<0>(key);
+                fuse->la = std::get<1>(key);
+                fuse->a = FsstFusedArgs{tab.ext, r, r + tiles, r + tiles + scans, wg_chunk, tiles, tiles,
+                                        scans, 0, scan_chunk, 1};
+                i = j;
+                continue;
+            }
             int64_t* tp = tiles_all;
             int64_t* bt = tiles_all + tiles;
             int64_t* tc = bt + scans;
             tiles_all += 2 * tiles + scans;
-            const auto key = fsst_key(cs[0]);
             if (std::get<2>(key) >= 0)
                 launch_tile_scan_fl32(std::get<2>(key), dim3(unsigned(scans)), s, tab, tp, bt, tc,
                                       std::make_integer_sequence<int, 33>{});
@@ -1094,7 +1332,7 @@ vxg_status launch_fsst_batch(std::vector<FsstChunk>& chunks, void* scratch, uint
                 fuse->valid = true;
                 fuse->oa = std::get<0>(key);
                 fuse->la = std::get<1>(key);
-                fuse->a = FsstFusedArgs{tab.ext, tp, bt, tc, wg_chunk, tiles, tiles};
+                fuse->a = FsstFusedArgs{tab.ext, tp, bt, tc, wg_chunk, tiles, tiles, 0, 0, nullptr, 0};
                 const vxg_status st = hip_check(hipGetLastError(), "fsst pre-pass");
                 if (st != VXG_OK) return st;
                 i = j;

@@ -104,7 +104,7 @@ extern const double kIF10d[24];
 
 // Device error word bits (set by kernels, read by vxg_check via vxg_stream_sync).
 enum : uint32_t { kErrTakeOOB = 1u, kErrPatchOOB = 2u, kErrRunEnd = 4u, kErrFsst = 8u, kErrRoaring = 16u, kErrVarBin = 32u,
-                  kErrPatchOrder = 64u };
+                  kErrPatchOrder = 64u, kErrPlanSync = 128u };
 
 // Per-context launch options (vxg_set_option, include/vortex_gpu.h): they shape launches, never
 // what a launch computes.  Defaults: the environment at vxg_open, else the values below.
@@ -469,7 +469,19 @@ struct FsstFusedArgs {
     const uint32_t* wg_chunk;   // chunk of every decode tile
     uint64_t tiles;             // decode tiles
     uint64_t mix;               // first workgroups of the grid the tiles are spread over (set at launch)
+    // In-grid pre-pass (round 6): the group's length pre-pass runs as the first `prepass`
+    // workgroups of the fused launch (one per kFusedScanTiles tiles, chunk scan_chunk[w]) and
+    // publishes tagged records (value | tag << 48) that the tiles wait for.  `tag` (1-65535,
+    // never the zeroed records' 0) is set by vxg_plan_launch before every launch: a new tag per
+    // launch.  prepass = 0: the separate pre-pass kernel.
+    uint64_t prepass;
+    uint64_t delay;             // K1g workgroups placed before the first decode tile
+    const uint32_t* scan_chunk;
+    uint32_t tag;
 };
+// The fused launch's kernel (fsst.hip): true if `func` is one of its instantiations, whose
+// arguments are (FsstFusedArgs, const GenChunk*, uint32_t, uint32_t, bool, uint32_t*, uint64_t).
+bool is_fsst_fused_kernel(const void* func);
 struct FsstFused {
     bool valid = false;
     int oa = 0, la = 0;         // offsets / lengths accessor kinds
