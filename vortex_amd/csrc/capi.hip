@@ -268,13 +268,17 @@ vxg_status launch_k1_jobs(std::vector<K1Job>& jobs, uint32_t* err, hipStream_t s
         uint64_t groups = 0;
         bool dict_lds = true;
         uint32_t packed_bytes = 0, dict_bytes = 0, runs_bytes = 0;
+        // a launch of string-dictionary jobs alone (an unbatched plan's chunked Dict(VarBin)
+        // column): one FastLanes block of codes per workgroup (gen_vb_bpw)
+        const bool vb_alone = n_runs == 0 && !(fuse && fuse->valid) &&
+                              std::all_of(gen.begin(), gen.end(), [](const K1Job* jp) { return jp->vb; });
         for (size_t k = 0; k < gen.size(); k++) {
             const K1Job& jb = *gen[k];
             GenChunk& g = host[k];
             g.d = jb.d;
             g.kind = uint32_t(gen_kind(jb.T, int(jb.epi), jb.vw, jb.vb));
             g.W = uint32_t(jb.W);
-            g.bpw = gen_bpw(jb.T, jb.W);
+            g.bpw = jb.vb ? gen_vb_bpw(jb.T, jb.W, vb_alone) : gen_bpw(jb.T, jb.W);
             g.d.first_group = groups;
             groups += (jb.d.n_blocks + g.bpw - 1) / g.bpw;
             packed_bytes = std::max(packed_bytes, g.bpw * 128u * uint32_t(jb.W));

@@ -72,6 +72,23 @@ uint32_t gen_bpw(int T, int W) {
     return b > m ? m : (b < 1 ? 1 : b);
 }
 
+// Dict-over-VarBin jobs: every workgroup builds the dictionary's views (one dependent round trip)
+// and then writes 16-byte views.  Alone in a launch (a one-generation grid: one C5 column is
+// ~1,500 workgroups of 4 blocks) 1,024-row workgroups write faster -- C5's four string columns
+// each as its own plan 0.56-0.59 -> 0.60-0.66 of 8 TB/s with 1 block (0.62-0.63 with 2; session
+// r06j; pure 96 MB view stores: 15.4 / 17.1 us for 1,024 / 4,096-row workgroups,
+// profiles/r04_ubench_views.txt) -- while beside FSST tiles in the fused launch 4 blocks stay
+// best (C5 1 GPU 0.272-0.280 ms with 4 and 2, 0.305 with 1; session r06k).
+uint32_t gen_vb_bpw(int T, int W, bool alone) {
+    static const long v = [] {
+        const char* e = std::getenv("VXG_K1G_VB_BPW");
+        return e ? std::strtol(e, nullptr, 10) : 0L;
+    }();
+    const uint32_t b = gen_bpw(T, W);
+    const uint32_t want = v >= 1 ? uint32_t(v) : (alone ? 1u : b);
+    return want < b ? want : b;
+}
+
 uint32_t gen_runs_lds_bytes(int value_width) {
     switch (value_width) {
     case 1: return uint32_t(runs_lds_bytes<uint8_t>());
@@ -93,7 +110,9 @@ vxg_status launch_k1_generic(const GenChunk* ext, uint32_t n, uint64_t groups, b
         return set_error(VXG_ERR_INVALID_ARGUMENT, "K1g stage sizes");
     // LDS = the largest packed stage + the largest dictionary stage, or a RunEnd expansion's
     // (sized by the launch's jobs, so small jobs keep residency high)
-    const uint32_t dict_off = (packed_bytes + 15) & ~15u;
+    // (+ one 128-byte word row of slack past the packed stage: gen_body_w reads, and masks, the
+    // row after a block's last)
+    const uint32_t dict_off = (packed_bytes + 128 + 15) & ~15u;
     const size_t shm = std::max<size_t>({size_t(dict_off) + dict_bytes, size_t(runs_bytes), 16});
     if (fuse && fuse->valid) return launch_fsst_k1g(*fuse, ext, n, groups, dict_off, dict_lds, shm, err, s, gpe);
     hipLaunchKernelGGL(k1_generic_kernel, dim3(unsigned(groups)), dim3(kGenThreads), shm, s, ext, n, dict_off, dict_lds,

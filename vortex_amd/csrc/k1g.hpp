@@ -53,6 +53,9 @@ __host__ __device__ constexpr uint32_t gen_vb_stage_bytes(uint64_t dict_len, uin
 }
 // Blocks per workgroup of a job (its packed words staged in <= 16 KiB of LDS).
 uint32_t gen_bpw(int T, int W);
+// ... of a Dict-over-VarBin job: 1 in a launch of such jobs alone, else gen_bpw's
+// (VXG_K1G_VB_BPW overrides both).
+uint32_t gen_vb_bpw(int T, int W, bool alone);
 // LDS a short-run RunEnd expansion of `value_width`-byte values needs.
 uint32_t gen_runs_lds_bytes(int value_width);
 // One launch over a device table of n jobs (first_group filled in).  `dict_lds` = every Dict

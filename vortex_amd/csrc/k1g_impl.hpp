@@ -12,6 +12,12 @@ namespace vxg {
 namespace {
 
 constexpr int kGenThreads = 256;
+// 32/64-bit numeric jobs decoded with the K1w store shape (gen_body_w); a -DVXG_K1G_WIDE=0 build
+// keeps the thread-per-value body for A/B.
+#ifndef VXG_K1G_WIDE
+#define VXG_K1G_WIDE 1
+#endif
+constexpr bool kGenWideStores = VXG_K1G_WIDE;
 constexpr uint32_t kGenPackedLds = 16 * 1024;  // staged packed words per workgroup
 
 // FL_ORDER[i] (0, 4, 2, 6, 1, 5, 3, 7) is the 3-bit reversal of i
@@ -163,6 +169,86 @@ __device__ __forceinline__ void gen_body(const GenChunk& gc, uint64_t g, uint8_t
         if (oob) __hip_atomic_fetch_or(err, kErrTakeOOB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// The K1w store shape with a runtime width (round 6) for the 32/64-bit numeric kinds: the
+// staged blocks are decoded one per wave (wave v takes blocks v, v + 4, ...); in store k lane
+// group gq (8 lanes) produces the row whose 128 output bytes are slot 8k + gq of the block and
+// lane t its 16-byte slice, funnel-shifted out of the two LDS word rows holding it -- every store
+// instruction writes 1 KiB contiguous (K1w, fl_unpack_impl.hpp kw_block / kw_extract; there W is
+// a template parameter).  The thread-per-value body (gen_body) stores 256 or 512 bytes per
+// instruction and reads LDS per value.  Word row w0 + 1 of a block's last row may be the next
+// block's or the stage's slack row (launch_k1_generic sizes the LDS with 128 bytes of slack): its
+// bits are masked off.
+template <int T>
+__device__ __forceinline__ Vec16<T> kw_extract_rt(const uint8_t* blk, int r, int t, uint32_t W) {
+    using U = typename Fl<T>::U;
+    constexpr int NV = Vec16<T>::NV;
+    const int start = r * int(W), w0 = start / T, sh = start % T;
+    const Vec16<T> lo = load16<T>(blk + w0 * 128 + 16 * t);
+    const Vec16<T> hi = load16<T>(blk + (w0 + 1) * 128 + 16 * t);
+    const int cur = T - sh;  // bits of the value held by word w0
+    const int nlo = cur < int(W) ? cur : int(W), nhi = int(W) - nlo;
+    const U mlo = Fl<T>::rep(kw_mask<U>(nlo)), mhi = Fl<T>::rep(kw_mask<U>(nhi));
+    const int hs = cur & (int(8 * sizeof(U)) - 1);  // == cur whenever mhi != 0
+    Vec16<T> v;
+#pragma unroll
+    for (int k = 0; k < NV; k++) v.w[k] = ((lo.w[k] >> sh) & mlo) | ((hi.w[k] & mhi) << hs);
+    return v;
+}
+
+template <int T, Epi EPI>
+__device__ __forceinline__ void gen_body_w(const GenChunk& gc, uint64_t g, uint8_t* lds, uint32_t* err) {
+    using E = typename Fl<T>::E;
+    using O = typename EpiOut<T, EPI, 0>::type;
+    constexpr int EPV = 16 / int(sizeof(E));
+    const ChunkDev& c = gc.d;
+    const uint32_t W = gc.W, tid = threadIdx.x;
+    const uint64_t blk0 = (g - c.first_group) * gc.bpw;
+    const uint32_t nb = uint32_t(c.n_blocks - blk0 < uint64_t(gc.bpw) ? c.n_blocks - blk0 : uint64_t(gc.bpw));
+    const uint32_t q16 = nb * 8 * W;
+    for (uint32_t q = tid; q < q16; q += kGenThreads)
+        reinterpret_cast<uint4*>(lds)[q] = gload(reinterpret_cast<const uint4*>(c.packed + blk0 * (128ull * W)) + q);
+    EpiParams ep;
+    ep.reference = c.reference;
+    ep.shift = c.shift;
+    ep.alp_a = c.alp_a;
+    ep.alp_b = c.alp_b;
+    ep.err = err;
+    __syncthreads();
+    O* __restrict__ out = static_cast<O*>(c.out);
+    const bool aligned = (reinterpret_cast<uintptr_t>(c.out) & 15) == 0;
+    const int lane = int(tid & 63), gq = lane >> 3, t = lane & 7;
+    bool oob = false;
+    for (uint32_t b = tid >> 6; b < nb; b += kGenThreads / 64) {  // wave-uniform
+        const uint8_t* pk = lds + b * (128 * W);
+        const uint64_t blk = blk0 + b;
+        const int64_t out_base = int64_t(blk * 1024) - int64_t(c.offset);
+        const bool full = c.offset == 0 && (blk + 1) * 1024 <= c.len && aligned;
+#pragma unroll 2  // (fully unrolled, the hoisted LDS reads took 101 VGPRs: 4 waves per SIMD)
+        for (int k = 0; k < T / 8; k++) {
+            const int q = 8 * k + gq;
+            const Vec16<T> v = W ? kw_extract_rt<T>(pk, kw_row<T>(q), t, W) : Vec16<T>{};
+            const int idx = q * (1024 / T) + t * EPV;  // element index of the slice in the block
+            if (full) {
+                O* dst = out + (out_base + idx);
+                if constexpr (EPI == Epi::Plain) {
+                    store_bytes<16, kOutNT>(reinterpret_cast<uint8_t*>(dst), v.w);
+                } else {
+                    O o[EPV];
+#pragma unroll
+                    for (int j = 0; j < EPV; j++) o[j] = apply_epi<T, EPI, 0>(v.elem(j), ep, oob);
+                    store_bytes<EPV * int(sizeof(O)), kOutNT>(reinterpret_cast<uint8_t*>(dst), o);
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < EPV; j++) {
+                    const int64_t o = out_base + idx + j;
+                    if (o >= 0 && uint64_t(o) < c.len) gstore(out + o, apply_epi<T, EPI, 0>(v.elem(j), ep, oob));
+                }
+            }
+        }
+    }
+}
+
 // kinds: T index ti (8, 16, 32, 64 -> 0..3); Plain/For/ForZigZag 3 ti + e (0..11); AlpF32 12;
 // AlpF64 13; Dict 14 + 5 ti + value-width index (1, 2, 4, 8, 16 -> 0..4) (14..33); Dict over a
 // VarBin dictionary 34 + ti (34..37); RunEnd short runs 38 + value-width index (38..42)
@@ -175,11 +261,14 @@ __device__ __forceinline__ void gen_dispatch_one(const GenChunk& gc, uint64_t g,
     constexpr int VWs[5] = {1, 2, 4, 8, 16};
     if constexpr (K < 12) {
         constexpr Epi e = K % 3 == 0 ? Epi::Plain : (K % 3 == 1 ? Epi::For : Epi::ForZigZag);
-        gen_body<Ts[K / 3], e, 0>(gc, g, lds, doff, dl, err);
+        if constexpr (K >= 6 && kGenWideStores) gen_body_w<Ts[K / 3], e>(gc, g, lds, err);  // T = 32, 64
+        else gen_body<Ts[K / 3], e, 0>(gc, g, lds, doff, dl, err);
     } else if constexpr (K == 12) {
-        gen_body<32, Epi::AlpF32, 0>(gc, g, lds, doff, dl, err);
+        if constexpr (kGenWideStores) gen_body_w<32, Epi::AlpF32>(gc, g, lds, err);
+        else gen_body<32, Epi::AlpF32, 0>(gc, g, lds, doff, dl, err);
     } else if constexpr (K == 13) {
-        gen_body<64, Epi::AlpF64, 0>(gc, g, lds, doff, dl, err);
+        if constexpr (kGenWideStores) gen_body_w<64, Epi::AlpF64>(gc, g, lds, err);
+        else gen_body<64, Epi::AlpF64, 0>(gc, g, lds, doff, dl, err);
     } else if constexpr (K < 34) {
         gen_body<Ts[(K - 14) / 5], Epi::Dict, VWs[(K - 14) % 5]>(gc, g, lds, doff, dl, err);
     } else if constexpr (K < 38) {
