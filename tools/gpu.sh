@@ -4,7 +4,8 @@
 # session are chained so that the first failure ends it.  Output goes to gpurun_out/.
 #
 #   tools/gpu.sh round TAG            the round's evidence: -m gpu suite, smoke, default bench,
-#                                     simulated 8/4/2-GPU shards (C3, C5), plan probe, then `prof`
+#                                     simulated 8/4/2-GPU shards (C3, C5), plan probe, per-column
+#                                     C5 (tools/c5_columns.py), then `prof`
 #   tools/gpu.sh tests TAG [EXPR]     -m gpu tests (optionally -k EXPR)
 #   tools/gpu.sh bench TAG WL [RUNS]  bench over workloads WL (e.g. c4,c5), RUNS times (default 2);
 #                                     prints each config's kernel time and roofline fraction
@@ -78,6 +79,7 @@ round)
   sim c3,c5 && \
   timeout -k 10 200 python -u tools/plan_probe.py 1 > "$O/plan_probe_$TAG.txt" 2>&1 && \
   timeout -k 10 200 python -u tools/plan_probe.py 8 >> "$O/plan_probe_$TAG.txt" 2>&1 && \
+  timeout -k 10 300 python -u tools/c5_columns.py --rotate 4 > "$O/c5_columns_$TAG.jsonl" 2> "$O/c5_columns_$TAG.err" && \
   prof
   ;;
 tests) tests "$3" ;;
