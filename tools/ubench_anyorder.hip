@@ -66,15 +66,21 @@ int main(int argc, char** argv) {
             CK(hipEventRecord(f1, s1));
             CK(hipStreamWaitEvent(s0, f1, 0));
             break;
+        case 4:  // any order, then a plain empty launch (does the event already wait for them?)
+            for (int k = 0; k < K; k++)
+                hipExtLaunchKernelGGL(job, dim3(unsigned(groups)), dim3(256), 0, s0, nullptr, nullptr, k ? hipExtAnyOrderLaunch : 0u,
+                                      (const uint4*)in[c * K + k], out[c * K + k], groups);
+            hipLaunchKernelGGL(job, dim3(1), dim3(256), 0, s0, in[c * K], out[c * K], uint64_t(0));
+            break;
         case 3:  // one launch
             hipLaunchKernelGGL(job, dim3(unsigned(K * groups)), dim3(256), 0, s0, big_in, big_out, K * groups);
             break;
         }
     };
-    const char* names[] = {"plain", "anyorder", "two_streams", "one_launch"};
-    std::vector<std::vector<float>> t(4);
+    const char* names[] = {"plain", "anyorder", "two_streams", "one_launch", "anyorder+tail"};
+    std::vector<std::vector<float>> t(5);
     for (int r = 0; r < 5; r++)
-        for (int m = 0; m < 4; m++) {
+        for (int m = 0; m < 5; m++) {
             for (int k = 0; k < 3; k++) seq(m);
             for (int k = 0; k < 20; k++) {
                 CK(hipEventRecord(a, s0));
@@ -88,7 +94,7 @@ int main(int argc, char** argv) {
         }
     CK(hipDeviceSynchronize());
     const double bytes = double(K) * groups * (2048 + 12288);
-    for (int m = 0; m < 4; m++) {
+    for (int m = 0; m < 5; m++) {
         auto v = t[m];
         std::sort(v.begin(), v.end());
         printf("%-12s groups %llu  median %8.2f us  min %8.2f us  %7.1f GB/s\n", names[m], (unsigned long long)groups,
