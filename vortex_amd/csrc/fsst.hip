@@ -1196,9 +1196,9 @@ static uint64_t fused_mix_pct() {
 // all of them with the in-grid pre-pass -- the tiles then find their records published --, none
 // without).  C5, same box, ms per step (session r06g): 8-GPU shard (2,930 tiles) 0.0434 separate
 // pre-pass -> 0.0392 in-grid with the tiles last (0.0422 spread from the start); 4-GPU (5,860)
-// 0.0745 -> 0.0735 (0.0803); 2-GPU (11,720) 0.1454 -> 0.1475; 1 GPU (23,443) 0.272 -> 0.280-0.288:
-// the tiles' device-scope record loads (past the XCD's L2, which may hold the previous replay's
-// record) lengthen every tile's first round trip, which a large group pays ~11 times per CU.
+// 0.0745 -> 0.0735 (0.0803); 2-GPU (11,720) 0.1454 -> 0.1475; 1 GPU (23,443) 0.272 -> 0.280-0.288
+// (not because of the device-scope record loads: plain first reads of parity-alternated record
+// buffers measured the same, profiles/r06_fsst_decode.md).
 static uint64_t fused_prepass_max_tiles() {
     const char* e = std::getenv("VXG_FUSED_PREPASS_MAX_TILES");
     return e ? uint64_t(std::strtoull(e, nullptr, 10)) : uint64_t(8192);
