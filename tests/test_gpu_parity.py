@@ -1277,6 +1277,28 @@ def test_plan_fused_fsst_k1g(ctx, fuse, prepass):
         p.close()
 
 
+def test_plan_fused_prepass_graph_replay(ctx):
+    """A plan that replays as a HIP graph (VXG_PLAN_DIRECT=0) gives its fused launch's in-grid
+    pre-pass a new record tag per replay through hipGraphExecKernelNodeSetParams: replays of
+    lineitem-like columns beside a chunked FSST column equal the oracle, with no device error."""
+    rng = np.random.default_rng(4711)
+    strs = _comment_strings(rng, 20_000, vocab=50)
+    strs = [None if i % 17 == 3 else x for i, x in enumerate(strs)]
+    fs = A.chunked([E.encode_fsst(strs[a:b]) for a, b in ((0, 7_000), (7_000, 7_001), (7_001, 20_000))])
+    codes = A.chunked([E.encode_bitpacked(rng.integers(0, 1000, 9_000).astype(np.uint32), bit_width=10,
+                                          allow_patches=False) for _ in range(3)])
+    with env_set(VXG_PLAN_DIRECT=0, VXG_FUSED_PREPASS_MAX_TILES=8192), plan_mode("1"):
+        plan = V.Plan([fs.to(torch_dev()), codes.to(torch_dev())], ctx)
+    info = plan.info()
+    assert info["batched"] and info["direct_nodes"] == 0, info
+    (rv, rb), rvalid = canon(fs)
+    for _ in range(4):
+        r = plan.launch(sync=True)[0]
+        assert r.numpy()[0].tobytes() == rv.tobytes() and [b.tobytes() for b in r.buffers()] == [b.tobytes() for b in rb]
+        assert np.array_equal(r.validity_mask(), rvalid)
+    plan.close()
+
+
 def test_plan_fused_prepass_tag_wraps(ctx):
     """The in-grid pre-pass's record tag (1-65535) is advanced by every vxg_plan_launch: 65,600
     back-to-back replays of a small fused plan (a FSST column beside a K1g job) wrap it.  Every

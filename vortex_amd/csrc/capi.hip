@@ -2230,20 +2230,14 @@ struct vxg_plan {
 
 // Direct replay of short kernel chains (VXG_PLAN_DIRECT=0 disables; at most
 // VXG_PLAN_DIRECT_MAX nodes, default 16: C5's 1-GPU batched chain is 9 kernels, 0.2745 ms per
-// step as a graph vs 0.2719 direct).
+// step as a graph vs 0.2719 direct).  Read at every plan recording.
 static size_t plan_direct_max() {
-    static const size_t v = [] {
-        const char* e = std::getenv("VXG_PLAN_DIRECT_MAX");
-        return e ? size_t(std::strtoull(e, nullptr, 10)) : size_t(16);
-    }();
-    return v;
+    const char* e = std::getenv("VXG_PLAN_DIRECT_MAX");
+    return e ? size_t(std::strtoull(e, nullptr, 10)) : size_t(16);
 }
 static bool plan_direct_enabled() {
-    static const bool on = [] {
-        const char* e = std::getenv("VXG_PLAN_DIRECT");
-        return !(e && e[0] == '0');
-    }();
-    return on;
+    const char* e = std::getenv("VXG_PLAN_DIRECT");
+    return !(e && e[0] == '0');
 }
 
 // The kernel nodes of `g` in order if g is a chain of <= plan_direct_max() kernel nodes, else empty.
