@@ -217,23 +217,14 @@ vxg_status launch_k1_jobs(std::vector<K1Job>& jobs, uint32_t* err, hipStream_t s
         return std::make_tuple(a.T, a.W, int(a.epi), a.vw, a.vb) < std::make_tuple(b.T, b.W, int(b.epi), b.vw, b.vb);
     });
     std::vector<const K1Job*> gen;  // jobs for the shared K1g launch
-    size_t i = 0;
-    while (i < jobs.size()) {
-        size_t j = i, live = 0;
-        uint64_t out_bytes = 0;
-        while (j < jobs.size() && (dt || j - i < size_t(kArgChunks)) && same_kernel(jobs[i], jobs[j])) {
-            live += jobs[j].d.n_blocks != 0;
-            out_bytes += jobs[j].d.len * uint64_t(k1_out_width(jobs[j]));
-            j++;
-        }
-        if (jobs[i].vb || (dt && generic_small && out_bytes < k1g_max_bytes() &&
-                           gen_kind(jobs[i].T, int(jobs[i].epi), jobs[i].vw) >= 0)) {
-            if (!dt) return set_error(VXG_ERR_INVALID_ARGUMENT, "VarBin-dictionary K1 jobs need a plan");
-            for (size_t k = i; k < j; k++)
-                if (jobs[k].d.n_blocks) gen.push_back(&jobs[k]);
-            i = j;
-            continue;
-        }
+    // (VXG_PLAN_K1G_FIRST=1, read at every recording: a plan batch records its K1g launch before
+    // the large groups' own launches -- A/B of the chain order)
+    const char* kf = std::getenv("VXG_PLAN_K1G_FIRST");
+    const bool k1g_first = generic_small && dt && kf && kf[0] == '1';
+    std::vector<std::pair<size_t, size_t>> deferred;  // large groups launched after K1g
+    auto launch_group = [&](size_t i, size_t j) -> vxg_status {
+        size_t live = 0;
+        for (size_t k = i; k < j; k++) live += jobs[k].d.n_blocks != 0;
         ChunkTable tab{};
         tab.err = err;
         if (patch && jobs.size() == 1) tab.patch = *patch;  // a single array's K1w (k1_takes_wave)
@@ -252,10 +243,29 @@ vxg_status launch_k1_jobs(std::vector<K1Job>& jobs, uint32_t* err, hipStream_t s
             groups += (c.n_blocks + 31) / 32;
         }
         if (groups > 0xFFFFFFFFull) return set_error(VXG_ERR_INVALID_ARGUMENT, "array too long for one launch");
-        if (tab.n) {
-            vxg_status st = launch_fl_unpack(jobs[i].T, jobs[i].W, jobs[i].epi, jobs[i].vw, tab, groups, s);
-            if (st != VXG_OK) return st;
+        if (tab.n) return launch_fl_unpack(jobs[i].T, jobs[i].W, jobs[i].epi, jobs[i].vw, tab, groups, s);
+        return VXG_OK;
+    };
+    size_t i = 0;
+    while (i < jobs.size()) {
+        size_t j = i, live = 0;
+        uint64_t out_bytes = 0;
+        while (j < jobs.size() && (dt || j - i < size_t(kArgChunks)) && same_kernel(jobs[i], jobs[j])) {
+            live += jobs[j].d.n_blocks != 0;
+            out_bytes += jobs[j].d.len * uint64_t(k1_out_width(jobs[j]));
+            j++;
         }
+        if (jobs[i].vb || (dt && generic_small && out_bytes < k1g_max_bytes() &&
+                           gen_kind(jobs[i].T, int(jobs[i].epi), jobs[i].vw) >= 0)) {
+            if (!dt) return set_error(VXG_ERR_INVALID_ARGUMENT, "VarBin-dictionary K1 jobs need a plan");
+            for (size_t k = i; k < j; k++)
+                if (jobs[k].d.n_blocks) gen.push_back(&jobs[k]);
+            i = j;
+            continue;
+        }
+        (void)live;
+        if (k1g_first) deferred.emplace_back(i, j);
+        else VXG_TRY_S(launch_group(i, j));
         i = j;
     }
     const size_t n_runs = gen_runs ? gen_runs->size() : 0;
@@ -315,6 +325,7 @@ vxg_status launch_k1_jobs(std::vector<K1Job>& jobs, uint32_t* err, hipStream_t s
         VXG_TRY_S(launch_k1_generic(ext, uint32_t(gen.size() + n_runs), groups, dict_lds, packed_bytes, dict_bytes,
                                     runs_bytes, err, s, common_groups(cnt.data(), cnt.size()), fuse));
     }
+    for (const auto& [a, b] : deferred) VXG_TRY_S(launch_group(a, b));
     return VXG_OK;
 }
 
