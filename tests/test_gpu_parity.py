@@ -1277,6 +1277,32 @@ def test_plan_fused_fsst_k1g(ctx, fuse, prepass):
         p.close()
 
 
+def test_plan_fused_prepass_length_widths(ctx):
+    """The in-grid pre-pass's FastLanes length body at the edges of its shapes: a chunk of
+    constant-length strings (FoR lengths of bit width 0: no words staged), a chunk whose lengths
+    need ~18 bits (a 200 KB string every 97 rows: those tiles take the direct per-string path),
+    and chunks of exactly one 32-tile scan block (8,192 strings) and one string more (a second
+    block of one tile), with nulls; three replays equal the oracle."""
+    rng = np.random.default_rng(1818)
+    const = [b"abcdefgh!" for _ in range(3_000)]
+    longs = _comment_strings(rng, 2_000, vocab=40)
+    longs = [bytes(rng.integers(97, 123, 200_000).astype(np.uint8)) if i % 97 == 13 else x for i, x in enumerate(longs)]
+    b1 = _comment_strings(rng, 8_192, vocab=60)
+    b2 = [None if i % 31 == 7 else x for i, x in enumerate(_comment_strings(rng, 8_193, vocab=60))]
+    chunks = [E.encode_fsst(c) for c in (const, longs, b1, b2)]
+    lw = [c.children[-1].children[0].meta["bit_width"] if c.children[-1].children else None for c in chunks]
+    fs = A.chunked(chunks)
+    with env_set(VXG_FUSED_PREPASS_MAX_TILES=8192), plan_mode("1"):
+        plan = V.Plan([fs.to(torch_dev())], ctx)
+    (rv, rb), rvalid = canon(fs)
+    for _ in range(3):
+        r = plan.launch(sync=True)[0]
+        assert r.numpy()[0].tobytes() == rv.tobytes(), lw
+        assert [b.tobytes() for b in r.buffers()] == [b.tobytes() for b in rb], lw
+        assert np.array_equal(r.validity_mask(), rvalid)
+    plan.close()
+
+
 def test_plan_fused_prepass_graph_replay(ctx):
     """A plan that replays as a HIP graph (VXG_PLAN_DIRECT=0) gives its fused launch's in-grid
     pre-pass a new record tag per replay through hipGraphExecKernelNodeSetParams: replays of
