@@ -322,8 +322,23 @@ vxg_status launch_k1_jobs(std::vector<K1Job>& jobs, uint32_t* err, hipStream_t s
         std::vector<uint64_t> cnt(gen.size() + n_runs);  // workgroups per job (direct job lookup when equal)
         for (size_t k = 0; k < cnt.size(); k++)
             cnt[k] = (k + 1 < cnt.size() ? host[k + 1].d.first_group : groups) - host[k].d.first_group;
+        uint64_t gpe = common_groups(cnt.data(), cnt.size());
+        // Nearly equal counts (C5's RunEnd chunks: 16 or 17 workgroups; every column's last chunk
+        // smaller): every job padded to the largest count when that adds <= 1/10 idle workgroups,
+        // so a workgroup finds its job by one division instead of a wave-wide search over the
+        // table (one or more dependent round trips before its loads; gen_dispatch returns at once
+        // on a padding workgroup).  VXG_K1G_PAD=0 (read at every recording) keeps the search.
+        const char* pe = std::getenv("VXG_K1G_PAD");
+        if (!gpe && cnt.size() > 1 && !(pe && pe[0] == '0')) {
+            const uint64_t m = *std::max_element(cnt.begin(), cnt.end());
+            if (m * cnt.size() - groups <= groups / 10) {
+                for (size_t k = 0; k < cnt.size(); k++) host[k].d.first_group = k * m;
+                groups = m * cnt.size();
+                gpe = m;
+            }
+        }
         VXG_TRY_S(launch_k1_generic(ext, uint32_t(gen.size() + n_runs), groups, dict_lds, packed_bytes, dict_bytes,
-                                    runs_bytes, err, s, common_groups(cnt.data(), cnt.size()), fuse));
+                                    runs_bytes, err, s, gpe, fuse));
     }
     for (const auto& [a, b] : deferred) VXG_TRY_S(launch_group(a, b));
     return VXG_OK;

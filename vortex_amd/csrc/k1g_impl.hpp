@@ -289,6 +289,12 @@ __device__ __forceinline__ void gen_dispatch_one(const GenChunk& gc, uint64_t g,
 // -- VarBin dictionaries, RunEnd -- ~80 scalar instructions per wave).
 __device__ __forceinline__ void gen_dispatch(int kind, const GenChunk& gc, uint64_t g, uint8_t* lds, uint32_t doff, bool dl,
                                              uint32_t* err) {
+    // a padded table (launch_k1_jobs: every job as many workgroups as the largest): the
+    // workgroups past a job's own have nothing to do
+    const uint64_t lg = g - gc.d.first_group;
+    const uint64_t own = kind >= 38 ? (gc.re.n_runs + kRunEndRunsPerGroup - 1) / kRunEndRunsPerGroup
+                                    : (gc.d.n_blocks + gc.bpw - 1) / (gc.bpw ? gc.bpw : 1);
+    if (lg >= own) return;
 #define VXG_K1G_CASE(K) \
     case K: gen_dispatch_one<K>(gc, g, lds, doff, dl, err); break;
     switch (kind) {
