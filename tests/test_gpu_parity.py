@@ -1089,6 +1089,35 @@ def test_runend_run_length_regimes(ctx, mean_run):
     assert ei.value.kind == "InvalidArgument"
 
 
+@pytest.mark.parametrize("case", ["max_direct", "one_long", "windows"])
+def test_runend_short_runs_window_shapes(ctx, case):
+    """K8r (runend_runs.hpp) at run-length shapes its 4,096-row windows meet: runs of exactly 32
+    rows among short ones, single 33-40-row runs among 1-7-row runs, and 1-15-row runs whose
+    1,024-run workgroups span two or three windows (a run carried across a window edge); plain,
+    FoR-packed values, sliced and chunked.  (Written for round 6's rejected direct head fill,
+    profiles/r06_k8r_direct_fill.md; kept as coverage of the max-scan form.)"""
+    rng = np.random.default_rng({"max_direct": 1, "one_long": 2, "windows": 3}[case])
+    n_runs = 6000
+    if case == "max_direct":
+        lens = np.where(rng.random(n_runs) < 0.3, 32, rng.integers(1, 8, n_runs))
+    elif case == "one_long":
+        lens = rng.integers(1, 8, n_runs)
+        lens[[100, 2500, 5000]] = [33, 40, 33]
+    else:
+        lens = rng.integers(1, 16, n_runs)
+    vals = np.repeat(rng.integers(-10**12, 10**12, n_runs).astype(np.int64), lens)
+    for compress in (False, True):
+        arr = E.encode_runend(vals, compress_values=compress)
+        assert_primitive_parity(arr, ctx, vals)
+    ends, rv = E.runend_encode(vals)
+    start, length = 37, vals.size - 50
+    sb = int(np.searchsorted(ends, start, side="right"))
+    sl = A.run_end(A.primitive(ends[sb:]), A.primitive(rv[sb:]), length=length, offset=start)
+    assert_primitive_parity(sl, ctx, vals[start:start + length])
+    ch = A.chunked([E.encode_runend(vals[:9000], compress_values=True), sl])
+    assert_primitive_parity(ch, ctx, np.concatenate([vals[:9000], vals[start:start + length]]))
+
+
 def _slice_bitpacked(bp, start, length):
     """BitPackedArray::slice (bitpacking/compute/slice.rs): whole blocks from the one holding
     `start`, offset = start % 1024."""
