@@ -282,13 +282,16 @@ vxg_status launch_k1_jobs(std::vector<K1Job>& jobs, uint32_t* err, hipStream_t s
         // column): one FastLanes block of codes per workgroup (gen_vb_bpw)
         const bool vb_alone = n_runs == 0 && !(fuse && fuse->valid) &&
                               std::all_of(gen.begin(), gen.end(), [](const K1Job* jp) { return jp->vb; });
+        uint64_t gen_blocks = 0;
+        for (const K1Job* jp : gen) gen_blocks += jp->d.n_blocks;
+        const uint32_t bpw_cap = gen_bpw_cap(gen_blocks);
         for (size_t k = 0; k < gen.size(); k++) {
             const K1Job& jb = *gen[k];
             GenChunk& g = host[k];
             g.d = jb.d;
             g.kind = uint32_t(gen_kind(jb.T, int(jb.epi), jb.vw, jb.vb));
             g.W = uint32_t(jb.W);
-            g.bpw = jb.vb ? gen_vb_bpw(jb.T, jb.W, vb_alone) : gen_bpw(jb.T, jb.W);
+            g.bpw = jb.vb ? gen_vb_bpw(jb.T, jb.W, vb_alone, bpw_cap) : gen_bpw(jb.T, jb.W, bpw_cap);
             g.d.first_group = groups;
             groups += (jb.d.n_blocks + g.bpw - 1) / g.bpw;
             packed_bytes = std::max(packed_bytes, g.bpw * 128u * uint32_t(jb.W));

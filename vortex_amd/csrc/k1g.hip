@@ -54,21 +54,31 @@ int gen_kind(int T, int epi, int vw, bool varbin_dict) {
     return -1;
 }
 
-// Blocks per K1g workgroup: as many as kGenPackedLds of packed words hold, at most
-// VXG_K1G_BPW (default 4; read once).
-static uint32_t gen_bpw_max() {
-    static const uint32_t v = [] {
+// Blocks per K1g workgroup: as many as kGenPackedLds of packed words hold, at most the launch's
+// cap (gen_bpw_cap; VXG_K1G_BPW, read once, fixes it for every launch).
+static long gen_bpw_env() {
+    static const long v = [] {
         const char* e = std::getenv("VXG_K1G_BPW");
-        const long x = e ? std::strtol(e, nullptr, 10) : 4;
-        return uint32_t(x >= 1 && x <= 32 ? x : 4);
+        const long x = e ? std::strtol(e, nullptr, 10) : 0;
+        return x >= 1 && x <= 32 ? x : 0L;
     }();
     return v;
 }
 
-uint32_t gen_bpw(int T, int W) {
+// 8 blocks per workgroup halve the per-workgroup prologue (job lookup, descriptor, dictionary
+// staging) per block, but only pay while the grid still has work for every CU's slots: C5 at one
+// GPU (the fused launch's ~29 K blocks) 0.2672 -> 0.2591 ms with 8, its 8-GPU shard (~3.7 K
+// blocks) 0.0387 -> 0.0406 (session r06v, profiles/r06_c5_plan.md).
+constexpr uint64_t kGenWideMinGroups = 2048;
+uint32_t gen_bpw_cap(uint64_t blocks) {
+    if (const long v = gen_bpw_env()) return uint32_t(v);
+    return blocks / 8 >= kGenWideMinGroups ? 8u : 4u;
+}
+
+uint32_t gen_bpw(int T, int W, uint32_t cap) {
     (void)T;
     const uint32_t per = 128u * uint32_t(W > 0 ? W : 1);
-    const uint32_t b = kGenPackedLds / per, m = gen_bpw_max();
+    const uint32_t b = kGenPackedLds / per, m = cap ? cap : (gen_bpw_env() ? uint32_t(gen_bpw_env()) : 4u);
     return b > m ? m : (b < 1 ? 1 : b);
 }
 
@@ -79,12 +89,12 @@ uint32_t gen_bpw(int T, int W) {
 // r06j; pure 96 MB view stores: 15.4 / 17.1 us for 1,024 / 4,096-row workgroups,
 // profiles/r04_ubench_views.txt) -- while beside FSST tiles in the fused launch 4 blocks stay
 // best (C5 1 GPU 0.272-0.280 ms with 4 and 2, 0.305 with 1; session r06k).
-uint32_t gen_vb_bpw(int T, int W, bool alone) {
+uint32_t gen_vb_bpw(int T, int W, bool alone, uint32_t cap) {
     static const long v = [] {
         const char* e = std::getenv("VXG_K1G_VB_BPW");
         return e ? std::strtol(e, nullptr, 10) : 0L;
     }();
-    const uint32_t b = gen_bpw(T, W);
+    const uint32_t b = gen_bpw(T, W, cap);
     const uint32_t want = v >= 1 ? uint32_t(v) : (alone ? 1u : b);
     return want < b ? want : b;
 }

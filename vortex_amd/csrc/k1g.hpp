@@ -52,10 +52,13 @@ __host__ __device__ constexpr uint32_t gen_vb_stage_bytes(uint64_t dict_len, uin
     return uint32_t(16 * dict_len + (gen_vb_heap_lds(dict_len, bytes) ? ((bytes + 15) & ~15ull) : 0));
 }
 // Blocks per workgroup of a job (its packed words staged in <= 16 KiB of LDS).
-uint32_t gen_bpw(int T, int W);
+uint32_t gen_bpw(int T, int W, uint32_t cap = 0);
+// The blocks-per-workgroup cap of a K1g launch over `blocks` FastLanes blocks (VXG_K1G_BPW if
+// set, else 8 when the launch keeps >= kGenWideMinGroups workgroups at 8, else 4)
+uint32_t gen_bpw_cap(uint64_t blocks);
 // ... of a Dict-over-VarBin job: 1 in a launch of such jobs alone, else gen_bpw's
 // (VXG_K1G_VB_BPW overrides both).
-uint32_t gen_vb_bpw(int T, int W, bool alone);
+uint32_t gen_vb_bpw(int T, int W, bool alone, uint32_t cap = 0);
 // LDS a short-run RunEnd expansion of `value_width`-byte values needs.
 uint32_t gen_runs_lds_bytes(int value_width);
 // One launch over a device table of n jobs (first_group filled in).  `dict_lds` = every Dict
