@@ -94,7 +94,8 @@ uint32_t gen_vb_bpw(int T, int W, bool alone, uint32_t cap) {
         const char* e = std::getenv("VXG_K1G_VB_BPW");
         return e ? std::strtol(e, nullptr, 10) : 0L;
     }();
-    const uint32_t b = gen_bpw(T, W, cap);
+    // (VXG_K1G_VB_BPW set: that many blocks, above the launch's cap too, as LDS allows)
+    const uint32_t b = gen_bpw(T, W, v >= 1 && uint32_t(v) > cap ? uint32_t(v) : cap);
     const uint32_t want = v >= 1 ? uint32_t(v) : (alone ? 1u : b);
     return want < b ? want : b;
 }
